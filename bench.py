@@ -1,0 +1,225 @@
+"""Benchmark: client leases apportioned per second (whole node) + % of HBM peak.
+
+One step = one apportionment tick over every lease of the rank's store: the
+device-resident snapshot is decided (Clean, learning mode, the resource's
+algorithm) and written back (DM_WRITEBACK), inputs already resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c1ps|c2|c3]
+
+For N > 1 it runs under torch.distributed.run, one rank per GPU; resources are
+sharded by id (each rank owns its own shard of the workload: weak scaling, no
+data-path collective).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_COPY_CEIL_GBS = 6290.0  # measured float4 copy ceiling (same table)
+METRIC = "client leases apportioned/sec (whole node) + % HBM peak, FairShare, 1-8 GPU"
+
+WORKLOADS = {
+    "c1": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), FairShare, uniform wants",
+    "c1ps": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), ProportionalShare",
+    "c2": "C2 (BASELINE configs[2]): 1M resources, Zipf 1..1M clients (13,970,034 leases), mixed kinds, 5% learning",
+    "c3": "C3 shape on one GPU (north-star target): 100,000 resources x 1,000 clients (100M leases), FairShare",
+}
+
+
+def make_workload(name: str, rank: int):
+    from doorman_amd import workloads as W
+    if name == "c1":
+        return W.c1(seed=1 + 1000 * rank, kind=W.FAIR_SHARE)
+    if name == "c1ps":
+        return W.c1(seed=1 + 1000 * rank, kind=W.PROPORTIONAL_SHARE)
+    if name == "c2":
+        return W.c2(seed=2 + 1000 * rank)
+    if name == "c3":
+        return W.uniform(100_000, 1_000, kind=W.FAIR_SHARE, seed=3 + 1000 * rank)
+    raise SystemExit(f"unknown workload {name}")
+
+
+def algorithmic_bytes(n_leases: int, n_resources: int) -> int:
+    # per lease read wants/has/subclients/expiry, write gets/expiry (48 B);
+    # per resource config + offsets + outputs (64 B).  Re-reads are not counted.
+    return 48 * n_leases + 64 * n_resources
+
+
+def kernel_units(eng, snap):
+    """(leases, resources) each kernel class of the plan processes per launch."""
+    so = snap["seg_off"]
+    sizes = np.diff(so)
+    units = {}
+    edges = [("wave64x1", 17, 64), ("block256x1", 65, 256), ("block256x2", 257, 512), ("block256x4", 513, 1024),
+             ("block256x8", 1025, 2048), ("block256x16", 2049, 4096)]
+    small = sizes <= 16
+    units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
+    for name, lo, hi in edges:
+        m = (sizes >= lo) & (sizes <= hi)
+        units[name] = (int(sizes[m].sum()), int(m.sum()))
+    big = sizes > 4096
+    for name in ("large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
+        units[name] = (int(sizes[big].sum()), int(big.sum()))
+    return units
+
+
+def cpu_baseline(snap, now_ns, budget_s=12.0):
+    """Reference algorithm restated in C (oracle, literal per-request Resource.Decide on a
+    private copy of the store, single thread), timed on a bounded sample of this workload."""
+    from oracle import oracle as O
+    so = snap["seg_off"]
+    sizes = np.diff(so)
+    order = np.argsort(-sizes, kind="stable")
+    # sample whole resources from the middle of the size distribution up to the budget
+    rng = np.random.default_rng(0)
+    cand = rng.permutation(np.flatnonzero(sizes > 0))
+    gets = np.empty(len(snap["wants"]))
+    done_rows, t_total, used = 0, 0.0, []
+    for r in cand:
+        n = int(sizes[r])
+        lo, hi = int(so[r]), int(so[r + 1])
+        if n > 4000:  # O(n^2) per resource: take a slice of clients of the big resources
+            hi = lo + 4000
+        t0 = time.perf_counter()
+        done_rows += O.apportion_literal_rows(snap, int(r), lo, hi, now_ns, gets)
+        t_total += time.perf_counter() - t0
+        used.append(int(r))
+        if t_total > budget_s:
+            break
+    del order
+    return {
+        "value": done_rows / t_total if t_total > 0 else None,
+        "unit": "leases/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done_rows} leases of {len(used)} resources of the same workload, each decided by the literal "
+                  f"C restatement of Resource.Decide (go/server/doorman/resource.go:100-113) on a private store copy "
+                  f"(O(n) per request as in the reference), single thread, {t_total:.1f} s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch  # loaded first: libdoorman_hip then binds to torch's HIP runtime
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from doorman_amd import workloads as W
+    from doorman_amd.engine import Engine
+
+    snap = make_workload(args.workload, rank)
+    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
+    eng = Engine(local_rank)
+    eng.load(snap)
+    now = W.NOW_NS
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.apportion(now, writeback=True, asynchronous=True)
+    eng.sync()
+    eng.set_profiling(True)
+    eng.reset_kernel_times()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.apportion(now, writeback=True, asynchronous=True)
+    eng.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ktimes = eng.kernel_times()
+    eng.set_profiling(False)
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    n = torch.tensor([N], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    t_max, n_total = float(t.item()), float(n.item())
+
+    # dominant kernel: largest share of in-stream time
+    units = kernel_units(eng, snap)
+    dom = max(ktimes.items(), key=lambda kv: kv[1][1]) if ktimes else None
+    roofline = None
+    if dom:
+        name, (launches, total_ms) = dom
+        avg_s = total_ms / launches / 1e3
+        leases_k, res_k = units.get(name, (N, R))
+        alg = algorithmic_bytes(leases_k, res_k)
+        achieved = alg / avg_s / 1e9
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get(name, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2),
+                    "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(snap, now, args.cpu_budget)
+
+    if rank == 0:
+        tick_bytes = algorithmic_bytes(N, R)
+        line = {
+            "metric": METRIC,
+            "value": n_total * args.steps / t_max,
+            "unit": "leases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded numpy generators of SURVEY.md §8d)",
+            "config": {"workload": WORKLOADS[args.workload], "resources_per_gpu": R, "leases_per_gpu": N,
+                       "parallelism": f"resource-sharded x{world} (no data-path collective)",
+                       "writeback": True},
+            "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in ktimes.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,115 @@
+"""ctypes binding of libdoorman_hip.so (the C-ABI in include/doorman_hip.h).
+
+No fallback: if the HIP library is missing or no GPU is visible, calls raise.
+Import torch BEFORE this module when both are used in one process, so the
+library binds to the HIP runtime torch already loaded (same soname).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdoorman_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "doorman_hip.h")
+
+DM_OK, DM_E_INVAL, DM_E_HIP, DM_E_STATE, DM_E_KIND, DM_E_RANGE, DM_E_ARGUMENT = 0, -1, -2, -3, -4, -5, -6
+DM_WRITEBACK, DM_AGG_RECOMPUTE, DM_ASYNC = 1, 2, 4
+
+
+class DmError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"doorman-hip error {code}: {msg}")
+        self.code = code
+
+
+class Snapshot(ctypes.Structure):
+    _fields_ = [
+        ("n_resources", ctypes.c_int64),
+        ("n_leases", ctypes.c_int64),
+        ("seg_off", ctypes.c_void_p),
+        ("wants", ctypes.c_void_p),
+        ("has", ctypes.c_void_p),
+        ("subclients", ctypes.c_void_p),
+        ("expiry_ns", ctypes.c_void_p),
+        ("agg_count", ctypes.c_void_p),
+        ("agg_sum_has", ctypes.c_void_p),
+        ("agg_sum_wants", ctypes.c_void_p),
+    ]
+
+
+class ResourceCfg(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_void_p),
+        ("capacity", ctypes.c_void_p),
+        ("lease_length_s", ctypes.c_void_p),
+        ("refresh_interval_s", ctypes.c_void_p),
+        ("learning_end_ns", ctypes.c_void_p),
+        ("parent_expiry_ns", ctypes.c_void_p),
+        ("safe_capacity", ctypes.c_void_p),
+    ]
+
+
+class KernelTime(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
+
+
+_lib = None
+
+_SIGS = {
+    "dm_version": (ctypes.c_char_p, []),
+    "dm_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "dm_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "dm_destroy": (None, [ctypes.c_void_p]),
+    "dm_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "dm_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "dm_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "dm_store_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Snapshot)]),
+    "dm_config_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ResourceCfg)]),
+    "dm_store_upsert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5),
+    "dm_store_release": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "dm_read_store": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "dm_apportion": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32]),
+    "dm_read_leases": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
+    "dm_read_leases_proto": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 3),
+    "dm_read_resources": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 4),
+    "dm_aggregate_bands": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    "dm_publish_totals": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
+    "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),
+    "dm_plan_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
+}
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(dm_\w+)\s*\(", text, flags=re.M)))
+
+
+def lib():
+    """Load the HIP library (raises if it was not built: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                               "(make -C doorman_amd/csrc); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, ctx=None) -> int:
+    if rc < 0:
+        msg = lib().dm_last_error(ctx)
+        raise DmError(rc, msg.decode() if msg else "")
+    return rc

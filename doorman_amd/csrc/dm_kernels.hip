@@ -1,0 +1,1045 @@
+// dm_kernels.hip — gfx950 kernels for one apportionment tick.
+//
+// Every lease row is decided against the same frozen store (include/doorman_hip.h).
+// Per resource the reference's per-request loops (go/server/doorman/algorithm.go)
+// collapse to segmented reductions:
+//   Clean          store.go:169-181   pass A: expired-row sums (parity) or live sums
+//   ProportionalShare algorithm.go:213-293  pass B: extraCapacity / extraNeed, then map
+//   FairShare      algorithm.go:95-206    pass B: extra / wantExtra (round 1),
+//                                         pass C: extraExtra / wantExtraExtra at T (round 2), then map
+//   NoAlgorithm / Static / Learn  algorithm.go:66-84,297-302  map only
+// The path is HBM-bound (48 B per lease, ~15 flops): no MFMA.  Rows are read once
+// from HBM into VGPRs and every pass runs from registers; the large-resource path
+// re-reads from L2 / Infinity Cache.
+//
+// Float semantics follow Go on amd64: binary64, no FMA contraction (built with
+// -ffp-contract=off), minF = `l > r ? r : l`, IEEE division by zero.
+#include <hip/hip_runtime.h>
+
+#include "dm_device.h"
+
+namespace dm {
+
+// --------------------------------------------------------------------------
+// helpers
+// --------------------------------------------------------------------------
+__device__ __forceinline__ double minF(double l, double r) { return l > r ? r : l; }  // algorithm.go:50-55
+
+struct Res {
+  int32_t kind;
+  int32_t learning;
+  double C;        // Resource.capacity() (resource.go:62-70)
+  double cap_cfg;  // config capacity (SetSafeCapacity, resource.go:92)
+  double safe;
+  int64_t exp_out; // now + lease_length (store.go:161)
+};
+
+__device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
+  Res r;
+  r.kind = p.kind[seg];
+  r.learning = p.learning_end[seg] > p.now;  // resource.go:108 learningModeEndTime.After(now)
+  r.cap_cfg = p.capacity[seg];
+  r.C = (p.parent_expiry[seg] < p.now) ? 0.0 : r.cap_cfg;  // expiryTime.Before(now)
+  r.safe = p.safe_cap[seg];
+  r.exp_out = p.now + p.lease_len_s[seg] * kNs;
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_xor_any(const T& v, int m) {
+  static_assert(sizeof(T) % 4 == 0, "4-byte granular");
+  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
+  __builtin_memcpy(src, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __shfl_xor(src[i], m, 64);
+  T r;
+  __builtin_memcpy(&r, dst, sizeof(T));
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_any(const T& v, int lane) {
+  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
+  __builtin_memcpy(src, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __shfl(src[i], lane, 64);
+  T r;
+  __builtin_memcpy(&r, dst, sizeof(T));
+  return r;
+}
+
+// Group reduction (G = 64: one wave; G = 256: four waves through LDS).  Butterfly
+// within the wave, then every thread combines the wave partials in the same
+// fixed order, so all threads (and all blocks reducing the same inputs) agree
+// bit for bit.
+template <int G, typename T, typename Op>
+__device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = op(v, shfl_xor_any(v, o));
+  v = shfl_any(v, 0);
+  if constexpr (G == 64) {
+    (void)lds;
+    return v;
+  } else {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) lds[w] = v;
+    __syncthreads();
+    T r = lds[0];
+#pragma unroll
+    for (int i = 1; i < G / 64; ++i) r = op(r, lds[i]);
+    __syncthreads();
+    return r;
+  }
+}
+
+struct AggA {
+  long long cnt;
+  double h;
+  double w;
+  long long smin;
+  long long smax;
+  int nan;
+  int pad;
+};
+struct OpA {
+  __device__ AggA operator()(const AggA& a, const AggA& b) const {
+    AggA r;
+    r.cnt = a.cnt + b.cnt;
+    r.h = a.h + b.h;
+    r.w = a.w + b.w;
+    r.smin = a.smin < b.smin ? a.smin : b.smin;
+    r.smax = a.smax > b.smax ? a.smax : b.smax;
+    r.nan = a.nan | b.nan;
+    r.pad = 0;
+    return r;
+  }
+};
+__device__ __forceinline__ AggA zeroA() {
+  AggA a;
+  a.cnt = 0;
+  a.h = 0.0;
+  a.w = 0.0;
+  a.smin = INT64_MAX;
+  a.smax = INT64_MIN;
+  a.nan = 0;
+  a.pad = 0;
+  return a;
+}
+
+struct AggB {
+  double x;    // FS: extra (E)          PS: extraCapacity
+  double y;    //                        PS: extraNeed
+  long long i; // FS: wantExtra (W)
+};
+struct OpB {
+  __device__ AggB operator()(const AggB& a, const AggB& b) const {
+    AggB r;
+    r.x = a.x + b.x;
+    r.y = a.y + b.y;
+    r.i = a.i + b.i;
+    return r;
+  }
+};
+
+struct AggC {
+  double ee;      // extraExtra
+  long long sgt;  // sum of subclients of wantExtraClients above T
+};
+struct OpC {
+  __device__ AggC operator()(const AggC& a, const AggC& b) const {
+    AggC r;
+    r.ee = a.ee + b.ee;
+    r.sgt = a.sgt + b.sgt;
+    return r;
+  }
+};
+
+struct TMin {
+  double t;
+  int found;
+  int pad;
+};
+struct OpTMin {
+  __device__ TMin operator()(const TMin& a, const TMin& b) const {
+    if (!b.found) return a;
+    if (!a.found) return b;
+    return b.t < a.t ? b : a;
+  }
+};
+
+struct SumD {
+  double v;
+};
+struct OpSumD {
+  __device__ SumD operator()(const SumD& a, const SumD& b) const { return SumD{a.v + b.v}; }
+};
+
+template <int G>
+struct Lds {
+  AggA a[G / 64];
+  AggB b[G / 64];
+  AggC c[G / 64];
+  TMin t[G / 64];
+  SumD d[G / 64];
+};
+
+// Cleaned store sums from pass A (store.go:169-181 applied to the snapshot).
+struct Clean {
+  long long count;
+  double sum_has;
+  double sum_wants;
+};
+__device__ __forceinline__ Clean clean_from(const DevParams& p, int seg, const AggA& a) {
+  Clean c;
+  if (p.recompute) {
+    c.count = a.cnt;
+    c.sum_has = a.h;
+    c.sum_wants = a.w;
+  } else {  // running sums minus the leases Clean releases
+    c.count = p.agg_count[seg] - a.cnt;
+    c.sum_has = p.agg_sum_has[seg] - a.h;
+    c.sum_wants = p.agg_sum_wants[seg] - a.w;
+  }
+  return c;
+}
+
+__device__ __forceinline__ void write_resource(const DevParams& p, int seg, const Res& rs, const Clean& c,
+                                               double delta) {
+  p.res_count[seg] = c.count;
+  p.res_sum_wants[seg] = c.sum_wants;
+  p.res_sum_has[seg] = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
+  p.res_safe[seg] = __builtin_isnan(rs.safe) ? rs.cap_cfg / (double)c.count : rs.safe;  // resource.go:91-95
+}
+
+// FairShare per-row stage (algorithm.go:115-181).  Returns true when the lease is
+// decided here (gets in *g); otherwise fills T = deservedExtra + deservedShare.
+__device__ __forceinline__ bool fs_stage01(double w, double h, long long s, double C, double sum_has, double eq,
+                                           double E, long long Wc, double* g, double* T) {
+  const double ds = eq * (double)s;              // :126 deservedShare
+  const double avail = C - sum_has + h;          // :120 available
+  if (w <= ds) {                                 // :131
+    *g = minF(w, avail);
+    return true;
+  }
+  const long long Wi = Wc + s - (w > ds ? s : 0);  // :148,168 wantExtra (self counted once)
+  const double dE = (E / (double)Wi) * (double)s;  // :175 deservedExtra
+  if (w < ds + dE) {                               // :179
+    *g = minF(w, avail);
+    return true;
+  }
+  *T = dE + ds;
+  return false;
+}
+
+// FairShare round 2 result for a row given the resource's sums at its T (:189-204).
+__device__ __forceinline__ double fs_stage2(double w, double h, long long s, double C, double sum_has, double eq,
+                                            double E, long long Wc, double T, const AggC& c) {
+  const double ds = eq * (double)s;
+  const double avail = C - sum_has + h;
+  const long long Wi = Wc + s - (w > ds ? s : 0);
+  const double dE = (E / (double)Wi) * (double)s;
+  const long long wee = s + c.sgt - ((w > ds && w > T) ? s : 0);  // :189,200 (self excluded, :193)
+  const double dEE = (c.ee / (double)wee) * (double)s;             // :203
+  return minF(ds + dE + dEE, avail);                               // :204
+}
+
+// --------------------------------------------------------------------------
+// Resource-per-group kernel: G threads (a wave or a 256-thread workgroup) own
+// one resource of up to G*R rows; rows live in VGPRs across all passes.
+// --------------------------------------------------------------------------
+template <int G, int R>
+__device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t, Lds<G>& lds) {
+  const int64_t lo = p.seg_off[seg];
+  const int n = (int)(p.seg_off[seg + 1] - lo);
+  double w[R], h[R];
+  long long s[R];
+  unsigned valid = 0, live = 0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = k * G + t;
+    w[k] = 0.0;
+    h[k] = 0.0;
+    s[k] = 0;
+    if (i < n) {
+      const int64_t row = lo + i;
+      w[k] = p.wants[row];
+      h[k] = p.has[row];
+      s[k] = p.sub[row];
+      const int64_t e = p.expiry[row];
+      valid |= 1u << k;
+      if (!(p.now > e)) live |= 1u << k;  // store.go:174 when.After(expiry)
+    }
+  }
+  const Res rs = load_res(p, seg);
+
+  // ---- pass A: Clean ----
+  AggA a = zeroA();
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    if (!(valid >> k & 1)) continue;
+    const bool lv = live >> k & 1;
+    if (p.recompute ? lv : !lv) {
+      a.cnt += s[k];
+      a.h += h[k];
+      a.w += w[k];
+    }
+    if (lv) {
+      a.smin = s[k] < a.smin ? s[k] : a.smin;
+      a.smax = s[k] > a.smax ? s[k] : a.smax;
+      a.nan |= __builtin_isnan(w[k]) ? 1 : 0;
+    }
+  }
+  a = group_reduce<G>(a, OpA(), lds.a);
+  const Clean cl = clean_from(p, seg, a);
+  const double C = rs.C;
+
+  double g[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) g[k] = 0.0;
+
+  if (rs.learning) {  // Learn (algorithm.go:297-302)
+#pragma unroll
+    for (int k = 0; k < R; ++k) g[k] = h[k];
+  } else if (rs.kind == 0) {  // NoAlgorithm
+#pragma unroll
+    for (int k = 0; k < R; ++k) g[k] = w[k];
+  } else if (rs.kind == 1) {  // Static
+#pragma unroll
+    for (int k = 0; k < R; ++k) g[k] = minF(C, w[k]);
+  } else if (rs.kind == 2) {  // ProportionalShare
+    const double eq = C / (double)cl.count;  // :229
+    AggB b{0.0, 0.0, 0};
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (!(live >> k & 1)) continue;
+      const double e = eq * (double)s[k];  // :273
+      if (w[k] < e)
+        b.x += e - w[k];  // :275
+      else
+        b.y += w[k] - e;  // :277
+    }
+    b = group_reduce<G>(b, OpB(), lds.b);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const double epc = eq * (double)s[k];           // :233
+      const double unused = C - cl.sum_has + h[k];    // :239
+      if (cl.sum_wants <= C || w[k] <= epc)           // :245
+        g[k] = minF(w[k], unused);
+      else
+        g[k] = minF(epc + (w[k] - epc) * (b.x / b.y), unused);  // :283,290
+    }
+  } else {  // FairShare
+    const double eq = C / (double)cl.count;  // :123
+    AggB b{0.0, 0.0, 0};
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (!(live >> k & 1)) continue;
+      const double d = (double)s[k] * eq;  // :160
+      if (w[k] < d)
+        b.x += d - w[k];  // :164
+      else if (w[k] > d)
+        b.i += s[k];  // :168
+    }
+    b = group_reduce<G>(b, OpB(), lds.b);
+    unsigned need2 = 0;
+    double T[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      T[k] = 0.0;
+      if (!(live >> k & 1)) continue;
+      if (!fs_stage01(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, &g[k], &T[k])) need2 |= 1u << k;
+    }
+    if (a.smin == a.smax && !a.nan) {
+      // uniform subclients: one threshold T for the whole resource
+      const double s0 = (double)a.smin;
+      const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
+      AggC c{0.0, 0};
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if (!(live >> k & 1)) continue;
+        if (!(w[k] > (double)s[k] * eq)) continue;  // j in wantExtraClients (:165-169)
+        if (w[k] < Tu)
+          c.ee += Tu - w[k];  // :197-198
+        else if (w[k] > Tu)
+          c.sgt += s[k];  // :199-200
+      }
+      c = group_reduce<G>(c, OpC(), lds.c);
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if (need2 >> k & 1) g[k] = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, T[k], c);
+    } else {
+      // heterogeneous subclients (GetServerCapacity, server.go:850-879) or NaN wants:
+      // one round-2 reduction per distinct threshold, smallest first.
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if ((need2 >> k & 1) && __builtin_isnan(T[k])) {
+          const AggC none{0.0, 0};
+          g[k] = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, T[k], none);
+          need2 &= ~(1u << k);
+        }
+      }
+      for (;;) {
+        TMin tm{0.0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+          if ((need2 >> k & 1) && (!tm.found || T[k] < tm.t)) tm = TMin{T[k], 1, 0};
+        tm = group_reduce<G>(tm, OpTMin(), lds.t);
+        if (!tm.found) break;
+        const double Ts = tm.t;
+        AggC c{0.0, 0};
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          if (!(live >> k & 1)) continue;
+          if (!(w[k] > (double)s[k] * eq)) continue;
+          if (w[k] < Ts)
+            c.ee += Ts - w[k];
+          else if (w[k] > Ts)
+            c.sgt += s[k];
+        }
+        c = group_reduce<G>(c, OpC(), lds.c);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          if ((need2 >> k & 1) && T[k] == Ts) {
+            g[k] = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, T[k], c);
+            need2 &= ~(1u << k);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- map: write the leases (store.go:153-167 Assign; released rows get none) ----
+  SumD delta{0.0};
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    if (!(valid >> k & 1)) continue;
+    const int64_t row = lo + k * G + t;
+    if (live >> k & 1) {
+      p.out_gets[row] = g[k];
+      p.out_expiry[row] = rs.exp_out;
+      delta.v += g[k] - h[k];
+    } else {
+      p.out_gets[row] = 0.0;
+      p.out_expiry[row] = kReleased;
+      if (p.out_wants) {
+        p.out_wants[row] = 0.0;
+        p.out_sub[row] = 0;
+      }
+    }
+  }
+  delta = group_reduce<G>(delta, OpSumD(), lds.d);
+  if (t == 0) write_resource(p, seg, rs, cl, delta.v);
+}
+
+// 256-thread workgroup per resource.
+template <int R>
+__global__ __launch_bounds__(256) void k_block(DevParams p, const int32_t* __restrict__ segs, int nsegs) {
+  __shared__ Lds<256> lds;
+  if ((int)blockIdx.x >= nsegs) return;
+  group_segment<256, R>(p, segs[blockIdx.x], threadIdx.x, lds);
+}
+
+// One wave per resource (n <= 64), four independent waves per workgroup.
+__global__ __launch_bounds__(256) void k_wave(DevParams p, const int32_t* __restrict__ segs, int nsegs) {
+  Lds<64> lds;  // unused by wave reductions
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nsegs) return;
+  group_segment<64, 1>(p, segs[i], threadIdx.x & 63, lds);
+}
+
+// --------------------------------------------------------------------------
+// Wave-packed small resources (n <= kSmallMax): one wave covers a run of whole
+// resources; every lane evaluates its own client literally, looping over its
+// resource's rows in row order (shuffles).  Sums are taken in the same order as
+// the oracle, so this path is bit-exact against it.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restrict__ packs, int npacks) {
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wv >= npacks) return;
+  const int lane = threadIdx.x & 63;
+  const Pack pk = packs[wv];
+  const int64_t offk = lane <= pk.nseg ? p.seg_off[pk.first_seg + lane] : INT64_MAX;
+  const int64_t row = pk.row0 + lane;
+  const bool valid = lane < pk.nrows;
+  // resource of this row: last k < nseg with seg_off[first+k] <= row
+  int k = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) {
+    const int c = k + step;
+    const long long oc = __shfl((long long)offk, c < 64 ? c : 63, 64);
+    if (c < pk.nseg && oc <= row) k = c;
+  }
+  const long long seg_lo = __shfl((long long)offk, k, 64);
+  const long long seg_hi = __shfl((long long)offk, k + 1 < 64 ? k + 1 : 63, 64);
+  const int lo = valid ? (int)(seg_lo - pk.row0) : 0;
+  const int hi = valid ? (int)(seg_hi - pk.row0) : 0;
+  const int seg = pk.first_seg + k;
+  const int maxlen = pk.maxlen;
+
+  double w = 0.0, h = 0.0;
+  long long s = 0;
+  int lv = 0;
+  if (valid) {
+    w = p.wants[row];
+    h = p.has[row];
+    s = p.sub[row];
+    lv = !(p.now > p.expiry[row]) ? 1 : 0;
+  }
+  const Res rs = load_res(p, seg);
+
+  // Clean, in row order (store.go:169-181)
+  long long count = 0;
+  double sh = 0.0, sw = 0.0;
+  if (p.recompute) {
+    for (int q = 0; q < maxlen; ++q) {
+      const int j = lo + q;
+      const double hj = __shfl(h, j & 63, 64), wj = __shfl(w, j & 63, 64);
+      const long long sj = __shfl(s, j & 63, 64);
+      if (j < hi) {
+        sh += hj - 0.0;
+        sw += wj - 0.0;
+        count += sj;
+      }
+    }
+  } else {
+    count = p.agg_count[seg];
+    sh = p.agg_sum_has[seg];
+    sw = p.agg_sum_wants[seg];
+  }
+  for (int q = 0; q < maxlen; ++q) {
+    const int j = lo + q;
+    const double hj = __shfl(h, j & 63, 64), wj = __shfl(w, j & 63, 64);
+    const long long sj = __shfl(s, j & 63, 64);
+    const int lj = __shfl(lv, j & 63, 64);
+    if (j < hi && !lj) {
+      sw -= wj;
+      sh -= hj;
+      count -= sj;
+    }
+  }
+
+  const double C = rs.C;
+  const double eq = C / (double)count;
+  double g = 0.0;
+  // every lane runs every loop (shuffles need the full wave); results are
+  // selected per lane afterwards.
+  double x = 0.0, y = 0.0;
+  long long wi = 0;
+  const bool ps = !rs.learning && rs.kind == 2, fs = !rs.learning && rs.kind == 3;
+  for (int q = 0; q < maxlen; ++q) {
+    const int j = lo + q;
+    const double wj = __shfl(w, j & 63, 64);
+    const long long sj = __shfl(s, j & 63, 64);
+    const int lj = __shfl(lv, j & 63, 64);
+    if (j < hi && lj) {
+      if (ps) {
+        const double e = eq * (double)sj;
+        if (wj < e)
+          x += e - wj;
+        else
+          y += wj - e;
+      } else if (fs) {
+        const double d = (double)sj * eq;
+        if (wj < d)
+          x += d - wj;
+        else if (wj > d)
+          wi += sj;
+      }
+    }
+  }
+  double T = 0.0;
+  bool need2 = false;
+  if (rs.learning) {
+    g = h;
+  } else if (rs.kind == 0) {
+    g = w;
+  } else if (rs.kind == 1) {
+    g = minF(C, w);
+  } else if (rs.kind == 2) {
+    const double epc = eq * (double)s;
+    const double unused = C - sh + h;
+    g = (sw <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (x / y), unused);
+  } else {
+    need2 = !fs_stage01(w, h, s, C, sh, eq, x, wi, &g, &T);
+  }
+  const int any2 = __any(need2 && valid && lv);
+  if (any2) {
+    AggC c{0.0, 0};
+    for (int q = 0; q < maxlen; ++q) {
+      const int j = lo + q;
+      const double wj = __shfl(w, j & 63, 64);
+      const long long sj = __shfl(s, j & 63, 64);
+      const int lj = __shfl(lv, j & 63, 64);
+      if (j < hi && lj && wj > (double)sj * eq) {
+        if (wj < T)
+          c.ee += T - wj;
+        else if (wj > T)
+          c.sgt += sj;
+      }
+    }
+    if (need2) g = fs_stage2(w, h, s, C, sh, eq, x, wi, T, c);
+  }
+  if (valid) {
+    if (lv) {
+      p.out_gets[row] = g;
+      p.out_expiry[row] = rs.exp_out;
+    } else {
+      p.out_gets[row] = 0.0;
+      p.out_expiry[row] = kReleased;
+      if (p.out_wants) {
+        p.out_wants[row] = 0.0;
+        p.out_sub[row] = 0;
+      }
+    }
+  }
+  // per-resource results: lane k (< nseg) owns resource first_seg + k
+  const bool owner = lane < pk.nseg;
+  const int olo = (int)(offk - pk.row0);
+  const int ohi = (int)(__shfl((long long)offk, lane + 1 < 64 ? lane + 1 : 63, 64) - pk.row0);
+  long long ocount = __shfl(count, olo & 63, 64);
+  double osh = __shfl(sh, olo & 63, 64), osw = __shfl(sw, olo & 63, 64);
+  const double gl = lv ? g : 0.0;
+  for (int q = 0; q < maxlen; ++q) {
+    const int j = olo + q;
+    const double gj = __shfl(gl, j & 63, 64), hj = __shfl(h, j & 63, 64);
+    const int lj = __shfl(lv, j & 63, 64);
+    if (owner && j < ohi && lj) osh += gj - hj;
+  }
+  if (owner) {
+    const int oseg = pk.first_seg + lane;
+    if (olo == ohi) {  // resource without rows
+      ocount = p.recompute ? 0 : p.agg_count[oseg];
+      osh = p.recompute ? 0.0 : p.agg_sum_has[oseg];
+      osw = p.recompute ? 0.0 : p.agg_sum_wants[oseg];
+    }
+    const Res ors = load_res(p, oseg);
+    Clean oc{ocount, osh, osw};
+    write_resource(p, oseg, ors, oc, 0.0);
+  }
+}
+
+// --------------------------------------------------------------------------
+// Large resources (n > kLargeMin): kChunkRows-row chunks, one workgroup each.
+// Per-resource totals are re-derived in every workgroup from the chunk partials
+// with the same fixed reduction tree, so all chunks of a resource agree exactly.
+// --------------------------------------------------------------------------
+struct SegState {
+  AggA a;
+  Clean cl;
+  Res rs;
+  int general;  // FairShare with heterogeneous subclients / NaN wants -> k_general
+};
+
+template <int G>
+__device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials& P, const LargeSeg& L,
+                                              Lds<G>& lds) {
+  AggA a = zeroA();
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += G) {
+    AggA x;
+    x.cnt = P.a_cnt[c];
+    x.h = P.a_has[c];
+    x.w = P.a_wants[c];
+    x.smin = P.a_smin[c];
+    x.smax = P.a_smax[c];
+    x.nan = P.a_nan[c];
+    x.pad = 0;
+    a = OpA()(a, x);
+  }
+  a = group_reduce<G>(a, OpA(), lds.a);
+  SegState st;
+  st.a = a;
+  st.cl = clean_from(p, L.seg, a);
+  st.rs = load_res(p, L.seg);
+  st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin == a.smax && !a.nan)) ? 1 : 0;
+  return st;
+}
+
+template <int G>
+__device__ __forceinline__ AggB seg_b(const Partials& P, const LargeSeg& L, Lds<G>& lds) {
+  AggB b{0.0, 0.0, 0};
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += G) b = OpB()(b, AggB{P.b_x[c], P.b_y[c], P.b_w[c]});
+  return group_reduce<G>(b, OpB(), lds.b);
+}
+
+template <int G>
+__device__ __forceinline__ AggC seg_c(const Partials& P, const LargeSeg& L, Lds<G>& lds) {
+  AggC c{0.0, 0};
+  for (int q = L.chunk_begin + (int)threadIdx.x; q < L.chunk_end; q += G) c = OpC()(c, AggC{P.c_ee[q], P.c_sgt[q]});
+  return group_reduce<G>(c, OpC(), lds.c);
+}
+
+__global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
+  __shared__ Lds<256> lds;
+  const Chunk ch = chunks[blockIdx.x];
+  AggA a = zeroA();
+  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
+    const int64_t row = ch.row0 + i;
+    const double w = p.wants[row], h = p.has[row];
+    const long long s = p.sub[row];
+    const bool lv = !(p.now > p.expiry[row]);
+    if (p.recompute ? lv : !lv) {
+      a.cnt += s;
+      a.h += h;
+      a.w += w;
+    }
+    if (lv) {
+      a.smin = s < a.smin ? s : a.smin;
+      a.smax = s > a.smax ? s : a.smax;
+      a.nan |= __builtin_isnan(w) ? 1 : 0;
+    }
+  }
+  a = group_reduce<256>(a, OpA(), lds.a);
+  if (threadIdx.x == 0) {
+    const int c = blockIdx.x;
+    P.a_cnt[c] = a.cnt;
+    P.a_has[c] = a.h;
+    P.a_wants[c] = a.w;
+    P.a_smin[c] = a.smin;
+    P.a_smax[c] = a.smax;
+    P.a_nan[c] = a.nan;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __restrict__ chunks,
+                                                 const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ Lds<256> lds;
+  const Chunk ch = chunks[blockIdx.x];
+  const SegState st = seg_state<256>(p, P, ls[ch.lseg], lds);
+  if (st.general || st.rs.learning || st.rs.kind < 2) return;
+  const double eq = st.rs.C / (double)st.cl.count;
+  AggB b{0.0, 0.0, 0};
+  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
+    const int64_t row = ch.row0 + i;
+    if (p.now > p.expiry[row]) continue;
+    const double w = p.wants[row];
+    const long long s = p.sub[row];
+    if (st.rs.kind == 2) {
+      const double e = eq * (double)s;
+      if (w < e)
+        b.x += e - w;
+      else
+        b.y += w - e;
+    } else {
+      const double d = (double)s * eq;
+      if (w < d)
+        b.x += d - w;
+      else if (w > d)
+        b.i += s;
+    }
+  }
+  b = group_reduce<256>(b, OpB(), lds.b);
+  if (threadIdx.x == 0) {
+    P.b_x[blockIdx.x] = b.x;
+    P.b_y[blockIdx.x] = b.y;
+    P.b_w[blockIdx.x] = b.i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __restrict__ chunks,
+                                                 const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ Lds<256> lds;
+  const Chunk ch = chunks[blockIdx.x];
+  const LargeSeg L = ls[ch.lseg];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (st.general || st.rs.learning || st.rs.kind != 3) return;
+  const AggB b = seg_b<256>(P, L, lds);
+  const double eq = st.rs.C / (double)st.cl.count;
+  const double s0 = (double)st.a.smin;
+  const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
+  AggC c{0.0, 0};
+  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
+    const int64_t row = ch.row0 + i;
+    if (p.now > p.expiry[row]) continue;
+    const double w = p.wants[row];
+    const long long s = p.sub[row];
+    if (!(w > (double)s * eq)) continue;
+    if (w < Tu)
+      c.ee += Tu - w;
+    else if (w > Tu)
+      c.sgt += s;
+  }
+  c = group_reduce<256>(c, OpC(), lds.c);
+  if (threadIdx.x == 0) {
+    P.c_ee[blockIdx.x] = c.ee;
+    P.c_sgt[blockIdx.x] = c.sgt;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __restrict__ chunks,
+                                                   const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ Lds<256> lds;
+  const Chunk ch = chunks[blockIdx.x];
+  const LargeSeg L = ls[ch.lseg];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (st.general) return;
+  const Res& rs = st.rs;
+  const double C = rs.C;
+  const double eq = C / (double)st.cl.count;
+  AggB b{0.0, 0.0, 0};
+  AggC c{0.0, 0};
+  if (!rs.learning && rs.kind >= 2) b = seg_b<256>(P, L, lds);
+  if (!rs.learning && rs.kind == 3) c = seg_c<256>(P, L, lds);
+  SumD delta{0.0};
+  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
+    const int64_t row = ch.row0 + i;
+    const double w = p.wants[row], h = p.has[row];
+    const long long s = p.sub[row];
+    const bool lv = !(p.now > p.expiry[row]);
+    if (!lv) {
+      p.out_gets[row] = 0.0;
+      p.out_expiry[row] = kReleased;
+      if (p.out_wants) {
+        p.out_wants[row] = 0.0;
+        p.out_sub[row] = 0;
+      }
+      continue;
+    }
+    double g;
+    if (rs.learning) {
+      g = h;
+    } else if (rs.kind == 0) {
+      g = w;
+    } else if (rs.kind == 1) {
+      g = minF(C, w);
+    } else if (rs.kind == 2) {
+      const double epc = eq * (double)s;
+      const double unused = C - st.cl.sum_has + h;
+      g = (st.cl.sum_wants <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (b.x / b.y), unused);
+    } else {
+      double T = 0.0;
+      if (!fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &T))
+        g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, T, c);
+    }
+    p.out_gets[row] = g;
+    p.out_expiry[row] = rs.exp_out;
+    delta.v += g - h;
+  }
+  delta = group_reduce<256>(delta, OpSumD(), lds.d);
+  if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
+}
+
+__global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ Lds<256> lds;
+  const LargeSeg L = ls[blockIdx.x];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (st.general) return;
+  SumD d{0.0};
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 256) d.v += P.d_delta[c];
+  d = group_reduce<256>(d, OpSumD(), lds.d);
+  if (threadIdx.x == 0) write_resource(p, L.seg, st.rs, st.cl, d.v);
+}
+
+// General FairShare for a large resource with heterogeneous subclients or NaN
+// wants: one workgroup streams the resource, one round-2 pass per distinct
+// threshold in increasing order.  Correct for any size; only the hierarchy's
+// root level produces such resources, and those are small.
+__global__ __launch_bounds__(256) void k_general(DevParams p, const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ Lds<256> lds;
+  const LargeSeg L = ls[blockIdx.x];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (!st.general) return;
+  const int64_t lo = p.seg_off[L.seg], hi = p.seg_off[L.seg + 1];
+  const double C = st.rs.C;
+  const double eq = C / (double)st.cl.count;
+  // round 1 sums
+  AggB b{0.0, 0.0, 0};
+  for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+    if (p.now > p.expiry[row]) continue;
+    const double w = p.wants[row];
+    const long long s = p.sub[row];
+    const double d = (double)s * eq;
+    if (w < d)
+      b.x += d - w;
+    else if (w > d)
+      b.i += s;
+  }
+  b = group_reduce<256>(b, OpB(), lds.b);
+  // rows decided in round 0/1, released rows, NaN thresholds
+  SumD delta{0.0};
+  for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+    const double w = p.wants[row], h = p.has[row];
+    const long long s = p.sub[row];
+    if (p.now > p.expiry[row]) {
+      p.out_gets[row] = 0.0;
+      p.out_expiry[row] = kReleased;
+      if (p.out_wants) {
+        p.out_wants[row] = 0.0;
+        p.out_sub[row] = 0;
+      }
+      continue;
+    }
+    double g, T = 0.0;
+    bool done = fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &T);
+    if (!done && __builtin_isnan(T)) {
+      g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, T, AggC{0.0, 0});
+      done = true;
+    }
+    if (done) {
+      p.out_gets[row] = g;
+      p.out_expiry[row] = st.rs.exp_out;
+      delta.v += g - h;
+    }
+  }
+  // round 2, one distinct threshold at a time
+  double prev = 0.0;
+  int have_prev = 0;
+  for (;;) {
+    TMin tm{0.0, 0, 0};
+    for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+      if (p.now > p.expiry[row]) continue;
+      double g, T = 0.0;
+      if (fs_stage01(p.wants[row], p.has[row], p.sub[row], C, st.cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+      if (__builtin_isnan(T) || (have_prev && !(T > prev))) continue;
+      if (!tm.found || T < tm.t) tm = TMin{T, 1, 0};
+    }
+    tm = group_reduce<256>(tm, OpTMin(), lds.t);
+    if (!tm.found) break;
+    const double Ts = tm.t;
+    AggC c{0.0, 0};
+    for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+      if (p.now > p.expiry[row]) continue;
+      const double w = p.wants[row];
+      const long long s = p.sub[row];
+      if (!(w > (double)s * eq)) continue;
+      if (w < Ts)
+        c.ee += Ts - w;
+      else if (w > Ts)
+        c.sgt += s;
+    }
+    c = group_reduce<256>(c, OpC(), lds.c);
+    for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+      if (p.now > p.expiry[row]) continue;
+      const double w = p.wants[row], h = p.has[row];
+      const long long s = p.sub[row];
+      double g, T = 0.0;
+      if (fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+      if (!(T == Ts)) continue;
+      g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, T, c);
+      p.out_gets[row] = g;
+      p.out_expiry[row] = st.rs.exp_out;
+      delta.v += g - h;
+    }
+    prev = Ts;
+    have_prev = 1;
+  }
+  delta = group_reduce<256>(delta, OpSumD(), lds.d);
+  if (threadIdx.x == 0) write_resource(p, L.seg, st.rs, st.cl, delta.v);
+}
+
+// --------------------------------------------------------------------------
+// store maintenance
+// --------------------------------------------------------------------------
+// Assign on existing rows (store.go:153-167): running sums += new - old.
+// Rows are applied in order by one thread per resource group? No: rows may hit
+// the same resource, so sums are accumulated with 64-bit atomics of the deltas.
+__global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
+                         const double* __restrict__ wants, const int64_t* __restrict__ sub,
+                         const int64_t* __restrict__ expiry, const int32_t* __restrict__ row_seg, double* s_has,
+                         double* s_wants, int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
+                         double* agg_sum_wants) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  const int seg = row_seg[i];
+  const double dh = has[i] - s_has[r], dw = wants[i] - s_wants[r];
+  const long long ds = sub[i] - s_sub[r];
+  s_has[r] = has[i];
+  s_wants[r] = wants[i];
+  s_sub[r] = sub[i];
+  s_exp[r] = expiry[i];
+  atomicAdd(&agg_sum_has[seg], dh);
+  atomicAdd(&agg_sum_wants[seg], dw);
+  atomicAdd((unsigned long long*)&agg_count[seg], (unsigned long long)ds);
+}
+
+__global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int32_t* __restrict__ row_seg,
+                          double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, int64_t* agg_count,
+                          double* agg_sum_has, double* agg_sum_wants) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  const int seg = row_seg[i];
+  atomicAdd(&agg_sum_has[seg], -s_has[r]);
+  atomicAdd(&agg_sum_wants[seg], -s_wants[r]);
+  atomicAdd((unsigned long long*)&agg_count[seg], (unsigned long long)(-s_sub[r]));
+  s_has[r] = 0.0;
+  s_wants[r] = 0.0;
+  s_sub[r] = 0;
+  s_exp[r] = kReleased;
+}
+
+// server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
+__global__ void k_publish(int64_t R, const double* __restrict__ sum_wants, const int64_t* __restrict__ count,
+                          double2* __restrict__ dst) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  double2 v;
+  v.x = sum_wants[r];
+  v.y = __longlong_as_double(count[r]);
+  dst[r] = v;
+}
+
+// --------------------------------------------------------------------------
+// host-side launchers (called by dm_runtime.cpp)
+// --------------------------------------------------------------------------
+hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_small<<<(n + 3) / 4, 256, 0, st>>>(p, packs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  switch (bin) {
+    case 0: k_wave<<<(n + 3) / 4, 256, 0, st>>>(p, segs, n); break;
+    case 1: k_block<1><<<n, 256, 0, st>>>(p, segs, n); break;
+    case 2: k_block<2><<<n, 256, 0, st>>>(p, segs, n); break;
+    case 3: k_block<4><<<n, 256, 0, st>>>(p, segs, n); break;
+    case 4: k_block<8><<<n, 256, 0, st>>>(p, segs, n); break;
+    case 5: k_block<16><<<n, 256, 0, st>>>(p, segs, n); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
+                        const Partials& P, hipStream_t st) {
+  if (nchunks <= 0) return hipSuccess;
+  switch (phase) {
+    case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
+    case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P); break;
+    case 5: k_general<<<nls, 256, 0, st>>>(p, ls, P); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
+                         const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
+                         int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
+                         double* agg_sum_wants, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, row_seg, s_has, s_wants,
+                                                        s_sub, s_exp, agg_count, agg_sum_has, agg_sum_wants);
+  return hipGetLastError();
+}
+
+hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
+                          int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
+                          double* agg_sum_wants, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, row_seg, s_has, s_wants, s_sub, s_exp, agg_count,
+                                                         agg_sum_has, agg_sum_wants);
+  return hipGetLastError();
+}
+
+hipError_t launch_publish(int64_t R, const double* sum_wants, const int64_t* count, void* dst, hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  k_publish<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, sum_wants, count, (double2*)dst);
+  return hipGetLastError();
+}
+
+}  // namespace dm

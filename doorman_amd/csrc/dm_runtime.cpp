@@ -1,0 +1,733 @@
+// dm_runtime.cpp — host runtime behind include/doorman_hip.h.
+//
+// Owns the device-resident columnar lease store (one context per GPU), builds
+// the size-binned dispatch plan from the segment offsets, launches a tick on the
+// context's HIP stream and reads results back.  See DESIGN.md §3-§5.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/doorman_hip.h"
+#include "dm_device.h"
+
+namespace dm {
+hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
+hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, hipStream_t st);
+hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
+                        const Partials& P, hipStream_t st);
+hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
+                         const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
+                         int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
+                         double* agg_sum_wants, hipStream_t st);
+hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
+                          int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
+                          double* agg_sum_wants, hipStream_t st);
+hipError_t launch_publish(int64_t R, const double* sum_wants, const int64_t* count, void* dst, hipStream_t st);
+}  // namespace dm
+
+using namespace dm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+// kernel classes for profiling
+enum KClass {
+  KC_SMALL = 0,
+  KC_BIN0,  // wave64 .. 256x16
+  KC_LARGE_A = KC_BIN0 + kNumBins,
+  KC_LARGE_B,
+  KC_LARGE_C,
+  KC_LARGE_MAP,
+  KC_LARGE_FIN,
+  KC_GENERAL,
+  KC_UPSERT,
+  KC_RELEASE,
+  KC_COUNT
+};
+const char* kClassNames[KC_COUNT] = {"small_packed", "wave64x1",   "block256x1", "block256x2",  "block256x4",
+                                     "block256x8",   "block256x16", "large_a",    "large_b",     "large_c",
+                                     "large_map",    "large_fin",  "general",    "store_upsert", "store_release"};
+
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (count == 0) return hipSuccess;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct ProfEvent {
+  int cls;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct dm_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  int64_t R = 0, N = 0;
+  bool store_loaded = false, cfg_loaded = false;
+  std::vector<int64_t> h_seg_off;
+  std::vector<int64_t> h_refresh_s;
+
+  // lease table
+  DBuf<int64_t> seg_off;
+  DBuf<double> wants, has;
+  DBuf<int64_t> sub, expiry;
+  // running sums
+  DBuf<int64_t> agg_count;
+  DBuf<double> agg_sum_has, agg_sum_wants;
+  // config
+  DBuf<int32_t> kind;
+  DBuf<double> capacity, safe_cap;
+  DBuf<int64_t> lease_len, refresh, learning_end, parent_expiry;
+  // outputs of a non-writeback tick
+  DBuf<double> out_gets;
+  DBuf<int64_t> out_expiry;
+  DBuf<int64_t> res_count;
+  DBuf<double> res_sum_has, res_sum_wants, res_safe;
+  bool last_writeback = false, have_result = false;
+  // plan
+  std::vector<Pack> h_packs;
+  std::vector<int32_t> h_bins[kNumBins];
+  std::vector<Chunk> h_chunks;
+  std::vector<LargeSeg> h_large;
+  DBuf<Pack> packs;
+  DBuf<int32_t> bins[kNumBins];
+  DBuf<Chunk> chunks;
+  DBuf<LargeSeg> large;
+  // large-path partials
+  DBuf<int64_t> pa_cnt, pa_smin, pa_smax, pb_w, pc_sgt;
+  DBuf<double> pa_has, pa_wants, pb_x, pb_y, pc_ee, pd_delta;
+  DBuf<int32_t> pa_nan;
+  // staging for upsert / release
+  DBuf<int64_t> st_rows, st_sub, st_exp;
+  DBuf<double> st_has, st_wants;
+  DBuf<int32_t> st_seg;
+  // profiling
+  bool profiling = false;
+  std::vector<ProfEvent> pending;
+  std::vector<hipEvent_t> event_pool;
+  int64_t prof_launches[KC_COUNT] = {};
+  double prof_ms[KC_COUNT] = {};
+
+  int fail(int code, const std::string& msg) {
+    err = msg;
+    g_last_error = msg;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* what) {
+    return fail(DM_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
+  hipEvent_t take_event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void collect_profile() {
+    for (auto& pe : pending) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+        prof_ms[pe.cls] += ms;
+        prof_launches[pe.cls] += 1;
+      }
+      event_pool.push_back(pe.a);
+      event_pool.push_back(pe.b);
+    }
+    pending.clear();
+  }
+  void free_all() {
+    seg_off.release(); wants.release(); has.release(); sub.release(); expiry.release();
+    agg_count.release(); agg_sum_has.release(); agg_sum_wants.release();
+    kind.release(); capacity.release(); safe_cap.release(); lease_len.release(); refresh.release();
+    learning_end.release(); parent_expiry.release();
+    out_gets.release(); out_expiry.release(); res_count.release(); res_sum_has.release();
+    res_sum_wants.release(); res_safe.release();
+    packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
+    pa_cnt.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
+    pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
+    pa_nan.release();
+    st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release(); st_seg.release();
+  }
+};
+
+#define DM_HIP(ctx, expr, what)                  \
+  do {                                           \
+    hipError_t _e = (expr);                      \
+    if (_e != hipSuccess) return (ctx)->hip_fail(_e, what); \
+  } while (0)
+
+#define DM_CHECK_CTX(ctx)                                   \
+  do {                                                      \
+    if (!(ctx)) {                                           \
+      g_last_error = "null context";                        \
+      return DM_E_INVAL;                                    \
+    }                                                       \
+    DM_HIP(ctx, hipSetDevice((ctx)->device), "hipSetDevice"); \
+  } while (0)
+
+template <typename T>
+static hipError_t upload(DBuf<T>& b, const T* src, size_t n, hipStream_t st) {
+  hipError_t e = b.ensure(n);
+  if (e != hipSuccess || n == 0) return e;
+  return hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, st);
+}
+
+// ---------------------------------------------------------------------------
+// plan: size-binned dispatch
+// ---------------------------------------------------------------------------
+static int bin_of(int64_t n) {
+  if (n <= 64) return 0;
+  if (n <= 256) return 1;
+  if (n <= 512) return 2;
+  if (n <= 1024) return 3;
+  if (n <= 2048) return 4;
+  return 5;
+}
+
+static void build_plan(dm_ctx* c) {
+  c->h_packs.clear();
+  for (auto& b : c->h_bins) b.clear();
+  c->h_chunks.clear();
+  c->h_large.clear();
+  const std::vector<int64_t>& off = c->h_seg_off;
+  Pack cur{};
+  bool open = false;
+  auto close = [&]() {
+    if (open) c->h_packs.push_back(cur);
+    open = false;
+  };
+  for (int64_t r = 0; r < c->R; ++r) {
+    const int64_t n = off[r + 1] - off[r];
+    if (n <= kSmallMax) {
+      if (open && (cur.nrows + n > 64 || cur.nseg >= 63)) close();
+      if (!open) {
+        cur = Pack{(int32_t)r, 0, off[r], 0, 0};
+        open = true;
+      }
+      cur.nseg += 1;
+      cur.nrows += (int32_t)n;
+      cur.maxlen = std::max<int32_t>(cur.maxlen, (int32_t)n);
+      continue;
+    }
+    close();
+    if (n <= kLargeMin) {
+      c->h_bins[bin_of(n)].push_back((int32_t)r);
+    } else {
+      LargeSeg L{(int32_t)r, (int32_t)c->h_chunks.size(), 0, 0};
+      for (int64_t o = off[r]; o < off[r + 1]; o += kChunkRows) {
+        Chunk ch{(int32_t)r, (int32_t)c->h_large.size(), o, (int32_t)std::min<int64_t>(kChunkRows, off[r + 1] - o), 0};
+        c->h_chunks.push_back(ch);
+      }
+      L.chunk_end = (int32_t)c->h_chunks.size();
+      c->h_large.push_back(L);
+    }
+  }
+  close();
+}
+
+static int upload_plan(dm_ctx* c) {
+  hipStream_t st = c->stream;
+  DM_HIP(c, upload(c->packs, c->h_packs.data(), c->h_packs.size(), st), "plan packs");
+  for (int b = 0; b < kNumBins; ++b) DM_HIP(c, upload(c->bins[b], c->h_bins[b].data(), c->h_bins[b].size(), st), "plan bins");
+  DM_HIP(c, upload(c->chunks, c->h_chunks.data(), c->h_chunks.size(), st), "plan chunks");
+  DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
+  const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
+  DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
+  DM_HIP(c, c->pa_smin.ensure(nc), "partials");
+  DM_HIP(c, c->pa_smax.ensure(nc), "partials");
+  DM_HIP(c, c->pb_w.ensure(nc), "partials");
+  DM_HIP(c, c->pc_sgt.ensure(nc), "partials");
+  DM_HIP(c, c->pa_has.ensure(nc), "partials");
+  DM_HIP(c, c->pa_wants.ensure(nc), "partials");
+  DM_HIP(c, c->pb_x.ensure(nc), "partials");
+  DM_HIP(c, c->pb_y.ensure(nc), "partials");
+  DM_HIP(c, c->pc_ee.ensure(nc), "partials");
+  DM_HIP(c, c->pd_delta.ensure(nc), "partials");
+  DM_HIP(c, c->pa_nan.ensure(nc), "partials");
+  return DM_OK;
+}
+
+template <typename T>
+static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStream_t st) {
+  if (!dst || n == 0) return hipSuccess;
+  return hipMemcpyAsync(dst, src + off, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, st);
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* dm_version(void) { return "doorman-hip 0.1 (gfx950, abi 1)"; }
+
+int dm_device_count(int* out) {
+  if (!out) return DM_E_INVAL;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    g_last_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(e);
+    *out = 0;
+    return DM_E_HIP;
+  }
+  *out = n;
+  return DM_OK;
+}
+
+int dm_create(int device, dm_ctx** out) {
+  if (!out) return DM_E_INVAL;
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    g_last_error = std::string("no HIP device: ") + hipGetErrorString(e);
+    return DM_E_HIP;
+  }
+  if (device < 0 || device >= n) {
+    g_last_error = "device index out of range";
+    return DM_E_RANGE;
+  }
+  e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    g_last_error = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return DM_E_HIP;
+  }
+  dm_ctx* c = new dm_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+    delete c;
+    return DM_E_HIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return DM_OK;
+}
+
+void dm_destroy(dm_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  c->collect_profile();
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  c->free_all();
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char* dm_last_error(dm_ctx* c) { return c ? c->err.c_str() : g_last_error.c_str(); }
+
+int dm_set_stream(dm_ctx* c, void* s) {
+  DM_CHECK_CTX(c);
+  DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return DM_OK;
+}
+
+void* dm_get_stream(dm_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int dm_sync(dm_ctx* c) {
+  DM_CHECK_CTX(c);
+  DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  c->collect_profile();
+  return DM_OK;
+}
+
+int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
+  DM_CHECK_CTX(c);
+  if (!s || s->n_resources < 0 || s->n_leases < 0 || !s->seg_off) return c->fail(DM_E_INVAL, "bad snapshot");
+  const int64_t R = s->n_resources, N = s->n_leases;
+  if (R > INT32_MAX - 1) return c->fail(DM_E_INVAL, "too many resources for one context (max 2^31-2)");
+  if (N > 0 && (!s->wants || !s->has || !s->subclients || !s->expiry_ns))
+    return c->fail(DM_E_INVAL, "snapshot columns missing");
+  if (s->seg_off[0] != 0 || s->seg_off[R] != N) return c->fail(DM_E_INVAL, "seg_off must run from 0 to n_leases");
+  for (int64_t r = 0; r < R; ++r)
+    if (s->seg_off[r + 1] < s->seg_off[r]) return c->fail(DM_E_INVAL, "seg_off must be non-decreasing");
+  const bool have_agg = s->agg_count && s->agg_sum_has && s->agg_sum_wants;
+  if ((s->agg_count || s->agg_sum_has || s->agg_sum_wants) && !have_agg)
+    return c->fail(DM_E_INVAL, "give all three running sums or none");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  c->R = R;
+  c->N = N;
+  c->h_seg_off.assign(s->seg_off, s->seg_off + R + 1);
+  hipStream_t st = c->stream;
+  DM_HIP(c, upload(c->seg_off, s->seg_off, (size_t)R + 1, st), "upload seg_off");
+  DM_HIP(c, upload(c->wants, s->wants, (size_t)N, st), "upload wants");
+  DM_HIP(c, upload(c->has, s->has, (size_t)N, st), "upload has");
+  DM_HIP(c, upload(c->sub, s->subclients, (size_t)N, st), "upload subclients");
+  DM_HIP(c, upload(c->expiry, s->expiry_ns, (size_t)N, st), "upload expiry");
+  std::vector<int64_t> cnt;
+  std::vector<double> sh, sw;
+  const int64_t* ac = s->agg_count;
+  const double* ah = s->agg_sum_has;
+  const double* aw = s->agg_sum_wants;
+  if (!have_agg) {  // one Assign per row, in row order (store.go:156-158)
+    cnt.assign(R, 0);
+    sh.assign(R, 0.0);
+    sw.assign(R, 0.0);
+    for (int64_t r = 0; r < R; ++r)
+      for (int64_t i = s->seg_off[r]; i < s->seg_off[r + 1]; ++i) {
+        sh[r] += s->has[i] - 0.0;
+        sw[r] += s->wants[i] - 0.0;
+        cnt[r] += s->subclients[i];
+      }
+    ac = cnt.data();
+    ah = sh.data();
+    aw = sw.data();
+  }
+  DM_HIP(c, upload(c->agg_count, ac, (size_t)R, st), "upload agg_count");
+  DM_HIP(c, upload(c->agg_sum_has, ah, (size_t)R, st), "upload agg_sum_has");
+  DM_HIP(c, upload(c->agg_sum_wants, aw, (size_t)R, st), "upload agg_sum_wants");
+  build_plan(c);
+  int rc = upload_plan(c);
+  if (rc) return rc;
+  DM_HIP(c, hipStreamSynchronize(st), "store load");
+  c->store_loaded = true;
+  c->have_result = false;
+  if (c->cfg_loaded && (int64_t)c->h_refresh_s.size() != R) c->cfg_loaded = false;
+  return DM_OK;
+}
+
+int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
+  DM_CHECK_CTX(c);
+  if (!cfg || R < 0 || !cfg->kind || !cfg->capacity || !cfg->lease_length_s || !cfg->refresh_interval_s ||
+      !cfg->learning_end_ns || !cfg->parent_expiry_ns || !cfg->safe_capacity)
+    return c->fail(DM_E_INVAL, "bad config");
+  for (int64_t r = 0; r < R; ++r)
+    if (cfg->kind[r] < DM_NO_ALGORITHM || cfg->kind[r] > DM_FAIR_SHARE) {
+      char buf[96];
+      snprintf(buf, sizeof buf, "unknown algorithm kind %d for resource %lld", cfg->kind[r], (long long)r);
+      return c->fail(DM_E_KIND, buf);
+    }
+  DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  hipStream_t st = c->stream;
+  DM_HIP(c, upload(c->kind, cfg->kind, (size_t)R, st), "upload kind");
+  DM_HIP(c, upload(c->capacity, cfg->capacity, (size_t)R, st), "upload capacity");
+  DM_HIP(c, upload(c->lease_len, cfg->lease_length_s, (size_t)R, st), "upload lease_length");
+  DM_HIP(c, upload(c->refresh, cfg->refresh_interval_s, (size_t)R, st), "upload refresh");
+  DM_HIP(c, upload(c->learning_end, cfg->learning_end_ns, (size_t)R, st), "upload learning_end");
+  DM_HIP(c, upload(c->parent_expiry, cfg->parent_expiry_ns, (size_t)R, st), "upload parent_expiry");
+  DM_HIP(c, upload(c->safe_cap, cfg->safe_capacity, (size_t)R, st), "upload safe_capacity");
+  c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
+  DM_HIP(c, hipStreamSynchronize(st), "config load");
+  c->cfg_loaded = true;
+  return DM_OK;
+}
+
+static int ready(dm_ctx* c) {
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (!c->cfg_loaded || (int64_t)c->h_refresh_s.size() != c->R)
+    return c->fail(DM_E_STATE, "no configuration loaded for the store's resources");
+  return DM_OK;
+}
+
+int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
+  DM_CHECK_CTX(c);
+  int rc = ready(c);
+  if (rc) return rc;
+  const bool wb = flags & DM_WRITEBACK;
+  DevParams p{};
+  p.seg_off = c->seg_off.p;
+  p.wants = c->wants.p;
+  p.has = c->has.p;
+  p.sub = c->sub.p;
+  p.expiry = c->expiry.p;
+  p.kind = c->kind.p;
+  p.capacity = c->capacity.p;
+  p.lease_len_s = c->lease_len.p;
+  p.refresh_s = c->refresh.p;
+  p.learning_end = c->learning_end.p;
+  p.parent_expiry = c->parent_expiry.p;
+  p.safe_cap = c->safe_cap.p;
+  p.agg_count = c->agg_count.p;
+  p.agg_sum_has = c->agg_sum_has.p;
+  p.agg_sum_wants = c->agg_sum_wants.p;
+  if (wb) {
+    p.out_gets = c->has.p;
+    p.out_expiry = c->expiry.p;
+    p.out_wants = c->wants.p;
+    p.out_sub = c->sub.p;
+    p.res_count = c->agg_count.p;
+    p.res_sum_has = c->agg_sum_has.p;
+    p.res_sum_wants = c->agg_sum_wants.p;
+    DM_HIP(c, c->res_safe.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res_safe");
+    p.res_safe = c->res_safe.p;
+  } else {
+    DM_HIP(c, c->out_gets.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_gets");
+    DM_HIP(c, c->out_expiry.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_expiry");
+    DM_HIP(c, c->res_count.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
+    DM_HIP(c, c->res_sum_has.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
+    DM_HIP(c, c->res_sum_wants.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
+    DM_HIP(c, c->res_safe.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
+    p.out_gets = c->out_gets.p;
+    p.out_expiry = c->out_expiry.p;
+    p.out_wants = nullptr;
+    p.out_sub = nullptr;
+    p.res_count = c->res_count.p;
+    p.res_sum_has = c->res_sum_has.p;
+    p.res_sum_wants = c->res_sum_wants.p;
+    p.res_safe = c->res_safe.p;
+  }
+  p.now = now_ns;
+  p.recompute = (flags & DM_AGG_RECOMPUTE) ? 1 : 0;
+
+  Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
+             c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p};
+  hipStream_t st = c->stream;
+  auto timed = [&](int cls, auto&& fn) -> hipError_t {
+    if (!c->profiling) return fn();
+    ProfEvent pe{cls, c->take_event(), c->take_event()};
+    (void)hipEventRecord(pe.a, st);
+    hipError_t e = fn();
+    (void)hipEventRecord(pe.b, st);
+    c->pending.push_back(pe);
+    return e;
+  };
+  const int nch = (int)c->h_chunks.size(), nls = (int)c->h_large.size();
+  // large resources first (longest dependency chain), then the binned groups
+  for (int ph = 0; ph < 6 && nch > 0; ++ph)
+    DM_HIP(c, timed(KC_LARGE_A + ph, [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, st); }),
+           "large-resource kernels");
+  for (int b = kNumBins - 1; b >= 0; --b) {
+    const int n = (int)c->h_bins[b].size();
+    if (n == 0) continue;
+    DM_HIP(c, timed(KC_BIN0 + b, [&] { return launch_bin(b, p, c->bins[b].p, n, st); }), "group kernel");
+  }
+  if (!c->h_packs.empty())
+    DM_HIP(c, timed(KC_SMALL, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), st); }),
+           "small kernel");
+  c->last_writeback = wb;
+  c->have_result = true;
+  if (!(flags & DM_ASYNC)) {
+    DM_HIP(c, hipStreamSynchronize(st), "tick");
+    c->collect_profile();
+  }
+  return DM_OK;
+}
+
+static int check_range(dm_ctx* c, int64_t off, int64_t n, int64_t total) {
+  if (off < 0 || n < 0 || off + n > total) return c->fail(DM_E_RANGE, "range out of bounds");
+  return DM_OK;
+}
+
+int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* expiry_ns) {
+  DM_CHECK_CTX(c);
+  if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
+  int rc = check_range(c, off, n, c->N);
+  if (rc) return rc;
+  const double* g = c->last_writeback ? c->has.p : c->out_gets.p;
+  const int64_t* e = c->last_writeback ? c->expiry.p : c->out_expiry.p;
+  DM_HIP(c, download(gets, g, off, n, c->stream), "read gets");
+  DM_HIP(c, download(expiry_ns, e, off, n, c->stream), "read expiry");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
+  return DM_OK;
+}
+
+int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, int64_t* expiry_time_s,
+                         int64_t* refresh_interval_s) {
+  std::vector<int64_t> e(n > 0 ? n : 0);
+  int rc = dm_read_leases(c, off, n, capacity, e.data());
+  if (rc) return rc;
+  if (expiry_time_s)
+    for (int64_t i = 0; i < n; ++i) {
+      // time.Time.Unix(): floor division by 1e9 (server.go:789)
+      int64_t v = e[i];
+      if (v == DM_RELEASED) {
+        expiry_time_s[i] = DM_RELEASED;
+        continue;
+      }
+      int64_t q = v / kNs;
+      if (v % kNs != 0 && v < 0) --q;
+      expiry_time_s[i] = q;
+    }
+  if (refresh_interval_s) {
+    const auto& so = c->h_seg_off;
+    int64_t r = std::upper_bound(so.begin(), so.end(), off) - so.begin() - 1;
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t row = off + i;
+      while (r + 1 < (int64_t)so.size() && so[r + 1] <= row) ++r;
+      refresh_interval_s[i] = e[i] == DM_RELEASED ? 0 : c->h_refresh_s[r];
+    }
+  }
+  return DM_OK;
+}
+
+int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* sum_has, double* sum_wants,
+                      double* safe) {
+  DM_CHECK_CTX(c);
+  int rc = check_range(c, r0, n, c->R);
+  if (rc) return rc;
+  const bool wb = !c->have_result || c->last_writeback;
+  if (safe && !c->have_result) return c->fail(DM_E_STATE, "safe capacity needs a dm_apportion result");
+  DM_HIP(c, download(count, wb ? c->agg_count.p : c->res_count.p, r0, n, c->stream), "read count");
+  DM_HIP(c, download(sum_has, wb ? c->agg_sum_has.p : c->res_sum_has.p, r0, n, c->stream), "read sum_has");
+  DM_HIP(c, download(sum_wants, wb ? c->agg_sum_wants.p : c->res_sum_wants.p, r0, n, c->stream), "read sum_wants");
+  DM_HIP(c, download(safe, (const double*)c->res_safe.p, r0, n, c->stream), "read safe");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "read resources");
+  return DM_OK;
+}
+
+int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants, int64_t* sub, int64_t* exp) {
+  DM_CHECK_CTX(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  int rc = check_range(c, off, n, c->N);
+  if (rc) return rc;
+  DM_HIP(c, download(has, (const double*)c->has.p, off, n, c->stream), "read has");
+  DM_HIP(c, download(wants, (const double*)c->wants.p, off, n, c->stream), "read wants");
+  DM_HIP(c, download(sub, (const int64_t*)c->sub.p, off, n, c->stream), "read sub");
+  DM_HIP(c, download(exp, (const int64_t*)c->expiry.p, off, n, c->stream), "read expiry");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "read store");
+  return DM_OK;
+}
+
+static int stage_rows(dm_ctx* c, int64_t n, const int64_t* rows) {
+  std::vector<int32_t> seg(n);
+  const auto& so = c->h_seg_off;
+  for (int64_t i = 0; i < n; ++i) {
+    if (rows[i] < 0 || rows[i] >= c->N) return c->fail(DM_E_RANGE, "row out of range");
+    seg[i] = (int32_t)(std::upper_bound(so.begin(), so.end(), rows[i]) - so.begin() - 1);
+  }
+  std::vector<int64_t> sorted(rows, rows + n);
+  std::sort(sorted.begin(), sorted.end());
+  if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+    return c->fail(DM_E_INVAL, "rows must be unique within one call");
+  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
+  DM_HIP(c, upload(c->st_seg, seg.data(), (size_t)n, c->stream), "stage seg");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "stage");
+  return DM_OK;
+}
+
+int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has, const double* wants,
+                    const int64_t* sub, const int64_t* exp) {
+  DM_CHECK_CTX(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
+  if (n == 0) return DM_OK;
+  int rc = stage_rows(c, n, rows);
+  if (rc) return rc;
+  DM_HIP(c, upload(c->st_has, has, (size_t)n, c->stream), "stage has");
+  DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
+  DM_HIP(c, upload(c->st_sub, sub, (size_t)n, c->stream), "stage sub");
+  DM_HIP(c, upload(c->st_exp, exp, (size_t)n, c->stream), "stage expiry");
+  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->st_seg.p,
+                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg_count.p, c->agg_sum_has.p,
+                          c->agg_sum_wants.p, c->stream),
+         "upsert");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "upsert");
+  c->have_result = false;
+  return DM_OK;
+}
+
+int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
+  DM_CHECK_CTX(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
+  if (n == 0) return DM_OK;
+  int rc = stage_rows(c, n, rows);
+  if (rc) return rc;
+  DM_HIP(c, launch_release(n, c->st_rows.p, c->st_seg.p, c->has.p, c->wants.p, c->sub.p, c->expiry.p,
+                           c->agg_count.p, c->agg_sum_has.p, c->agg_sum_wants.p, c->stream),
+         "release");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "release");
+  c->have_result = false;
+  return DM_OK;
+}
+
+int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t n, double* wants_total,
+                       int64_t* subclients_total) {
+  if (n < 0 || (n > 0 && (!wants || !num_clients)) || !wants_total || !subclients_total) return DM_E_INVAL;
+  double wt = 0.0;
+  int64_t stot = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    wt += wants[i];
+    if (num_clients[i] < 1) {
+      g_last_error = "subclients should be > 0";
+      return DM_E_ARGUMENT;
+    }
+    stot += num_clients[i];
+  }
+  *wants_total = wt;
+  *subclients_total = stot;
+  return DM_OK;
+}
+
+int dm_publish_totals(dm_ctx* c, void* dst) {
+  DM_CHECK_CTX(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (!dst) return c->fail(DM_E_INVAL, "null destination");
+  DM_HIP(c, launch_publish(c->R, c->agg_sum_wants.p, c->agg_count.p, dst, c->stream), "publish");
+  return DM_OK;
+}
+
+int dm_set_profiling(dm_ctx* c, int on) {
+  DM_CHECK_CTX(c);
+  c->profiling = on != 0;
+  return DM_OK;
+}
+
+int dm_kernel_times(dm_ctx* c, dm_kernel_time* out, int max) {
+  DM_CHECK_CTX(c);
+  DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  c->collect_profile();
+  for (int i = 0; i < KC_COUNT && i < max; ++i) {
+    out[i].name = kClassNames[i];
+    out[i].launches = c->prof_launches[i];
+    out[i].total_ms = c->prof_ms[i];
+  }
+  return KC_COUNT;
+}
+
+int dm_reset_kernel_times(dm_ctx* c) {
+  DM_CHECK_CTX(c);
+  DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  c->collect_profile();
+  for (int i = 0; i < KC_COUNT; ++i) {
+    c->prof_ms[i] = 0.0;
+    c->prof_launches[i] = 0;
+  }
+  return DM_OK;
+}
+
+int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
+  if (!c || !out) return DM_E_INVAL;
+  int64_t v[4 + kNumBins];
+  v[0] = (int64_t)c->h_packs.size();
+  for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
+  v[1 + kNumBins] = (int64_t)c->h_large.size();
+  v[2 + kNumBins] = (int64_t)c->h_chunks.size();
+  v[3 + kNumBins] = c->N;
+  const int n = 4 + kNumBins;
+  for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
+  return n;
+}
+
+}  // extern "C"

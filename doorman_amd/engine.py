@@ -1,0 +1,195 @@
+"""Python handle on one device context of the C-ABI (include/doorman_hip.h).
+
+This is a thin binding used by tests and bench.py; the store, the planner and
+the kernels live in libdoorman_hip.so.  Method names follow the reference's
+LeaseStore / Algorithm surface (go/server/doorman/store.go:68-103,
+algorithm.go:44) where one exists.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .workloads import CFG_FIELDS
+
+_BIN_NAMES = ("small_packs", "wave64x1", "block256x1", "block256x2", "block256x4", "block256x8", "block256x16",
+              "large_resources", "large_chunks", "leases")
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class Engine:
+    """One GPU context owning a device-resident columnar lease store."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        check(lib().dm_create(device, ctypes.byref(self._ctx)))
+        self.device = device
+        self.n_resources = 0
+        self.n_leases = 0
+
+    # -- lifetime --
+    def close(self):
+        if self._ctx:
+            lib().dm_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc):
+        return check(rc, self._ctx)
+
+    @property
+    def stream(self) -> int:
+        return lib().dm_get_stream(self._ctx) or 0
+
+    def set_stream(self, stream_ptr: int | None):
+        self._chk(lib().dm_set_stream(self._ctx, stream_ptr))
+
+    def sync(self):
+        self._chk(lib().dm_sync(self._ctx))
+
+    # -- LeaseStore --
+    def load(self, snap: dict):
+        """NewLeaseStore + Assign of every row (store.go:114,153) and the resolved config."""
+        self.load_store(snap)
+        self.load_config(snap)
+
+    def load_store(self, snap: dict):
+        keep = {
+            "seg_off": _c(snap["seg_off"], np.int64),
+            "wants": _c(snap["wants"], np.float64),
+            "has": _c(snap["has"], np.float64),
+            "subclients": _c(snap["subclients"], np.int64),
+            "expiry_ns": _c(snap["expiry_ns"], np.int64),
+        }
+        have = snap.get("agg_count") is not None
+        if have:
+            keep["agg_count"] = _c(snap["agg_count"], np.int64)
+            keep["agg_sum_has"] = _c(snap["agg_sum_has"], np.float64)
+            keep["agg_sum_wants"] = _c(snap["agg_sum_wants"], np.float64)
+        s = _lib.Snapshot()
+        s.n_resources = len(keep["seg_off"]) - 1
+        s.n_leases = len(keep["wants"])
+        for k in ("seg_off", "wants", "has", "subclients", "expiry_ns"):
+            setattr(s, k, _ptr(keep[k]))
+        if have:
+            s.agg_count = _ptr(keep["agg_count"])
+            s.agg_sum_has = _ptr(keep["agg_sum_has"])
+            s.agg_sum_wants = _ptr(keep["agg_sum_wants"])
+        self._chk(lib().dm_store_load(self._ctx, ctypes.byref(s)))
+        self.n_resources, self.n_leases = s.n_resources, s.n_leases
+
+    def load_config(self, snap: dict):
+        R = len(snap["kind"])
+        keep = {
+            "kind": _c(snap["kind"], np.int32),
+            "capacity": _c(snap["capacity"], np.float64),
+            "lease_length_s": _c(snap["lease_length_s"], np.int64),
+            "refresh_interval_s": _c(snap["refresh_interval_s"], np.int64),
+            "learning_end_ns": _c(snap["learning_end_ns"], np.int64),
+            "parent_expiry_ns": _c(snap["parent_expiry_ns"], np.int64),
+            "safe_capacity": _c(snap["safe_capacity"], np.float64),
+        }
+        cfg = _lib.ResourceCfg(*[_ptr(keep[k]) for k in CFG_FIELDS])
+        self._chk(lib().dm_config_load(self._ctx, R, ctypes.byref(cfg)))
+
+    def upsert(self, rows, has, wants, subclients, expiry_ns):
+        """Assign on existing rows (store.go:153-167)."""
+        rows = _c(rows, np.int64)
+        a = [_c(has, np.float64), _c(wants, np.float64), _c(subclients, np.int64), _c(expiry_ns, np.int64)]
+        self._chk(lib().dm_store_upsert(self._ctx, len(rows), _ptr(rows), *[_ptr(x) for x in a]))
+
+    def release(self, rows):
+        """Release (store.go:142-151)."""
+        rows = _c(rows, np.int64)
+        self._chk(lib().dm_store_release(self._ctx, len(rows), _ptr(rows)))
+
+    def read_store(self, off: int = 0, n: int | None = None) -> dict:
+        n = self.n_leases - off if n is None else n
+        out = {"has": np.empty(n), "wants": np.empty(n), "subclients": np.empty(n, np.int64),
+               "expiry_ns": np.empty(n, np.int64)}
+        self._chk(lib().dm_read_store(self._ctx, off, n, _ptr(out["has"]), _ptr(out["wants"]),
+                                      _ptr(out["subclients"]), _ptr(out["expiry_ns"])))
+        return out
+
+    # -- the batch algorithm --
+    def apportion(self, now_ns: int, writeback: bool = False, recompute: bool = False, asynchronous: bool = False):
+        flags = ((_lib.DM_WRITEBACK if writeback else 0) | (_lib.DM_AGG_RECOMPUTE if recompute else 0)
+                 | (_lib.DM_ASYNC if asynchronous else 0))
+        self._chk(lib().dm_apportion(self._ctx, int(now_ns), flags))
+
+    def leases(self, off: int = 0, n: int | None = None):
+        n = self.n_leases - off if n is None else n
+        gets, exp = np.empty(n), np.empty(n, np.int64)
+        self._chk(lib().dm_read_leases(self._ctx, off, n, _ptr(gets), _ptr(exp)))
+        return gets, exp
+
+    def leases_proto(self, off: int = 0, n: int | None = None):
+        n = self.n_leases - off if n is None else n
+        cap, exp, ref = np.empty(n), np.empty(n, np.int64), np.empty(n, np.int64)
+        self._chk(lib().dm_read_leases_proto(self._ctx, off, n, _ptr(cap), _ptr(exp), _ptr(ref)))
+        return cap, exp, ref
+
+    def resources(self, r0: int = 0, n: int | None = None, safe: bool = True) -> dict:
+        n = self.n_resources - r0 if n is None else n
+        out = {"count": np.empty(n, np.int64), "sum_has": np.empty(n), "sum_wants": np.empty(n)}
+        if safe:
+            out["safe_capacity"] = np.empty(n)
+        self._chk(lib().dm_read_resources(self._ctx, r0, n, _ptr(out["count"]), _ptr(out["sum_has"]),
+                                          _ptr(out["sum_wants"]), _ptr(out.get("safe_capacity"))))
+        return out
+
+    def publish_totals(self, dev_ptr: int):
+        """{SumWants, Count} per resource into a 16 B x R device buffer (server.go:234-255)."""
+        self._chk(lib().dm_publish_totals(self._ctx, ctypes.c_void_p(dev_ptr)))
+
+    # -- profiling --
+    def set_profiling(self, on: bool):
+        self._chk(lib().dm_set_profiling(self._ctx, 1 if on else 0))
+
+    def kernel_times(self) -> dict:
+        arr = (_lib.KernelTime * 32)()
+        n = self._chk(lib().dm_kernel_times(self._ctx, arr, 32))
+        return {arr[i].name.decode(): (arr[i].launches, arr[i].total_ms) for i in range(n) if arr[i].launches}
+
+    def reset_kernel_times(self):
+        self._chk(lib().dm_reset_kernel_times(self._ctx))
+
+    def plan_info(self) -> dict:
+        arr = (ctypes.c_int64 * 16)()
+        n = self._chk(lib().dm_plan_info(self._ctx, arr, 16))
+        return {_BIN_NAMES[i]: int(arr[i]) for i in range(min(n, len(_BIN_NAMES)))}
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    rc = lib().dm_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def aggregate_bands(wants, num_clients):
+    """GetServerCapacity band sums (server.go:850-868); DmError(DM_E_ARGUMENT) if num_clients < 1."""
+    w, nc = _c(wants, np.float64), _c(num_clients, np.int64)
+    wt, st = ctypes.c_double(), ctypes.c_int64()
+    check(lib().dm_aggregate_bands(_ptr(w), _ptr(nc), len(w), ctypes.byref(wt), ctypes.byref(st)))
+    return wt.value, st.value

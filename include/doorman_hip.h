@@ -1,0 +1,158 @@
+/*
+ * doorman_hip.h — C-ABI of the MI355X batched lease-apportionment engine.
+ *
+ * Drop-in boundary for Doorman's lease path (paths relative to the reference
+ * repository root).  The reference binds no native code; these entry points are
+ * what a cgo shim behind its own interfaces would call (INTEGRATION.md shows the
+ * Go side):
+ *
+ *   LeaseStore interface        go/server/doorman/store.go:68-103   -> dm_store_* / dm_read_*
+ *   NewLeaseStore               go/server/doorman/store.go:114      -> dm_create + dm_store_load
+ *   Algorithm (per request)     go/server/doorman/algorithm.go:44   -> dm_apportion (batch of every client)
+ *   GetAlgorithm / algorithms   go/server/doorman/algorithm.go:304-313 -> dm_resource_cfg.kind
+ *   Resource.Decide             go/server/doorman/resource.go:100-113  -> dm_apportion (Clean + learning + algorithm)
+ *   Resource.capacity           go/server/doorman/resource.go:62-70    -> dm_resource_cfg.parent_expiry_ns
+ *   Resource.SetSafeCapacity    go/server/doorman/resource.go:81-96    -> dm_read_resources(.safe_capacity)
+ *   GetCapacity lease -> proto  go/server/doorman/server.go:787-791    -> dm_read_leases (unix seconds)
+ *   performRequests aggregation go/server/doorman/server.go:234-255    -> dm_read_resources(count, sum_wants)
+ *   GetServerCapacity bands     go/server/doorman/server.go:850-879    -> dm_aggregate_bands
+ *
+ * Batch semantics: every stored lease row is also that client's refresh request
+ * (has, wants, subclients taken from the row) and is decided against the same
+ * frozen store, as if Resource.Decide ran on a private copy of the store for
+ * each client at time now_ns.  Rows that Clean drops (now_ns > expiry_ns,
+ * store.go:174) are released and get no lease (expiry DM_RELEASED).
+ *
+ * Conventions: plain pointers and sizes only; every host pointer is read or
+ * written before the call returns (the caller keeps ownership); return 0 on
+ * success or a negative DM_E_* code, with a message in dm_last_error(ctx).
+ * One call in flight per context; different contexts (GPUs) are independent.
+ */
+#ifndef DOORMAN_HIP_H
+#define DOORMAN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DM_ABI_VERSION 1
+
+/* return codes */
+#define DM_OK 0
+#define DM_E_INVAL (-1)   /* bad argument / shape */
+#define DM_E_HIP (-2)     /* HIP runtime failure (message has the HIP error) */
+#define DM_E_STATE (-3)   /* no store / config loaded, or sizes disagree */
+#define DM_E_KIND (-4)    /* unknown algorithm kind (the reference panics: algorithm.go:312) */
+#define DM_E_RANGE (-5)   /* row / resource index out of range */
+#define DM_E_ARGUMENT (-6) /* codes.InvalidArgument, e.g. num_clients < 1 (server.go:863-866) */
+
+/* pb.Algorithm_Kind (proto/doorman/doorman.proto:139-144) */
+#define DM_NO_ALGORITHM 0
+#define DM_STATIC 1
+#define DM_PROPORTIONAL_SHARE 2
+#define DM_FAIR_SHARE 3
+
+#define DM_RELEASED INT64_MIN /* expiry of a lease Clean released (store.go:169-181) */
+#define DM_NO_PARENT_EXPIRY INT64_MAX /* Resource.expiryTime == nil (resource.go:64) */
+#define DM_NO_LEARNING INT64_MIN      /* learning mode disabled (server.go:173-179) */
+
+/* dm_apportion flags */
+#define DM_WRITEBACK 1u     /* store the tick: has := gets, expiry := lease expiry, released rows zeroed,
+                               running sums updated as the Assigns would (store.go:153-167) */
+#define DM_AGG_RECOMPUTE 2u /* ignore the store's running sums; recompute them from the rows */
+#define DM_ASYNC 4u         /* enqueue on the context stream and return without waiting */
+
+typedef struct dm_ctx dm_ctx;
+
+/* Frozen store snapshot: R resources as CSR segments over N lease rows (SoA). */
+typedef struct {
+  int64_t n_resources;
+  int64_t n_leases;
+  const int64_t* seg_off;    /* [R+1] resource r owns rows [seg_off[r], seg_off[r+1]) */
+  const double* wants;       /* [N] Lease.Wants */
+  const double* has;         /* [N] Lease.Has */
+  const int64_t* subclients; /* [N] Lease.Subclients */
+  const int64_t* expiry_ns;  /* [N] Lease.Expiry, unix ns */
+  const int64_t* agg_count;  /* [R] or NULL: store.count     (running sum; NULL = recompute) */
+  const double* agg_sum_has; /* [R] or NULL: store.sumHas */
+  const double* agg_sum_wants; /* [R] or NULL: store.sumWants */
+} dm_snapshot;
+
+/* Resolved per-resource configuration, SoA over R resources. */
+typedef struct {
+  const int32_t* kind;              /* DM_* algorithm kind */
+  const double* capacity;           /* ResourceTemplate.capacity */
+  const int64_t* lease_length_s;    /* Algorithm.lease_length */
+  const int64_t* refresh_interval_s; /* Algorithm.refresh_interval */
+  const int64_t* learning_end_ns;   /* learningModeEndTime; DM_NO_LEARNING = none */
+  const int64_t* parent_expiry_ns;  /* parent lease expiry; DM_NO_PARENT_EXPIRY = nil */
+  const double* safe_capacity;      /* ResourceTemplate.safe_capacity; NaN = unset */
+} dm_resource_cfg;
+
+typedef struct {
+  const char* name;
+  int64_t launches;
+  double total_ms; /* HIP-event time summed over launches (profiling on) */
+} dm_kernel_time;
+
+/* ---- context ---- */
+const char* dm_version(void);
+int dm_device_count(int* out);
+int dm_create(int device, dm_ctx** out);
+void dm_destroy(dm_ctx* ctx);
+const char* dm_last_error(dm_ctx* ctx);
+/* use an existing hipStream_t (e.g. the caller's current stream); NULL = the context's own */
+int dm_set_stream(dm_ctx* ctx, void* hip_stream);
+void* dm_get_stream(dm_ctx* ctx);
+int dm_sync(dm_ctx* ctx);
+
+/* ---- LeaseStore: device-resident columnar table ---- */
+int dm_store_load(dm_ctx* ctx, const dm_snapshot* snap);
+int dm_config_load(dm_ctx* ctx, int64_t n_resources, const dm_resource_cfg* cfg);
+/* Assign (store.go:153-167) on existing rows: sums += new - old; expiry_ns as given */
+int dm_store_upsert(dm_ctx* ctx, int64_t n, const int64_t* rows, const double* has, const double* wants,
+                    const int64_t* subclients, const int64_t* expiry_ns);
+/* Release (store.go:142-151): sums -= row; row zeroed and marked DM_RELEASED */
+int dm_store_release(dm_ctx* ctx, int64_t n, const int64_t* rows);
+/* read back stored rows (has/wants/subclients/expiry_ns) — any pointer may be NULL */
+int dm_read_store(dm_ctx* ctx, int64_t off, int64_t n, double* has, double* wants, int64_t* subclients,
+                  int64_t* expiry_ns);
+
+/* ---- the batch algorithm: every client of every resource, one frozen snapshot ---- */
+int dm_apportion(dm_ctx* ctx, int64_t now_ns, uint32_t flags);
+
+/* lease outputs of the last dm_apportion: gets (Lease.Has), expiry in unix ns
+ * (DM_RELEASED for released rows); any pointer may be NULL */
+int dm_read_leases(dm_ctx* ctx, int64_t off, int64_t n, double* gets, int64_t* expiry_ns);
+/* proto form (server.go:787-791): capacity, expiry_time = Expiry.Unix(), refresh_interval seconds */
+int dm_read_leases_proto(dm_ctx* ctx, int64_t off, int64_t n, double* capacity, int64_t* expiry_time_s,
+                         int64_t* refresh_interval_s);
+/* per-resource results of the last dm_apportion: store Count/SumHas/SumWants after
+ * the tick, and the safe capacity SetSafeCapacity would report */
+int dm_read_resources(dm_ctx* ctx, int64_t r0, int64_t n, int64_t* count, double* sum_has, double* sum_wants,
+                      double* safe_capacity);
+
+/* ---- hierarchy (intermediate servers) ---- */
+/* server.go:850-879: wants_total = sum(wants), subclients_total = sum(num_clients);
+ * DM_E_ARGUMENT when some num_clients < 1 */
+int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t n, double* wants_total,
+                       int64_t* subclients_total);
+/* server.go:234-255: per-resource {SumWants f64, Count i64} of the current store into a
+ * device buffer (16 B x R, interleaved), ready for an RCCL all-gather */
+int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
+
+/* ---- profiling ---- */
+int dm_set_profiling(dm_ctx* ctx, int on);
+/* fills up to max entries; returns the number of kernel classes (>= 0) */
+int dm_kernel_times(dm_ctx* ctx, dm_kernel_time* out, int max);
+int dm_reset_kernel_times(dm_ctx* ctx);
+/* plan summary of the loaded store: counts per dispatch bin (small packs, 64x1,
+ * 256x1..256x16, large chunks) */
+int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,254 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar: expiries / counts bit-exact; gets within
+1e-9 * max(|ref|, capacity_r); the wave-packed small-resource path is bit-exact
+(it sums in the oracle's row order).  Full-size configs are checked on sampled
+resources, which the oracle evaluates on the same rows.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from doorman_amd import workloads as W
+from oracle import oracle as O
+from parity_util import (assert_leases_match, assert_resources_match, binned_sizes, float_close,
+                         snapshot_with_sizes)
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+KATS = json.load(open(os.path.join(HERE, "golden", "reference_kats.json")))
+NOW = W.NOW_NS
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from doorman_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def run(eng, snap, writeback=False, recompute=False):
+    eng.load(snap)
+    eng.apportion(NOW, writeback=writeback, recompute=recompute)
+    gets, exp = eng.leases()
+    return gets, exp, eng.resources()
+
+
+@pytest.mark.parametrize("case", KATS["snapshot"], ids=lambda c: c["name"])
+def test_reference_kats_bit_exact(eng, case):
+    n = len(case["wants"])
+    snap = W.make_snapshot([n], case["wants"], case["has"], case["sub"], NOW + 300 * W.NS, case["kind"],
+                           case["capacity"], lease_length_s=300)
+    gets, exp, _ = run(eng, snap)
+    assert gets.tolist() == case["gets"]
+    assert (exp == NOW + 300 * W.NS).all()
+
+
+@pytest.mark.parametrize("size", [3, 40, 200, 1000, 3000, 10000])
+@pytest.mark.parametrize("kind", [2, 3])
+def test_doc_examples_at_every_bin(eng, size, kind):
+    """doc/algorithms.md:44-69 pattern replicated to each dispatch bin: one greedy
+    client, one moderate, the rest below the equal share."""
+    rng = np.random.default_rng(size)
+    C = 120.0 * size / 3
+    wants = np.full(size, 10.0 * C / 120.0 / (size / 3))
+    wants[0], wants[1] = 1000.0 * C / 120, 50.0 * C / 120 / (size / 3)
+    rng.shuffle(wants)
+    snap = W.make_snapshot([size], wants, 0.0, 1, NOW + W.NS, kind, C)
+    gets, exp, res = run(eng, snap)
+    ref = O.apportion(snap, NOW)
+    assert_leases_match(snap, gets, exp, ref)
+    assert_resources_match(snap, res, ref)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("variant", ["uniform", "hetero", "edge"])
+@pytest.mark.parametrize("recompute", [False, True])
+def test_random_all_bins(eng, seed, variant, recompute):
+    rng = np.random.default_rng(1000 + seed)
+    sizes = binned_sizes(rng)
+    snap = snapshot_with_sizes(rng, sizes, hetero=variant == "hetero", edge=variant == "edge")
+    if recompute:
+        for k in ("agg_count", "agg_sum_has", "agg_sum_wants"):
+            snap.pop(k)
+    gets, exp, res = run(eng, snap, recompute=recompute)
+    ref = O.apportion(snap, NOW)
+    label = f"seed={seed} {variant} recompute={recompute}"
+    assert_leases_match(snap, gets, exp, ref, label)
+    assert_resources_match(snap, res, ref, label)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fair_share_heavy_contention(eng, seed):
+    """Every resource FairShare, most clients above the equal share, some exactly at
+    round thresholds: exercises round 2 (algorithm.go:188-204) in every bin."""
+    rng = np.random.default_rng(2000 + seed)
+    sizes = binned_sizes(rng, per_bin=2)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(3,), hetero=seed % 2 == 1, expired_frac=0.0, learning_frac=0.0,
+                               parent_expired_frac=0.0)
+    n_of_row = np.maximum(np.repeat(sizes, sizes), 1)
+    cap = np.repeat(snap["capacity"], sizes)
+    snap["wants"] = np.where(rng.random(len(n_of_row)) < 0.7, rng.uniform(1.0, 4.0, len(n_of_row)),
+                             rng.uniform(0.0, 1.0, len(n_of_row))) * cap / n_of_row
+    W.add_store_sums(snap)
+    gets, exp, res = run(eng, snap)
+    ref = O.apportion(snap, NOW)
+    assert_leases_match(snap, gets, exp, ref, f"seed={seed}")
+    assert_resources_match(snap, res, ref)
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_small_resources_bit_exact(eng, seed):
+    """Resources of <= 16 rows go through the wave-packed literal path, which sums in
+    row order like the oracle: results are bit-identical, per-resource sums too."""
+    rng = np.random.default_rng(3000 + seed)
+    snap = snapshot_with_sizes(rng, rng.integers(0, 17, 3000), hetero=seed % 2 == 1, edge=seed >= 3)
+    if seed == 2:
+        for k in ("agg_count", "agg_sum_has", "agg_sum_wants"):
+            snap.pop(k)
+    gets, exp, res = run(eng, snap, recompute=seed == 2)
+    ref = O.apportion(snap, NOW)
+    np.testing.assert_array_equal(exp, ref["expiry_ns"])
+    assert float_close(gets, ref["gets"], 0.0, tol=0.0).all()
+    np.testing.assert_array_equal(res["count"], ref["res_count"])
+    for a, b in (("sum_has", "res_sum_has"), ("sum_wants", "res_sum_wants"), ("safe_capacity", "res_safe_capacity")):
+        assert float_close(res[a], ref[b], 0.0, tol=0.0).all(), a
+
+
+def test_deterministic(eng):
+    rng = np.random.default_rng(7)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng), hetero=True)
+    g1, e1, r1 = run(eng, snap)
+    g2, e2, r2 = run(eng, snap)
+    assert g1.tobytes() == g2.tobytes() and e1.tobytes() == e2.tobytes()
+    assert r1["sum_has"].tobytes() == r2["sum_has"].tobytes()
+
+
+def test_writeback_updates_store_like_assign(eng):
+    """DM_WRITEBACK: has := gets, expiry := now + lease, released rows zeroed and
+    the running sums updated (store.go:142-167); a second tick on the written-back
+    store matches the oracle on that store."""
+    rng = np.random.default_rng(11)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng), expired_frac=0.1)
+    ref = O.apportion(snap, NOW)
+    eng.load(snap)
+    eng.apportion(NOW, writeback=True)
+    st = eng.read_store()
+    live = ref["expiry_ns"] != W.RELEASED
+    assert float_close(st["has"], np.where(live, ref["gets"], 0.0), np.repeat(snap["capacity"],
+                       np.diff(snap["seg_off"]))).all()
+    np.testing.assert_array_equal(st["expiry_ns"], ref["expiry_ns"])
+    assert (st["wants"][~live] == 0).all() and (st["subclients"][~live] == 0).all()
+    res = eng.resources()
+    assert_resources_match(snap, res, ref)
+    # second tick, later clock, on the device store as it now stands
+    snap2 = dict(snap)
+    snap2.update(has=st["has"], wants=st["wants"], subclients=st["subclients"], expiry_ns=st["expiry_ns"],
+                 agg_count=res["count"], agg_sum_has=res["sum_has"], agg_sum_wants=res["sum_wants"])
+    now2 = NOW + 200 * W.NS
+    ref2 = O.apportion(snap2, now2)
+    eng.apportion(now2, writeback=False)
+    g2, e2 = eng.leases()
+    assert_leases_match(snap2, g2, e2, ref2, "second tick")
+
+
+def test_upsert_and_release(eng):
+    """Assign / Release on the device store keep the running sums (store.go:142-167)."""
+    rng = np.random.default_rng(12)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=False), expired_frac=0.0)
+    eng.load(snap)
+    N = len(snap["wants"])
+    rows = rng.choice(N, N // 10, replace=False)
+    new_w = rng.uniform(0, 50, len(rows))
+    new_h = rng.uniform(0, 5, len(rows))
+    new_s = np.ones(len(rows), np.int64)
+    new_e = np.full(len(rows), NOW + 100 * W.NS)
+    eng.upsert(rows, new_h, new_w, new_s, new_e)
+    gone = rng.choice(np.setdiff1d(np.arange(N), rows), N // 20, replace=False)
+    eng.release(gone)
+    # the same edits applied to the host snapshot
+    snap2 = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    seg_of = np.repeat(np.arange(len(snap["seg_off"]) - 1), np.diff(snap["seg_off"]))
+    for r, w, h, s, e in zip(rows, new_w, new_h, new_s, new_e):
+        g = seg_of[r]
+        snap2["agg_sum_has"][g] += h - snap2["has"][r]
+        snap2["agg_sum_wants"][g] += w - snap2["wants"][r]
+        snap2["agg_count"][g] += s - snap2["subclients"][r]
+        snap2["has"][r], snap2["wants"][r], snap2["subclients"][r], snap2["expiry_ns"][r] = h, w, s, e
+    for r in gone:
+        g = seg_of[r]
+        snap2["agg_sum_has"][g] -= snap2["has"][r]
+        snap2["agg_sum_wants"][g] -= snap2["wants"][r]
+        snap2["agg_count"][g] -= snap2["subclients"][r]
+        snap2["has"][r] = snap2["wants"][r] = 0.0
+        snap2["subclients"][r] = 0
+        snap2["expiry_ns"][r] = W.RELEASED
+    st = eng.read_store()
+    np.testing.assert_array_equal(st["expiry_ns"], snap2["expiry_ns"])
+    np.testing.assert_array_equal(st["wants"], snap2["wants"])
+    agg = eng.resources(safe=False)
+    np.testing.assert_array_equal(agg["count"], snap2["agg_count"])
+    assert float_close(agg["sum_wants"], snap2["agg_sum_wants"], np.maximum(snap["capacity"], 1e3), 1e-12).all()
+    eng.apportion(NOW)
+    gets, exp = eng.leases()
+    snap2["agg_sum_has"], snap2["agg_sum_wants"] = agg["sum_has"], agg["sum_wants"]
+    ref = O.apportion(snap2, NOW)
+    assert_leases_match(snap2, gets, exp, ref, "after upsert/release")
+
+
+def test_proto_form(eng):
+    """server.go:787-791: capacity, Expiry.Unix(), int64(RefreshInterval.Seconds())."""
+    rng = np.random.default_rng(13)
+    snap = snapshot_with_sizes(rng, np.array([5, 0, 70, 300]), expired_frac=0.2)
+    gets, exp, _ = run(eng, snap)
+    cap, exp_s, ref_s = eng.leases_proto()
+    assert cap.tobytes() == gets.tobytes()
+    live = exp != W.RELEASED
+    np.testing.assert_array_equal(exp_s[live], exp[live] // W.NS)
+    refresh_row = np.repeat(snap["refresh_interval_s"], np.diff(snap["seg_off"]))
+    np.testing.assert_array_equal(ref_s[live], refresh_row[live])
+
+
+def test_unknown_kind_rejected(eng):
+    from doorman_amd._lib import DM_E_KIND, DmError
+    snap = W.make_snapshot([2], [1.0, 2.0], 0.0, 1, NOW + W.NS, 9, 10.0)
+    with pytest.raises(DmError) as e:
+        eng.load(snap)
+    assert e.value.code == DM_E_KIND
+
+
+def _sample_check(eng, snap, resources, label):
+    gets, exp = eng.leases()
+    res = eng.resources()
+    sub = W.subset(snap, resources)
+    ref = O.apportion(sub, NOW)
+    so = snap["seg_off"]
+    rows = np.concatenate([np.arange(so[r], so[r + 1]) for r in resources])
+    assert_leases_match(sub, gets[rows], exp[rows], ref, label)
+    assert_resources_match(sub, {k: v[resources] for k, v in res.items()}, ref, label)
+
+
+@pytest.mark.parametrize("kind", [W.FAIR_SHARE, W.PROPORTIONAL_SHARE])
+def test_c1_full_size_sampled(eng, kind):
+    """configs[1]: 10k resources x 1k clients (10M leases), sampled against the oracle."""
+    snap = W.c1(kind=kind)
+    eng.load(snap)
+    eng.apportion(NOW)
+    rng = np.random.default_rng(5)
+    _sample_check(eng, snap, np.sort(rng.choice(10_000, 48, replace=False)), f"C1 kind={kind}")
+
+
+def test_c2_zipf_full_size_sampled(eng):
+    """configs[2]: 1M resources, Zipf 1..1M clients, mixed kinds, 5% learning."""
+    snap = W.c2()
+    eng.load(snap)
+    info = eng.plan_info()
+    assert info["leases"] == 13_970_034 and info["large_resources"] > 0 and info["small_packs"] > 0
+    eng.apportion(NOW)
+    rng = np.random.default_rng(6)
+    sample = np.unique(np.concatenate([[0, 1, 2, 3, 7, 100, 121, 122, 243, 244],
+                                       rng.choice(1_000_000, 300, replace=False)]))
+    _sample_check(eng, snap, sample, "C2")
