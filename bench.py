@@ -60,7 +60,7 @@ def kernel_units(eng, snap):
     sizes = np.diff(so)
     units = {}
     edges = [("wave64x1", 17, 64), ("block256x1", 65, 256), ("block256x2", 257, 512), ("block256x4", 513, 1024),
-             ("block256x8", 1025, 2048), ("block256x16", 2049, 4096)]
+             ("block512x4", 1025, 2048), ("block1024x4", 2049, 4096)]
     small = sizes <= 16
     units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
     for name, lo, hi in edges:

@@ -10,12 +10,13 @@ constexpr int64_t kNs = 1000000000LL;
 // Dispatch bins.  A segment of n rows goes to:
 //   n <= kSmallMax            : wave-packed literal path (many resources per wave)
 //   n <= 64                   : one wave per resource (64x1)
-//   n <= 256 * R, R=1..16     : one 256-thread workgroup per resource, R rows per thread in VGPRs
-//   n >  256 * 16 = kLargeMin : multi-workgroup chunks of kChunkRows rows
+//   n <= 1024                 : one 256-thread workgroup, R = 1, 2, 4 rows per thread in VGPRs
+//   n <= 2048 / 4096          : one 512- / 1024-thread workgroup, 4 rows per thread
+//   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
 constexpr int kSmallMax = 16;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 4096;
-constexpr int kNumBins = 6;  // 64x1, 256x1, 256x2, 256x4, 256x8, 256x16
+constexpr int kNumBins = 6;  // 64x1, 256x1, 256x2, 256x4, 512x4, 1024x4
 
 struct Pack {  // a run of consecutive small resources covering <= 64 rows
   int32_t first_seg;
@@ -42,10 +43,13 @@ struct LargeSeg {
 
 // Per-chunk partial results of the large path (one slot per chunk).
 struct Partials {
-  // pass A: live (recompute) or expired (parity) sums, plus uniformity flags
+  // pass A: expired-row sums, all-row sums (recompute mode), uniformity flags
   int64_t* a_cnt;
   double* a_has;
   double* a_wants;
+  int64_t* a_cnt_all;
+  double* a_has_all;
+  double* a_wants_all;
   int64_t* a_smin;
   int64_t* a_smax;
   int32_t* a_nan;

@@ -85,28 +85,48 @@ __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
     if ((threadIdx.x & 63) == 0) lds[w] = v;
     __syncthreads();
     T r = lds[0];
-#pragma unroll
-    for (int i = 1; i < G / 64; ++i) r = op(r, lds[i]);
+#pragma unroll 3
+    for (int i = 1; i < G / 64; ++i) {
+      const T x = lds[i];
+      r = op(r, x);
+    }
     __syncthreads();
     return r;
   }
 }
 
-struct AggA {
+struct AggR {  // every row: the store's sums rebuilt by Assign (recompute mode)
   long long cnt;
   double h;
   double w;
+};
+struct OpR {
+  __device__ AggR operator()(AggR a, AggR b) const {
+    AggR r;
+    r.cnt = a.cnt + b.cnt;
+    r.h = a.h + b.h;
+    r.w = a.w + b.w;
+    return r;
+  }
+};
+
+struct AggA {
+  long long cnt;  // leases Clean releases (expired rows)
+  double h;
+  double w;
+  AggR all;       // filled in recompute mode only
   long long smin;
   long long smax;
   int nan;
   int pad;
 };
 struct OpA {
-  __device__ AggA operator()(const AggA& a, const AggA& b) const {
+  __device__ AggA operator()(AggA a, AggA b) const {
     AggA r;
     r.cnt = a.cnt + b.cnt;
     r.h = a.h + b.h;
     r.w = a.w + b.w;
+    r.all = a.all;
     r.smin = a.smin < b.smin ? a.smin : b.smin;
     r.smax = a.smax > b.smax ? a.smax : b.smax;
     r.nan = a.nan | b.nan;
@@ -119,6 +139,7 @@ __device__ __forceinline__ AggA zeroA() {
   a.cnt = 0;
   a.h = 0.0;
   a.w = 0.0;
+  a.all = AggR{0, 0.0, 0.0};
   a.smin = INT64_MAX;
   a.smax = INT64_MIN;
   a.nan = 0;
@@ -132,7 +153,7 @@ struct AggB {
   long long i; // FS: wantExtra (W)
 };
 struct OpB {
-  __device__ AggB operator()(const AggB& a, const AggB& b) const {
+  __device__ AggB operator()(AggB a, AggB b) const {
     AggB r;
     r.x = a.x + b.x;
     r.y = a.y + b.y;
@@ -146,7 +167,7 @@ struct AggC {
   long long sgt;  // sum of subclients of wantExtraClients above T
 };
 struct OpC {
-  __device__ AggC operator()(const AggC& a, const AggC& b) const {
+  __device__ AggC operator()(AggC a, AggC b) const {
     AggC r;
     r.ee = a.ee + b.ee;
     r.sgt = a.sgt + b.sgt;
@@ -160,23 +181,32 @@ struct TMin {
   int pad;
 };
 struct OpTMin {
-  __device__ TMin operator()(const TMin& a, const TMin& b) const {
-    if (!b.found) return a;
-    if (!a.found) return b;
-    return b.t < a.t ? b : a;
+  __device__ TMin operator()(TMin a, TMin b) const {
+    const bool take_b = b.found && (!a.found || b.t < a.t);
+    TMin r;
+    r.t = take_b ? b.t : a.t;
+    r.found = a.found | b.found;
+    r.pad = 0;
+    return r;
   }
 };
+__device__ __forceinline__ void tmin_add(TMin& m, double T) {
+  const bool take = !m.found || T < m.t;
+  m.t = take ? T : m.t;
+  m.found = 1;
+}
 
 struct SumD {
   double v;
 };
 struct OpSumD {
-  __device__ SumD operator()(const SumD& a, const SumD& b) const { return SumD{a.v + b.v}; }
+  __device__ SumD operator()(SumD a, SumD b) const { return SumD{a.v + b.v}; }
 };
 
 template <int G>
 struct Lds {
   AggA a[G / 64];
+  AggR r[G / 64];
   AggB b[G / 64];
   AggC c[G / 64];
   TMin t[G / 64];
@@ -190,12 +220,13 @@ struct Clean {
   double sum_wants;
 };
 __device__ __forceinline__ Clean clean_from(const DevParams& p, int seg, const AggA& a) {
+  // store sums (running, or rebuilt from every row) minus the leases Clean releases
   Clean c;
   if (p.recompute) {
-    c.count = a.cnt;
-    c.sum_has = a.h;
-    c.sum_wants = a.w;
-  } else {  // running sums minus the leases Clean releases
+    c.count = a.all.cnt - a.cnt;
+    c.sum_has = a.all.h - a.h;
+    c.sum_wants = a.all.w - a.w;
+  } else {
     c.count = p.agg_count[seg] - a.cnt;
     c.sum_has = p.agg_sum_has[seg] - a.h;
     c.sum_wants = p.agg_sum_wants[seg] - a.w;
@@ -248,9 +279,18 @@ __device__ __forceinline__ double fs_stage2(double w, double h, long long s, dou
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
 template <int G, int R>
-__device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t, Lds<G>& lds) {
+__device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t, Lds<G>& lds,
+                                              int32_t* general_list, int32_t* general_count) {
   const int64_t lo = p.seg_off[seg];
   const int n = (int)(p.seg_off[seg + 1] - lo);
+  // wave-uniform bases + 32-bit per-lane offsets: one VGPR addresses every column
+  const double* __restrict__ wb = p.wants + lo;
+  const double* __restrict__ hb = p.has + lo;
+  const int64_t* __restrict__ sb = p.sub + lo;
+  const int64_t* __restrict__ eb = p.expiry + lo;
+  double* gb = p.out_gets + lo;
+  int64_t* xb = p.out_expiry + lo;
+  // the rows stay in VGPRs for every pass: 6 registers per row
   double w[R], h[R];
   long long s[R];
   unsigned valid = 0, live = 0;
@@ -261,11 +301,11 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
     h[k] = 0.0;
     s[k] = 0;
     if (i < n) {
-      const int64_t row = lo + i;
-      w[k] = p.wants[row];
-      h[k] = p.has[row];
-      s[k] = p.sub[row];
-      const int64_t e = p.expiry[row];
+      const unsigned u = (unsigned)i;
+      w[k] = wb[u];
+      h[k] = hb[u];
+      s[k] = sb[u];
+      const int64_t e = eb[u];
       valid |= 1u << k;
       if (!(p.now > e)) live |= 1u << k;  // store.go:174 when.After(expiry)
     }
@@ -278,10 +318,15 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
   for (int k = 0; k < R; ++k) {
     if (!(valid >> k & 1)) continue;
     const bool lv = live >> k & 1;
-    if (p.recompute ? lv : !lv) {
+    if (!lv) {
       a.cnt += s[k];
       a.h += h[k];
       a.w += w[k];
+    }
+    if (p.recompute) {
+      a.all.cnt += s[k];
+      a.all.h += h[k];
+      a.all.w += w[k];
     }
     if (lv) {
       a.smin = s[k] < a.smin ? s[k] : a.smin;
@@ -289,162 +334,124 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
       a.nan |= __builtin_isnan(w[k]) ? 1 : 0;
     }
   }
-  a = group_reduce<G>(a, OpA(), lds.a);
+  {
+    const AggR all_part = a.all;
+    a = group_reduce<G>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce<G>(all_part, OpR(), lds.r);
+  }
   const Clean cl = clean_from(p, seg, a);
   const double C = rs.C;
-
-  double g[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) g[k] = 0.0;
-
-  if (rs.learning) {  // Learn (algorithm.go:297-302)
-#pragma unroll
-    for (int k = 0; k < R; ++k) g[k] = h[k];
-  } else if (rs.kind == 0) {  // NoAlgorithm
-#pragma unroll
-    for (int k = 0; k < R; ++k) g[k] = w[k];
-  } else if (rs.kind == 1) {  // Static
-#pragma unroll
-    for (int k = 0; k < R; ++k) g[k] = minF(C, w[k]);
-  } else if (rs.kind == 2) {  // ProportionalShare
-    const double eq = C / (double)cl.count;  // :229
-    AggB b{0.0, 0.0, 0};
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      if (!(live >> k & 1)) continue;
-      const double e = eq * (double)s[k];  // :273
-      if (w[k] < e)
-        b.x += e - w[k];  // :275
-      else
-        b.y += w[k] - e;  // :277
-    }
-    b = group_reduce<G>(b, OpB(), lds.b);
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const double epc = eq * (double)s[k];           // :233
-      const double unused = C - cl.sum_has + h[k];    // :239
-      if (cl.sum_wants <= C || w[k] <= epc)           // :245
-        g[k] = minF(w[k], unused);
-      else
-        g[k] = minF(epc + (w[k] - epc) * (b.x / b.y), unused);  // :283,290
-    }
-  } else {  // FairShare
-    const double eq = C / (double)cl.count;  // :123
-    AggB b{0.0, 0.0, 0};
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      if (!(live >> k & 1)) continue;
-      const double d = (double)s[k] * eq;  // :160
-      if (w[k] < d)
-        b.x += d - w[k];  // :164
-      else if (w[k] > d)
-        b.i += s[k];  // :168
-    }
-    b = group_reduce<G>(b, OpB(), lds.b);
-    unsigned need2 = 0;
-    double T[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      T[k] = 0.0;
-      if (!(live >> k & 1)) continue;
-      if (!fs_stage01(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, &g[k], &T[k])) need2 |= 1u << k;
-    }
-    if (a.smin == a.smax && !a.nan) {
-      // uniform subclients: one threshold T for the whole resource
-      const double s0 = (double)a.smin;
-      const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
-      AggC c{0.0, 0};
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        if (!(live >> k & 1)) continue;
-        if (!(w[k] > (double)s[k] * eq)) continue;  // j in wantExtraClients (:165-169)
-        if (w[k] < Tu)
-          c.ee += Tu - w[k];  // :197-198
-        else if (w[k] > Tu)
-          c.sgt += s[k];  // :199-200
-      }
-      c = group_reduce<G>(c, OpC(), lds.c);
-#pragma unroll
-      for (int k = 0; k < R; ++k)
-        if (need2 >> k & 1) g[k] = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, T[k], c);
-    } else {
-      // heterogeneous subclients (GetServerCapacity, server.go:850-879) or NaN wants:
-      // one round-2 reduction per distinct threshold, smallest first.
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        if ((need2 >> k & 1) && __builtin_isnan(T[k])) {
-          const AggC none{0.0, 0};
-          g[k] = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, T[k], none);
-          need2 &= ~(1u << k);
-        }
-      }
-      for (;;) {
-        TMin tm{0.0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < R; ++k)
-          if ((need2 >> k & 1) && (!tm.found || T[k] < tm.t)) tm = TMin{T[k], 1, 0};
-        tm = group_reduce<G>(tm, OpTMin(), lds.t);
-        if (!tm.found) break;
-        const double Ts = tm.t;
-        AggC c{0.0, 0};
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          if (!(live >> k & 1)) continue;
-          if (!(w[k] > (double)s[k] * eq)) continue;
-          if (w[k] < Ts)
-            c.ee += Ts - w[k];
-          else if (w[k] > Ts)
-            c.sgt += s[k];
-        }
-        c = group_reduce<G>(c, OpC(), lds.c);
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          if ((need2 >> k & 1) && T[k] == Ts) {
-            g[k] = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, T[k], c);
-            need2 &= ~(1u << k);
-          }
-        }
-      }
-    }
+  const double eq = C / (double)cl.count;  // algorithm.go:123,229 equalShare
+  const bool ps = !rs.learning && rs.kind == 2;
+  const bool fs = !rs.learning && rs.kind == 3;
+  const bool fs_uniform = fs && a.smin >= a.smax && !a.nan;  // no live rows counts as uniform
+  if (fs && !fs_uniform) {
+    // heterogeneous subclients (GetServerCapacity, server.go:850-879) or NaN wants:
+    // one round-2 threshold per distinct subclient count.  Rare (the hierarchy's
+    // root level), so the whole resource goes to k_general, untouched here.
+    if (t == 0) general_list[atomicAdd(general_count, 1)] = seg;
+    return;
   }
 
-  // ---- map: write the leases (store.go:153-167 Assign; released rows get none) ----
+  // ---- pass B: ProportionalShare extraCapacity/extraNeed, FairShare round 1 ----
+  AggB b{0.0, 0.0, 0};
+  if (ps || fs) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (!(live >> k & 1)) continue;
+      if (ps) {
+        const double e = eq * (double)s[k];  // :273
+        if (w[k] < e)
+          b.x += e - w[k];  // :275
+        else
+          b.y += w[k] - e;  // :277
+      } else {
+        const double d = (double)s[k] * eq;  // :160
+        if (w[k] < d)
+          b.x += d - w[k];  // :164
+        else if (w[k] > d)
+          b.i += s[k];  // :168
+      }
+    }
+    b = group_reduce<G>(b, OpB(), lds.b);
+  }
+
+  // ---- pass C (uniform subclients): FairShare round 2 at the resource's one threshold ----
+  AggC cu{0.0, 0};
+  double Tu = 0.0;
+  if (fs_uniform) {
+    const double s0 = (double)a.smin;
+    Tu = (b.x / (double)b.i) * s0 + eq * s0;  // deservedExtra + deservedShare (:175,:126)
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (!(live >> k & 1)) continue;
+      if (!(w[k] > (double)s[k] * eq)) continue;  // j in wantExtraClients (:165-169)
+      if (w[k] < Tu)
+        cu.ee += Tu - w[k];  // :197-198
+      else if (w[k] > Tu)
+        cu.sgt += s[k];  // :199-200
+    }
+    cu = group_reduce<G>(cu, OpC(), lds.c);
+  }
+
+  // ---- map: decide and write every lease (store.go:153-167 Assign) ----
   SumD delta{0.0};
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     if (!(valid >> k & 1)) continue;
-    const int64_t row = lo + k * G + t;
-    if (live >> k & 1) {
-      p.out_gets[row] = g[k];
-      p.out_expiry[row] = rs.exp_out;
-      delta.v += g[k] - h[k];
-    } else {
-      p.out_gets[row] = 0.0;
-      p.out_expiry[row] = kReleased;
+    const unsigned u = (unsigned)(k * G + t);
+    if (!(live >> k & 1)) {  // released by Clean: no lease
+      gb[u] = 0.0;
+      xb[u] = kReleased;
       if (p.out_wants) {
-        p.out_wants[row] = 0.0;
-        p.out_sub[row] = 0;
+        p.out_wants[lo + u] = 0.0;
+        p.out_sub[lo + u] = 0;
+      }
+      continue;
+    }
+    double g;
+    if (rs.learning) {
+      g = h[k];  // Learn (algorithm.go:297-302)
+    } else if (rs.kind == 0) {
+      g = w[k];  // NoAlgorithm
+    } else if (rs.kind == 1) {
+      g = minF(C, w[k]);  // Static
+    } else if (ps) {
+      const double epc = eq * (double)s[k];         // :233
+      const double unused = C - cl.sum_has + h[k];  // :239
+      g = (cl.sum_wants <= C || w[k] <= epc) ? minF(w[k], unused)            // :245
+                                             : minF(epc + (w[k] - epc) * (b.x / b.y), unused);  // :283
+    } else {
+      double T = 0.0;
+      if (!fs_stage01(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, &g, &T)) {
+        g = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, Tu, cu);
       }
     }
+    gb[u] = g;
+    xb[u] = rs.exp_out;
+    delta.v += g - h[k];
   }
+
   delta = group_reduce<G>(delta, OpSumD(), lds.d);
   if (t == 0) write_resource(p, seg, rs, cl, delta.v);
 }
 
-// 256-thread workgroup per resource.
-template <int R>
-__global__ __launch_bounds__(256) void k_block(DevParams p, const int32_t* __restrict__ segs, int nsegs) {
-  __shared__ Lds<256> lds;
+// One G-thread workgroup per resource (G = 256..1024, R <= 4 rows per thread).
+template <int G, int R>
+__global__ __launch_bounds__(G) void k_block(DevParams p, const int32_t* __restrict__ segs, int nsegs,
+                                             int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nsegs) return;
-  group_segment<256, R>(p, segs[blockIdx.x], threadIdx.x, lds);
+  group_segment<G, R>(p, segs[blockIdx.x], threadIdx.x, lds, general_list, general_count);
 }
 
 // One wave per resource (n <= 64), four independent waves per workgroup.
-__global__ __launch_bounds__(256) void k_wave(DevParams p, const int32_t* __restrict__ segs, int nsegs) {
+__global__ __launch_bounds__(256) void k_wave(DevParams p, const int32_t* __restrict__ segs, int nsegs,
+                                              int32_t* general_list, int32_t* general_count) {
   Lds<64> lds;  // unused by wave reductions
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nsegs) return;
-  group_segment<64, 1>(p, segs[i], threadIdx.x & 63, lds);
+  group_segment<64, 1>(p, segs[i], threadIdx.x & 63, lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -639,18 +646,25 @@ __device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials
     x.cnt = P.a_cnt[c];
     x.h = P.a_has[c];
     x.w = P.a_wants[c];
+    x.all = AggR{P.a_cnt_all[c], P.a_has_all[c], P.a_wants_all[c]};
     x.smin = P.a_smin[c];
     x.smax = P.a_smax[c];
     x.nan = P.a_nan[c];
     x.pad = 0;
+    const AggR all = OpR()(a.all, x.all);  // OpA carries `all` through unchanged
     a = OpA()(a, x);
+    a.all = all;
   }
-  a = group_reduce<G>(a, OpA(), lds.a);
+  {
+    const AggR all_part = a.all;
+    a = group_reduce<G>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce<G>(all_part, OpR(), lds.r);
+  }
   SegState st;
   st.a = a;
   st.cl = clean_from(p, L.seg, a);
   st.rs = load_res(p, L.seg);
-  st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin == a.smax && !a.nan)) ? 1 : 0;
+  st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin >= a.smax && !a.nan)) ? 1 : 0;
   return st;
 }
 
@@ -677,10 +691,15 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
     const double w = p.wants[row], h = p.has[row];
     const long long s = p.sub[row];
     const bool lv = !(p.now > p.expiry[row]);
-    if (p.recompute ? lv : !lv) {
+    if (!lv) {
       a.cnt += s;
       a.h += h;
       a.w += w;
+    }
+    if (p.recompute) {
+      a.all.cnt += s;
+      a.all.h += h;
+      a.all.w += w;
     }
     if (lv) {
       a.smin = s < a.smin ? s : a.smin;
@@ -688,10 +707,17 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
       a.nan |= __builtin_isnan(w) ? 1 : 0;
     }
   }
-  a = group_reduce<256>(a, OpA(), lds.a);
+  {
+    const AggR all_part = a.all;
+    a = group_reduce<256>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
+  }
   if (threadIdx.x == 0) {
     const int c = blockIdx.x;
     P.a_cnt[c] = a.cnt;
+    P.a_cnt_all[c] = a.all.cnt;
+    P.a_has_all[c] = a.all.h;
+    P.a_wants_all[c] = a.all.w;
     P.a_has[c] = a.h;
     P.a_wants[c] = a.w;
     P.a_smin[c] = a.smin;
@@ -818,112 +844,145 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
 }
 
-__global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P) {
+__global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P,
+                                                   int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<256> lds;
   const LargeSeg L = ls[blockIdx.x];
   const SegState st = seg_state<256>(p, P, L, lds);
-  if (st.general) return;
+  if (st.general) {
+    if (threadIdx.x == 0) general_list[atomicAdd(general_count, 1)] = L.seg;
+    return;
+  }
   SumD d{0.0};
   for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 256) d.v += P.d_delta[c];
   d = group_reduce<256>(d, OpSumD(), lds.d);
   if (threadIdx.x == 0) write_resource(p, L.seg, st.rs, st.cl, d.v);
 }
 
-// General FairShare for a large resource with heterogeneous subclients or NaN
-// wants: one workgroup streams the resource, one round-2 pass per distinct
-// threshold in increasing order.  Correct for any size; only the hierarchy's
-// root level produces such resources, and those are small.
-__global__ __launch_bounds__(256) void k_general(DevParams p, const LargeSeg* __restrict__ ls, Partials P) {
+// General FairShare: resources with heterogeneous subclients or NaN wants, from
+// any size bin (appended to the worklist by the other kernels, which leave such
+// a resource untouched).  One workgroup streams the resource: Clean, round 1,
+// then one round-2 pass per distinct threshold in increasing order.  Only the
+// hierarchy's root level (GetServerCapacity) produces such resources.
+__global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __restrict__ list,
+                                                 const int32_t* __restrict__ count) {
   __shared__ Lds<256> lds;
-  const LargeSeg L = ls[blockIdx.x];
-  const SegState st = seg_state<256>(p, P, L, lds);
-  if (!st.general) return;
-  const int64_t lo = p.seg_off[L.seg], hi = p.seg_off[L.seg + 1];
-  const double C = st.rs.C;
-  const double eq = C / (double)st.cl.count;
-  // round 1 sums
-  AggB b{0.0, 0.0, 0};
-  for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
-    if (p.now > p.expiry[row]) continue;
-    const double w = p.wants[row];
-    const long long s = p.sub[row];
-    const double d = (double)s * eq;
-    if (w < d)
-      b.x += d - w;
-    else if (w > d)
-      b.i += s;
-  }
-  b = group_reduce<256>(b, OpB(), lds.b);
-  // rows decided in round 0/1, released rows, NaN thresholds
-  SumD delta{0.0};
-  for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
-    const double w = p.wants[row], h = p.has[row];
-    const long long s = p.sub[row];
-    if (p.now > p.expiry[row]) {
-      p.out_gets[row] = 0.0;
-      p.out_expiry[row] = kReleased;
-      if (p.out_wants) {
-        p.out_wants[row] = 0.0;
-        p.out_sub[row] = 0;
-      }
-      continue;
-    }
-    double g, T = 0.0;
-    bool done = fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &T);
-    if (!done && __builtin_isnan(T)) {
-      g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, T, AggC{0.0, 0});
-      done = true;
-    }
-    if (done) {
-      p.out_gets[row] = g;
-      p.out_expiry[row] = st.rs.exp_out;
-      delta.v += g - h;
-    }
-  }
-  // round 2, one distinct threshold at a time
-  double prev = 0.0;
-  int have_prev = 0;
-  for (;;) {
-    TMin tm{0.0, 0, 0};
+  const int nlist = *count;
+  for (int idx = blockIdx.x; idx < nlist; idx += gridDim.x) {
+    const int seg = list[idx];
+    const int64_t lo = p.seg_off[seg], hi = p.seg_off[seg + 1];
+    const Res rs = load_res(p, seg);
+    AggA a = zeroA();
     for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
-      if (p.now > p.expiry[row]) continue;
-      double g, T = 0.0;
-      if (fs_stage01(p.wants[row], p.has[row], p.sub[row], C, st.cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
-      if (__builtin_isnan(T) || (have_prev && !(T > prev))) continue;
-      if (!tm.found || T < tm.t) tm = TMin{T, 1, 0};
+      const double w = p.wants[row], h = p.has[row];
+      const long long s = p.sub[row];
+      const bool lv = !(p.now > p.expiry[row]);
+      if (!lv) {
+        a.cnt += s;
+        a.h += h;
+        a.w += w;
+      }
+      if (p.recompute) {
+        a.all.cnt += s;
+        a.all.h += h;
+        a.all.w += w;
+      }
     }
-    tm = group_reduce<256>(tm, OpTMin(), lds.t);
-    if (!tm.found) break;
-    const double Ts = tm.t;
-    AggC c{0.0, 0};
+    {
+    const AggR all_part = a.all;
+    a = group_reduce<256>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
+  }
+    const Clean cl = clean_from(p, seg, a);
+    const double C = rs.C;
+    const double eq = C / (double)cl.count;
+    // round 1 sums (algorithm.go:156-171)
+    AggB b{0.0, 0.0, 0};
     for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
       if (p.now > p.expiry[row]) continue;
       const double w = p.wants[row];
       const long long s = p.sub[row];
-      if (!(w > (double)s * eq)) continue;
-      if (w < Ts)
-        c.ee += Ts - w;
-      else if (w > Ts)
-        c.sgt += s;
+      const double d = (double)s * eq;
+      if (w < d)
+        b.x += d - w;
+      else if (w > d)
+        b.i += s;
     }
-    c = group_reduce<256>(c, OpC(), lds.c);
+    b = group_reduce<256>(b, OpB(), lds.b);
+    // rows decided in round 0/1, released rows, NaN thresholds
+    SumD delta{0.0};
     for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
-      if (p.now > p.expiry[row]) continue;
       const double w = p.wants[row], h = p.has[row];
       const long long s = p.sub[row];
+      if (p.now > p.expiry[row]) {
+        p.out_gets[row] = 0.0;
+        p.out_expiry[row] = kReleased;
+        if (p.out_wants) {
+          p.out_wants[row] = 0.0;
+          p.out_sub[row] = 0;
+        }
+        continue;
+      }
       double g, T = 0.0;
-      if (fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
-      if (!(T == Ts)) continue;
-      g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, T, c);
-      p.out_gets[row] = g;
-      p.out_expiry[row] = st.rs.exp_out;
-      delta.v += g - h;
+      bool done = fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T);
+      if (!done && __builtin_isnan(T)) {
+        g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, AggC{0.0, 0});
+        done = true;
+      }
+      if (done) {
+        p.out_gets[row] = g;
+        p.out_expiry[row] = rs.exp_out;
+        delta.v += g - h;
+      }
     }
-    prev = Ts;
-    have_prev = 1;
+    // round 2 (algorithm.go:188-204), one distinct threshold at a time.  The rows
+    // written above keep their inputs in registers only within their own pass, so
+    // round 2 re-reads has from a resource that is already partly written back:
+    // only rows that are still undecided are read, and those are untouched.
+    double prev = 0.0;
+    int have_prev = 0;
+    for (;;) {
+      TMin tm{0.0, 0, 0};
+      for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+        if (p.now > p.expiry[row]) continue;
+        double g, T = 0.0;
+        if (fs_stage01(p.wants[row], p.has[row], p.sub[row], C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+        if (__builtin_isnan(T) || (have_prev && !(T > prev))) continue;
+        tmin_add(tm, T);
+      }
+      tm = group_reduce<256>(tm, OpTMin(), lds.t);
+      if (!tm.found) break;
+      const double Ts = tm.t;
+      AggC c{0.0, 0};
+      for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+        if (p.now > p.expiry[row]) continue;
+        const double w = p.wants[row];
+        const long long s = p.sub[row];
+        if (!(w > (double)s * eq)) continue;
+        if (w < Ts)
+          c.ee += Ts - w;
+        else if (w > Ts)
+          c.sgt += s;
+      }
+      c = group_reduce<256>(c, OpC(), lds.c);
+      for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+        if (p.now > p.expiry[row]) continue;
+        const double w = p.wants[row], h = p.has[row];
+        const long long s = p.sub[row];
+        double g, T = 0.0;
+        if (fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+        if (!(T == Ts)) continue;
+        g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, c);
+        p.out_gets[row] = g;
+        p.out_expiry[row] = rs.exp_out;
+        delta.v += g - h;
+      }
+      prev = Ts;
+      have_prev = 1;
+    }
+    delta = group_reduce<256>(delta, OpSumD(), lds.d);
+    if (threadIdx.x == 0) write_resource(p, seg, rs, cl, delta.v);
   }
-  delta = group_reduce<256>(delta, OpSumD(), lds.d);
-  if (threadIdx.x == 0) write_resource(p, L.seg, st.rs, st.cl, delta.v);
 }
 
 // --------------------------------------------------------------------------
@@ -988,32 +1047,39 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, hipStream_t st) {
+hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, int32_t* glist, int32_t* gcount,
+                      hipStream_t st) {
   if (n <= 0) return hipSuccess;
   switch (bin) {
-    case 0: k_wave<<<(n + 3) / 4, 256, 0, st>>>(p, segs, n); break;
-    case 1: k_block<1><<<n, 256, 0, st>>>(p, segs, n); break;
-    case 2: k_block<2><<<n, 256, 0, st>>>(p, segs, n); break;
-    case 3: k_block<4><<<n, 256, 0, st>>>(p, segs, n); break;
-    case 4: k_block<8><<<n, 256, 0, st>>>(p, segs, n); break;
-    case 5: k_block<16><<<n, 256, 0, st>>>(p, segs, n); break;
+    case 0: k_wave<<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 1: k_block<256, 1><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 2: k_block<256, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 3: k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 4: k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 5: k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
-                        const Partials& P, hipStream_t st) {
+                        const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st) {
   if (nchunks <= 0) return hipSuccess;
   switch (phase) {
     case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
     case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
-    case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P); break;
-    case 5: k_general<<<nls, 256, 0, st>>>(p, ls, P); break;
+    case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
+                          hipStream_t st) {
+  if (blocks <= 0) return hipSuccess;
+  k_general<<<blocks, 256, 0, st>>>(p, glist, gcount);
   return hipGetLastError();
 }
 

@@ -17,9 +17,12 @@
 
 namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
-hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, hipStream_t st);
+hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, int32_t* glist, int32_t* gcount,
+                      hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
-                        const Partials& P, hipStream_t st);
+                        const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
+hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
+                          hipStream_t st);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
                          int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
@@ -51,7 +54,7 @@ enum KClass {
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "wave64x1",   "block256x1", "block256x2",  "block256x4",
-                                     "block256x8",   "block256x16", "large_a",    "large_b",     "large_c",
+                                     "block512x4",   "block1024x4", "large_a",    "large_b",     "large_c",
                                      "large_map",    "large_fin",  "general",    "store_upsert", "store_release"};
 
 template <typename T>
@@ -120,9 +123,14 @@ struct dm_ctx {
   DBuf<Chunk> chunks;
   DBuf<LargeSeg> large;
   // large-path partials
-  DBuf<int64_t> pa_cnt, pa_smin, pa_smax, pb_w, pc_sgt;
-  DBuf<double> pa_has, pa_wants, pb_x, pb_y, pc_ee, pd_delta;
+  DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
+  DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
   DBuf<int32_t> pa_nan;
+  // worklist of resources for k_general (heterogeneous-subclient FairShare)
+  DBuf<int32_t> glist, gcount;
+  bool maybe_general = false;
+  bool all_sub_one = true;  // every loaded row had subclients == 1
+  int64_t n_nonsmall = 0;
   // staging for upsert / release
   DBuf<int64_t> st_rows, st_sub, st_exp;
   DBuf<double> st_has, st_wants;
@@ -172,9 +180,10 @@ struct dm_ctx {
     out_gets.release(); out_expiry.release(); res_count.release(); res_sum_has.release();
     res_sum_wants.release(); res_safe.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
-    pa_cnt.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
+    pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
     pa_nan.release();
+    glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release(); st_seg.release();
   }
 };
@@ -262,6 +271,9 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
+  DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
+  DM_HIP(c, c->pa_has_all.ensure(nc), "partials");
+  DM_HIP(c, c->pa_wants_all.ensure(nc), "partials");
   DM_HIP(c, c->pa_smin.ensure(nc), "partials");
   DM_HIP(c, c->pa_smax.ensure(nc), "partials");
   DM_HIP(c, c->pb_w.ensure(nc), "partials");
@@ -273,7 +285,24 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pc_ee.ensure(nc), "partials");
   DM_HIP(c, c->pd_delta.ensure(nc), "partials");
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
+  c->n_nonsmall = 0;
+  for (int64_t r = 0; r < c->R; ++r)
+    if (c->h_seg_off[r + 1] - c->h_seg_off[r] > kSmallMax) ++c->n_nonsmall;
+  DM_HIP(c, c->glist.ensure((size_t)std::max<int64_t>(c->n_nonsmall, 1)), "worklist");
+  DM_HIP(c, c->gcount.ensure(1), "worklist");
   return DM_OK;
+}
+
+// Could some non-small resource need k_general (heterogeneous subclients or NaN
+// wants among its rows)?  Conservative: expiry is ignored.
+static bool scan_maybe_general(const int64_t* off, int64_t R, const int64_t* sub, const double* wants) {
+  for (int64_t r = 0; r < R; ++r) {
+    if (off[r + 1] - off[r] <= kSmallMax) continue;
+    const int64_t s0 = sub[off[r]];
+    for (int64_t i = off[r]; i < off[r + 1]; ++i)
+      if (sub[i] != s0 || std::isnan(wants[i])) return true;
+  }
+  return false;
 }
 
 template <typename T>
@@ -410,6 +439,9 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   build_plan(c);
   int rc = upload_plan(c);
   if (rc) return rc;
+  c->maybe_general = scan_maybe_general(s->seg_off, R, s->subclients, s->wants);
+  c->all_sub_one = true;
+  for (int64_t i = 0; i < N && c->all_sub_one; ++i) c->all_sub_one = s->subclients[i] == 1;
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
   c->have_result = false;
@@ -422,6 +454,10 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   if (!cfg || R < 0 || !cfg->kind || !cfg->capacity || !cfg->lease_length_s || !cfg->refresh_interval_s ||
       !cfg->learning_end_ns || !cfg->parent_expiry_ns || !cfg->safe_capacity)
     return c->fail(DM_E_INVAL, "bad config");
+  for (int64_t r = 0; r < R; ++r) {
+    if (cfg->lease_length_s[r] < 0 || cfg->refresh_interval_s[r] < 0)
+      return c->fail(DM_E_INVAL, "lease_length and refresh_interval must be >= 0 (server.go:384-434)");
+  }
   for (int64_t r = 0; r < R; ++r)
     if (cfg->kind[r] < DM_NO_ALGORITHM || cfg->kind[r] > DM_FAIR_SHARE) {
       char buf[96];
@@ -500,7 +536,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   p.now = now_ns;
   p.recompute = (flags & DM_AGG_RECOMPUTE) ? 1 : 0;
 
-  Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
+  Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
+             c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p};
   hipStream_t st = c->stream;
   auto timed = [&](int cls, auto&& fn) -> hipError_t {
@@ -513,18 +550,26 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     return e;
   };
   const int nch = (int)c->h_chunks.size(), nls = (int)c->h_large.size();
+  int32_t* gl = c->glist.p;
+  int32_t* gc = c->gcount.p;
+  if (c->maybe_general) DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
   // large resources first (longest dependency chain), then the binned groups
-  for (int ph = 0; ph < 6 && nch > 0; ++ph)
-    DM_HIP(c, timed(KC_LARGE_A + ph, [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, st); }),
+  for (int ph = 0; ph < 5 && nch > 0; ++ph)
+    DM_HIP(c, timed(KC_LARGE_A + ph,
+                    [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, st); }),
            "large-resource kernels");
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    DM_HIP(c, timed(KC_BIN0 + b, [&] { return launch_bin(b, p, c->bins[b].p, n, st); }), "group kernel");
+    DM_HIP(c, timed(KC_BIN0 + b, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, st); }), "group kernel");
   }
   if (!c->h_packs.empty())
     DM_HIP(c, timed(KC_SMALL, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), st); }),
            "small kernel");
+  if (c->maybe_general && c->n_nonsmall > 0) {
+    const int blocks = (int)std::min<int64_t>(c->n_nonsmall, 1024);
+    DM_HIP(c, timed(KC_GENERAL, [&] { return launch_general(p, gl, gc, blocks, st); }), "general kernel");
+  }
   c->last_writeback = wb;
   c->have_result = true;
   if (!(flags & DM_ASYNC)) {
@@ -638,6 +683,9 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
   DM_HIP(c, upload(c->st_sub, sub, (size_t)n, c->stream), "stage sub");
   DM_HIP(c, upload(c->st_exp, exp, (size_t)n, c->stream), "stage expiry");
+  // an upsert can make a resource's subclients heterogeneous: stay conservative
+  for (int64_t i = 0; i < n && !c->maybe_general; ++i)
+    if (std::isnan(wants[i]) || sub[i] != 1 || !c->all_sub_one) c->maybe_general = true;
   DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->st_seg.p,
                           c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg_count.p, c->agg_sum_has.p,
                           c->agg_sum_wants.p, c->stream),

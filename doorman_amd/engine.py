@@ -15,7 +15,7 @@ from . import _lib
 from ._lib import check, lib
 from .workloads import CFG_FIELDS
 
-_BIN_NAMES = ("small_packs", "wave64x1", "block256x1", "block256x2", "block256x4", "block256x8", "block256x16",
+_BIN_NAMES = ("small_packs", "wave64x1", "block256x1", "block256x2", "block256x4", "block512x4", "block1024x4",
               "large_resources", "large_chunks", "leases")
 
 
