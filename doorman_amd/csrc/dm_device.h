@@ -26,6 +26,12 @@ struct Pack {  // a run of consecutive small resources covering <= 64 rows
   int32_t maxlen;  // longest resource in the pack
 };
 
+struct WorkItem {  // one resource of a size bin: no dependent load before its rows
+  int32_t seg;
+  int32_t n;
+  int64_t lo;
+};
+
 struct Chunk {  // kChunkRows rows of one large resource
   int32_t seg;
   int32_t lseg;  // index into the large-resource table

@@ -262,6 +262,28 @@ __device__ __forceinline__ bool fs_stage01(double w, double h, long long s, doub
   return false;
 }
 
+// Uniform-subclient FairShare: every per-row quantity of algorithm.go:123-204
+// that does not depend on the row's own wants/has is a per-resource constant
+// (deservedShare, deservedExtra, T, and the two possible deservedExtraExtra).
+struct FsU {
+  double ds, dE, T, dee_gt, dee_eq;
+};
+__device__ __forceinline__ FsU make_fsu(double eq, long long s0, double E, long long Wc, AggC c) {
+  FsU f;
+  f.ds = eq * (double)s0;                      // :126
+  f.dE = (E / (double)Wc) * (double)s0;        // :175 (wantExtra == W for every row that gets here)
+  f.T = f.dE + f.ds;                           // :197 deservedExtra + deservedShare
+  f.dee_gt = (c.ee / (double)(s0 + c.sgt - s0)) * (double)s0;  // :203, row above T (excluded, :193)
+  f.dee_eq = (c.ee / (double)(s0 + c.sgt)) * (double)s0;       // :203, row exactly at T
+  return f;
+}
+__device__ __forceinline__ double fs_uniform_row(double w, double h, double C, double sum_has, const FsU& f) {
+  const double avail = C - sum_has + h;  // :120
+  if (w <= f.ds) return minF(w, avail);  // :131
+  if (w < f.ds + f.dE) return minF(w, avail);  // :179
+  return minF(f.ds + f.dE + (w > f.T ? f.dee_gt : f.dee_eq), avail);  // :204
+}
+
 // FairShare round 2 result for a row given the resource's sums at its T (:189-204).
 __device__ __forceinline__ double fs_stage2(double w, double h, long long s, double C, double sum_has, double eq,
                                             double E, long long Wc, double T, const AggC& c) {
@@ -279,10 +301,11 @@ __device__ __forceinline__ double fs_stage2(double w, double h, long long s, dou
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
 template <int G, int R>
-__device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t, Lds<G>& lds,
+__device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, int t, Lds<G>& lds,
                                               int32_t* general_list, int32_t* general_count) {
-  const int64_t lo = p.seg_off[seg];
-  const int n = (int)(p.seg_off[seg + 1] - lo);
+  const int seg = wi.seg;
+  const int64_t lo = wi.lo;
+  const int n = wi.n;
   // wave-uniform bases + 32-bit per-lane offsets: one VGPR addresses every column
   const double* __restrict__ wb = p.wants + lo;
   const double* __restrict__ hb = p.has + lo;
@@ -378,10 +401,10 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
 
   // ---- pass C (uniform subclients): FairShare round 2 at the resource's one threshold ----
   AggC cu{0.0, 0};
-  double Tu = 0.0;
+  FsU fu{0.0, 0.0, 0.0, 0.0, 0.0};
   if (fs_uniform) {
-    const double s0 = (double)a.smin;
-    Tu = (b.x / (double)b.i) * s0 + eq * s0;  // deservedExtra + deservedShare (:175,:126)
+    fu = make_fsu(eq, a.smin, b.x, b.i, cu);
+    const double Tu = fu.T;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       if (!(live >> k & 1)) continue;
@@ -392,6 +415,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
         cu.sgt += s[k];  // :199-200
     }
     cu = group_reduce<G>(cu, OpC(), lds.c);
+    fu = make_fsu(eq, a.smin, b.x, b.i, cu);
   }
 
   // ---- map: decide and write every lease (store.go:153-167 Assign) ----
@@ -401,8 +425,8 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      gb[u] = 0.0;
-      xb[u] = kReleased;
+      __builtin_nontemporal_store(0.0, gb + u);
+      __builtin_nontemporal_store((int64_t)(kReleased), xb + u);
       if (p.out_wants) {
         p.out_wants[lo + u] = 0.0;
         p.out_sub[lo + u] = 0;
@@ -422,13 +446,10 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
       g = (cl.sum_wants <= C || w[k] <= epc) ? minF(w[k], unused)            // :245
                                              : minF(epc + (w[k] - epc) * (b.x / b.y), unused);  // :283
     } else {
-      double T = 0.0;
-      if (!fs_stage01(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, &g, &T)) {
-        g = fs_stage2(w[k], h[k], s[k], C, cl.sum_has, eq, b.x, b.i, Tu, cu);
-      }
+      g = fs_uniform_row(w[k], h[k], C, cl.sum_has, fu);
     }
-    gb[u] = g;
-    xb[u] = rs.exp_out;
+    __builtin_nontemporal_store(g, gb + u);
+    __builtin_nontemporal_store((int64_t)(rs.exp_out), xb + u);
     delta.v += g - h[k];
   }
 
@@ -438,20 +459,20 @@ __device__ __forceinline__ void group_segment(const DevParams& p, int seg, int t
 
 // One G-thread workgroup per resource (G = 256..1024, R <= 4 rows per thread).
 template <int G, int R>
-__global__ __launch_bounds__(G) void k_block(DevParams p, const int32_t* __restrict__ segs, int nsegs,
+__global__ __launch_bounds__(G) void k_block(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<G> lds;
-  if ((int)blockIdx.x >= nsegs) return;
-  group_segment<G, R>(p, segs[blockIdx.x], threadIdx.x, lds, general_list, general_count);
+  if ((int)blockIdx.x >= nitems) return;
+  group_segment<G, R>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
 }
 
 // One wave per resource (n <= 64), four independent waves per workgroup.
-__global__ __launch_bounds__(256) void k_wave(DevParams p, const int32_t* __restrict__ segs, int nsegs,
+__global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                               int32_t* general_list, int32_t* general_count) {
   Lds<64> lds;  // unused by wave reductions
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= nsegs) return;
-  group_segment<64, 1>(p, segs[i], threadIdx.x & 63, lds, general_list, general_count);
+  if (i >= nitems) return;
+  group_segment<64, 1>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -588,11 +609,11 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   }
   if (valid) {
     if (lv) {
-      p.out_gets[row] = g;
-      p.out_expiry[row] = rs.exp_out;
+      __builtin_nontemporal_store(g, p.out_gets + row);
+      __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
     } else {
-      p.out_gets[row] = 0.0;
-      p.out_expiry[row] = kReleased;
+      __builtin_nontemporal_store(0.0, p.out_gets + row);
+      __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row);
       if (p.out_wants) {
         p.out_wants[row] = 0.0;
         p.out_sub[row] = 0;
@@ -805,6 +826,7 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   AggC c{0.0, 0};
   if (!rs.learning && rs.kind >= 2) b = seg_b<256>(P, L, lds);
   if (!rs.learning && rs.kind == 3) c = seg_c<256>(P, L, lds);
+  const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
   SumD delta{0.0};
   for (int i = threadIdx.x; i < ch.nrows; i += 256) {
     const int64_t row = ch.row0 + i;
@@ -812,8 +834,8 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     const long long s = p.sub[row];
     const bool lv = !(p.now > p.expiry[row]);
     if (!lv) {
-      p.out_gets[row] = 0.0;
-      p.out_expiry[row] = kReleased;
+      __builtin_nontemporal_store(0.0, p.out_gets + row);
+      __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row);
       if (p.out_wants) {
         p.out_wants[row] = 0.0;
         p.out_sub[row] = 0;
@@ -832,12 +854,10 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
       const double unused = C - st.cl.sum_has + h;
       g = (st.cl.sum_wants <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (b.x / b.y), unused);
     } else {
-      double T = 0.0;
-      if (!fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &T))
-        g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, T, c);
+      g = fs_uniform_row(w, h, C, st.cl.sum_has, fu);
     }
-    p.out_gets[row] = g;
-    p.out_expiry[row] = rs.exp_out;
+    __builtin_nontemporal_store(g, p.out_gets + row);
+    __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);
@@ -915,8 +935,8 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
       const double w = p.wants[row], h = p.has[row];
       const long long s = p.sub[row];
       if (p.now > p.expiry[row]) {
-        p.out_gets[row] = 0.0;
-        p.out_expiry[row] = kReleased;
+        __builtin_nontemporal_store(0.0, p.out_gets + row);
+        __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row);
         if (p.out_wants) {
           p.out_wants[row] = 0.0;
           p.out_sub[row] = 0;
@@ -930,8 +950,8 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         done = true;
       }
       if (done) {
-        p.out_gets[row] = g;
-        p.out_expiry[row] = rs.exp_out;
+        __builtin_nontemporal_store(g, p.out_gets + row);
+        __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
         delta.v += g - h;
       }
     }
@@ -973,8 +993,8 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         if (fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
         if (!(T == Ts)) continue;
         g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, c);
-        p.out_gets[row] = g;
-        p.out_expiry[row] = rs.exp_out;
+        __builtin_nontemporal_store(g, p.out_gets + row);
+        __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
         delta.v += g - h;
       }
       prev = Ts;
@@ -1047,7 +1067,7 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, int32_t* glist, int32_t* gcount,
+hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st) {
   if (n <= 0) return hipSuccess;
   switch (bin) {

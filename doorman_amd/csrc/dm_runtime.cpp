@@ -17,7 +17,7 @@
 
 namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
-hipError_t launch_bin(int bin, const DevParams& p, const int32_t* segs, int n, int32_t* glist, int32_t* gcount,
+hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
@@ -115,11 +115,11 @@ struct dm_ctx {
   bool last_writeback = false, have_result = false;
   // plan
   std::vector<Pack> h_packs;
-  std::vector<int32_t> h_bins[kNumBins];
+  std::vector<WorkItem> h_bins[kNumBins];
   std::vector<Chunk> h_chunks;
   std::vector<LargeSeg> h_large;
   DBuf<Pack> packs;
-  DBuf<int32_t> bins[kNumBins];
+  DBuf<WorkItem> bins[kNumBins];
   DBuf<Chunk> chunks;
   DBuf<LargeSeg> large;
   // large-path partials
@@ -249,7 +249,7 @@ static void build_plan(dm_ctx* c) {
     }
     close();
     if (n <= kLargeMin) {
-      c->h_bins[bin_of(n)].push_back((int32_t)r);
+      c->h_bins[bin_of(n)].push_back(WorkItem{(int32_t)r, (int32_t)n, off[r]});
     } else {
       LargeSeg L{(int32_t)r, (int32_t)c->h_chunks.size(), 0, 0};
       for (int64_t o = off[r]; o < off[r + 1]; o += kChunkRows) {
