@@ -32,6 +32,11 @@ struct Res {
   double cap_cfg;  // config capacity (SetSafeCapacity, resource.go:92)
   double safe;
   int64_t exp_out; // now + lease_length (store.go:161)
+  // the store's running sums, loaded with the config so that no global load
+  // waits behind the first reduction's barrier
+  long long agg_count;
+  double agg_has;
+  double agg_wants;
 };
 
 __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
@@ -42,18 +47,15 @@ __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
   r.C = (p.parent_expiry[seg] < p.now) ? 0.0 : r.cap_cfg;  // expiryTime.Before(now)
   r.safe = p.safe_cap[seg];
   r.exp_out = p.now + p.lease_len_s[seg] * kNs;
-  return r;
-}
-
-template <typename T>
-__device__ __forceinline__ T shfl_xor_any(const T& v, int m) {
-  static_assert(sizeof(T) % 4 == 0, "4-byte granular");
-  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
-  __builtin_memcpy(src, &v, sizeof(T));
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __shfl_xor(src[i], m, 64);
-  T r;
-  __builtin_memcpy(&r, dst, sizeof(T));
+  if (!p.recompute) {
+    r.agg_count = p.agg_count[seg];
+    r.agg_has = p.agg_sum_has[seg];
+    r.agg_wants = p.agg_sum_wants[seg];
+  } else {
+    r.agg_count = 0;
+    r.agg_has = 0.0;
+    r.agg_wants = 0.0;
+  }
   return r;
 }
 
@@ -68,15 +70,51 @@ __device__ __forceinline__ T shfl_any(const T& v, int lane) {
   return r;
 }
 
-// Group reduction (G = 64: one wave; G = 256: four waves through LDS).  Butterfly
-// within the wave, then every thread combines the wave partials in the same
-// fixed order, so all threads (and all blocks reducing the same inputs) agree
-// bit for bit.
+// DPP lane permute of every dword of v (a VALU operand modifier: no LDS trip).
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_any(const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "4-byte granular");
+  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
+  __builtin_memcpy(src, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i)
+    dst[i] = __builtin_amdgcn_update_dpp(0, src[i], CTRL, 0xF, 0xF, true);
+  T r;
+  __builtin_memcpy(&r, dst, sizeof(T));
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ T readlane_any(const T& v, int lane) {
+  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
+  __builtin_memcpy(src, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __builtin_amdgcn_readlane(src[i], lane);
+  T r;
+  __builtin_memcpy(&r, dst, sizeof(T));
+  return r;
+}
+
+// Wave reduction: a DPP butterfly inside each 16-lane row (xor 1, xor 2, half
+// mirror, mirror: partner lanes compute a+b and b+a, so every lane of a row holds
+// the same row total), then the four row totals combined in a fixed order from
+// scalar readlanes.  Requires all 64 lanes active.
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+  v = op(v, dpp_any<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_any<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_any<0x141>(v));  // row_half_mirror
+  v = op(v, dpp_any<0x140>(v));  // row_mirror
+  const T r0 = readlane_any(v, 0), r1 = readlane_any(v, 16), r2 = readlane_any(v, 32), r3 = readlane_any(v, 48);
+  return op(op(r0, r1), op(r2, r3));
+}
+
+// Group reduction (G = 64: one wave; G >= 256: the waves' totals through LDS).
+// Every thread combines the wave totals in the same fixed order, so all threads
+// (and all workgroups reducing the same inputs) agree bit for bit.
 template <int G, typename T, typename Op>
 __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = op(v, shfl_xor_any(v, o));
-  v = shfl_any(v, 0);
+  v = wave_reduce(v, op);
   if constexpr (G == 64) {
     (void)lds;
     return v;
@@ -219,7 +257,7 @@ struct Clean {
   double sum_has;
   double sum_wants;
 };
-__device__ __forceinline__ Clean clean_from(const DevParams& p, int seg, const AggA& a) {
+__device__ __forceinline__ Clean clean_from(const DevParams& p, const Res& rs, const AggA& a) {
   // store sums (running, or rebuilt from every row) minus the leases Clean releases
   Clean c;
   if (p.recompute) {
@@ -227,9 +265,9 @@ __device__ __forceinline__ Clean clean_from(const DevParams& p, int seg, const A
     c.sum_has = a.all.h - a.h;
     c.sum_wants = a.all.w - a.w;
   } else {
-    c.count = p.agg_count[seg] - a.cnt;
-    c.sum_has = p.agg_sum_has[seg] - a.h;
-    c.sum_wants = p.agg_sum_wants[seg] - a.w;
+    c.count = rs.agg_count - a.cnt;
+    c.sum_has = rs.agg_has - a.h;
+    c.sum_wants = rs.agg_wants - a.w;
   }
   return c;
 }
@@ -362,7 +400,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     a = group_reduce<G>(a, OpA(), lds.a);
     if (p.recompute) a.all = group_reduce<G>(all_part, OpR(), lds.r);
   }
-  const Clean cl = clean_from(p, seg, a);
+  const Clean cl = clean_from(p, rs, a);
   const double C = rs.C;
   const double eq = C / (double)cl.count;  // algorithm.go:123,229 equalShare
   const bool ps = !rs.learning && rs.kind == 2;
@@ -683,8 +721,8 @@ __device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials
   }
   SegState st;
   st.a = a;
-  st.cl = clean_from(p, L.seg, a);
   st.rs = load_res(p, L.seg);
+  st.cl = clean_from(p, st.rs, a);
   st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin >= a.smax && !a.nan)) ? 1 : 0;
   return st;
 }
@@ -913,7 +951,7 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
     a = group_reduce<256>(a, OpA(), lds.a);
     if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
   }
-    const Clean cl = clean_from(p, seg, a);
+    const Clean cl = clean_from(p, rs, a);
     const double C = rs.C;
     const double eq = C / (double)cl.count;
     // round 1 sums (algorithm.go:156-171)
