@@ -70,6 +70,25 @@ struct Partials {
   double* d_delta;
 };
 
+// Per-resource configuration, AoS (one scalar burst per resource).
+struct ResCfg {
+  double capacity;          // ResourceTemplate.capacity
+  double safe_capacity;     // NaN = unset (resource.go:91)
+  int64_t lease_len_ns;     // Algorithm.lease_length * 1e9
+  int64_t learning_end_ns;  // learningModeEndTime
+  int64_t parent_expiry_ns; // Resource.expiryTime (INT64_MAX = nil)
+  int32_t kind;             // pb.Algorithm.Kind
+  int32_t pad;
+};
+
+// The store's running sums (store.go:105-111) and the tick's SetSafeCapacity value.
+struct ResAgg {
+  int64_t count;
+  double sum_has;
+  double sum_wants;
+  double safe;
+};
+
 struct DevParams {
   const int64_t* seg_off;
   // lease table (SoA).  out_* alias these in writeback mode, so no __restrict__.
@@ -77,28 +96,14 @@ struct DevParams {
   const double* has;
   const int64_t* sub;
   const int64_t* expiry;
-  // per-resource configuration
-  const int32_t* kind;
-  const double* capacity;
-  const int64_t* lease_len_s;
-  const int64_t* refresh_s;
-  const int64_t* learning_end;
-  const int64_t* parent_expiry;
-  const double* safe_cap;
-  // store running sums (parity mode input)
-  const int64_t* agg_count;
-  const double* agg_sum_has;
-  const double* agg_sum_wants;
+  const ResCfg* cfg;
+  const ResAgg* agg;  // running sums read by the tick (parity mode)
   // lease outputs
   double* out_gets;
   int64_t* out_expiry;
   double* out_wants;  // writeback only: released rows zeroed (else nullptr)
   int64_t* out_sub;   // writeback only
-  // per-resource outputs
-  int64_t* res_count;
-  double* res_sum_has;
-  double* res_sum_wants;
-  double* res_safe;
+  ResAgg* res;        // per-resource results (== agg in writeback mode)
   int64_t now;
   int32_t recompute;
   int32_t pad;

@@ -41,16 +41,18 @@ struct Res {
 
 __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
   Res r;
-  r.kind = p.kind[seg];
-  r.learning = p.learning_end[seg] > p.now;  // resource.go:108 learningModeEndTime.After(now)
-  r.cap_cfg = p.capacity[seg];
-  r.C = (p.parent_expiry[seg] < p.now) ? 0.0 : r.cap_cfg;  // expiryTime.Before(now)
-  r.safe = p.safe_cap[seg];
-  r.exp_out = p.now + p.lease_len_s[seg] * kNs;
+  const ResCfg c = p.cfg[seg];
+  r.kind = c.kind;
+  r.learning = c.learning_end_ns > p.now;  // resource.go:108 learningModeEndTime.After(now)
+  r.cap_cfg = c.capacity;
+  r.C = (c.parent_expiry_ns < p.now) ? 0.0 : r.cap_cfg;  // expiryTime.Before(now)
+  r.safe = c.safe_capacity;
+  r.exp_out = p.now + c.lease_len_ns;
   if (!p.recompute) {
-    r.agg_count = p.agg_count[seg];
-    r.agg_has = p.agg_sum_has[seg];
-    r.agg_wants = p.agg_sum_wants[seg];
+    const ResAgg g = p.agg[seg];
+    r.agg_count = g.count;
+    r.agg_has = g.sum_has;
+    r.agg_wants = g.sum_wants;
   } else {
     r.agg_count = 0;
     r.agg_has = 0.0;
@@ -153,8 +155,8 @@ struct AggA {
   double h;
   double w;
   AggR all;       // filled in recompute mode only
-  long long smin;
-  long long smax;
+  int smin;       // live rows' subclients range and any NaN wants
+  int smax;
   int nan;
   int pad;
 };
@@ -178,8 +180,8 @@ __device__ __forceinline__ AggA zeroA() {
   a.h = 0.0;
   a.w = 0.0;
   a.all = AggR{0, 0.0, 0.0};
-  a.smin = INT64_MAX;
-  a.smax = INT64_MIN;
+  a.smin = INT32_MAX;
+  a.smax = INT32_MIN;
   a.nan = 0;
   a.pad = 0;
   return a;
@@ -274,10 +276,12 @@ __device__ __forceinline__ Clean clean_from(const DevParams& p, const Res& rs, c
 
 __device__ __forceinline__ void write_resource(const DevParams& p, int seg, const Res& rs, const Clean& c,
                                                double delta) {
-  p.res_count[seg] = c.count;
-  p.res_sum_wants[seg] = c.sum_wants;
-  p.res_sum_has[seg] = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
-  p.res_safe[seg] = __builtin_isnan(rs.safe) ? rs.cap_cfg / (double)c.count : rs.safe;  // resource.go:91-95
+  ResAgg r;
+  r.count = c.count;
+  r.sum_wants = c.sum_wants;
+  r.sum_has = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
+  r.safe = __builtin_isnan(rs.safe) ? rs.cap_cfg / (double)c.count : rs.safe;  // resource.go:91-95
+  p.res[seg] = r;
 }
 
 // FairShare per-row stage (algorithm.go:115-181).  Returns true when the lease is
@@ -353,7 +357,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   int64_t* xb = p.out_expiry + lo;
   // the rows stay in VGPRs for every pass: 6 registers per row
   double w[R], h[R];
-  long long s[R];
+  int s[R];  // subclients < 2^31 (checked by the host at load/upsert)
   unsigned valid = 0, live = 0;
 #pragma unroll
   for (int k = 0; k < R; ++k) {
@@ -365,7 +369,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       const unsigned u = (unsigned)i;
       w[k] = wb[u];
       h[k] = hb[u];
-      s[k] = sb[u];
+      s[k] = (int)sb[u];
       const int64_t e = eb[u];
       valid |= 1u << k;
       if (!(p.now > e)) live |= 1u << k;  // store.go:174 when.After(expiry)
@@ -568,9 +572,9 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
       }
     }
   } else {
-    count = p.agg_count[seg];
-    sh = p.agg_sum_has[seg];
-    sw = p.agg_sum_wants[seg];
+    count = rs.agg_count;
+    sh = rs.agg_has;
+    sw = rs.agg_wants;
   }
   for (int q = 0; q < maxlen; ++q) {
     const int j = lo + q;
@@ -674,9 +678,9 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   if (owner) {
     const int oseg = pk.first_seg + lane;
     if (olo == ohi) {  // resource without rows
-      ocount = p.recompute ? 0 : p.agg_count[oseg];
-      osh = p.recompute ? 0.0 : p.agg_sum_has[oseg];
-      osw = p.recompute ? 0.0 : p.agg_sum_wants[oseg];
+      ocount = p.recompute ? 0 : p.agg[oseg].count;
+      osh = p.recompute ? 0.0 : p.agg[oseg].sum_has;
+      osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
     }
     const Res ors = load_res(p, oseg);
     Clean oc{ocount, osh, osw};
@@ -706,8 +710,8 @@ __device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials
     x.h = P.a_has[c];
     x.w = P.a_wants[c];
     x.all = AggR{P.a_cnt_all[c], P.a_has_all[c], P.a_wants_all[c]};
-    x.smin = P.a_smin[c];
-    x.smax = P.a_smax[c];
+    x.smin = (int)P.a_smin[c];
+    x.smax = (int)P.a_smax[c];
     x.nan = P.a_nan[c];
     x.pad = 0;
     const AggR all = OpR()(a.all, x.all);  // OpA carries `all` through unchanged
@@ -761,8 +765,9 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
       a.all.w += w;
     }
     if (lv) {
-      a.smin = s < a.smin ? s : a.smin;
-      a.smax = s > a.smax ? s : a.smax;
+      const int si = (int)s;
+      a.smin = si < a.smin ? si : a.smin;
+      a.smax = si > a.smax ? si : a.smax;
       a.nan |= __builtin_isnan(w) ? 1 : 0;
     }
   }
@@ -1052,8 +1057,7 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
                          const int64_t* __restrict__ expiry, const int32_t* __restrict__ row_seg, double* s_has,
-                         double* s_wants, int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
-                         double* agg_sum_wants) {
+                         double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = rows[i];
@@ -1064,21 +1068,20 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
   s_wants[r] = wants[i];
   s_sub[r] = sub[i];
   s_exp[r] = expiry[i];
-  atomicAdd(&agg_sum_has[seg], dh);
-  atomicAdd(&agg_sum_wants[seg], dw);
-  atomicAdd((unsigned long long*)&agg_count[seg], (unsigned long long)ds);
+  atomicAdd(&agg[seg].sum_has, dh);
+  atomicAdd(&agg[seg].sum_wants, dw);
+  atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)ds);
 }
 
 __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int32_t* __restrict__ row_seg,
-                          double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, int64_t* agg_count,
-                          double* agg_sum_has, double* agg_sum_wants) {
+                          double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = rows[i];
   const int seg = row_seg[i];
-  atomicAdd(&agg_sum_has[seg], -s_has[r]);
-  atomicAdd(&agg_sum_wants[seg], -s_wants[r]);
-  atomicAdd((unsigned long long*)&agg_count[seg], (unsigned long long)(-s_sub[r]));
+  atomicAdd(&agg[seg].sum_has, -s_has[r]);
+  atomicAdd(&agg[seg].sum_wants, -s_wants[r]);
+  atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)(-s_sub[r]));
   s_has[r] = 0.0;
   s_wants[r] = 0.0;
   s_sub[r] = 0;
@@ -1086,13 +1089,12 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int
 }
 
 // server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
-__global__ void k_publish(int64_t R, const double* __restrict__ sum_wants, const int64_t* __restrict__ count,
-                          double2* __restrict__ dst) {
+__global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __restrict__ dst) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   double2 v;
-  v.x = sum_wants[r];
-  v.y = __longlong_as_double(count[r]);
+  v.x = agg[r].sum_wants;
+  v.y = __longlong_as_double(agg[r].count);
   dst[r] = v;
 }
 
@@ -1143,26 +1145,23 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
-                         int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
-                         double* agg_sum_wants, hipStream_t st) {
+                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, row_seg, s_has, s_wants,
-                                                        s_sub, s_exp, agg_count, agg_sum_has, agg_sum_wants);
+                                                        s_sub, s_exp, agg);
   return hipGetLastError();
 }
 
 hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
-                          int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
-                          double* agg_sum_wants, hipStream_t st) {
+                          int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, row_seg, s_has, s_wants, s_sub, s_exp, agg_count,
-                                                         agg_sum_has, agg_sum_wants);
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, row_seg, s_has, s_wants, s_sub, s_exp, agg);
   return hipGetLastError();
 }
 
-hipError_t launch_publish(int64_t R, const double* sum_wants, const int64_t* count, void* dst, hipStream_t st) {
+hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st) {
   if (R <= 0) return hipSuccess;
-  k_publish<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, sum_wants, count, (double2*)dst);
+  k_publish<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, agg, (double2*)dst);
   return hipGetLastError();
 }
 

@@ -25,12 +25,10 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
                           hipStream_t st);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
-                         int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
-                         double* agg_sum_wants, hipStream_t st);
+                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
-                          int64_t* s_sub, int64_t* s_exp, int64_t* agg_count, double* agg_sum_has,
-                          double* agg_sum_wants, hipStream_t st);
-hipError_t launch_publish(int64_t R, const double* sum_wants, const int64_t* count, void* dst, hipStream_t st);
+                          int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
+hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
 }  // namespace dm
 
 using namespace dm;
@@ -100,18 +98,14 @@ struct dm_ctx {
   DBuf<int64_t> seg_off;
   DBuf<double> wants, has;
   DBuf<int64_t> sub, expiry;
-  // running sums
-  DBuf<int64_t> agg_count;
-  DBuf<double> agg_sum_has, agg_sum_wants;
-  // config
-  DBuf<int32_t> kind;
-  DBuf<double> capacity, safe_cap;
-  DBuf<int64_t> lease_len, refresh, learning_end, parent_expiry;
+  // running sums (+ the last writeback tick's safe capacity), AoS
+  DBuf<ResAgg> agg;
+  // config, AoS
+  DBuf<ResCfg> cfg;
   // outputs of a non-writeback tick
   DBuf<double> out_gets;
   DBuf<int64_t> out_expiry;
-  DBuf<int64_t> res_count;
-  DBuf<double> res_sum_has, res_sum_wants, res_safe;
+  DBuf<ResAgg> res;
   bool last_writeback = false, have_result = false;
   // plan
   std::vector<Pack> h_packs;
@@ -174,11 +168,8 @@ struct dm_ctx {
   }
   void free_all() {
     seg_off.release(); wants.release(); has.release(); sub.release(); expiry.release();
-    agg_count.release(); agg_sum_has.release(); agg_sum_wants.release();
-    kind.release(); capacity.release(); safe_cap.release(); lease_len.release(); refresh.release();
-    learning_end.release(); parent_expiry.release();
-    out_gets.release(); out_expiry.release(); res_count.release(); res_sum_has.release();
-    res_sum_wants.release(); res_safe.release();
+    agg.release(); cfg.release();
+    out_gets.release(); out_expiry.release(); res.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
@@ -401,6 +392,9 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   if (s->seg_off[0] != 0 || s->seg_off[R] != N) return c->fail(DM_E_INVAL, "seg_off must run from 0 to n_leases");
   for (int64_t r = 0; r < R; ++r)
     if (s->seg_off[r + 1] < s->seg_off[r]) return c->fail(DM_E_INVAL, "seg_off must be non-decreasing");
+  for (int64_t i = 0; i < N; ++i)
+    if (s->subclients[i] < 0 || s->subclients[i] > INT32_MAX)
+      return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
   const bool have_agg = s->agg_count && s->agg_sum_has && s->agg_sum_wants;
   if ((s->agg_count || s->agg_sum_has || s->agg_sum_wants) && !have_agg)
     return c->fail(DM_E_INVAL, "give all three running sums or none");
@@ -433,9 +427,9 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     ah = sh.data();
     aw = sw.data();
   }
-  DM_HIP(c, upload(c->agg_count, ac, (size_t)R, st), "upload agg_count");
-  DM_HIP(c, upload(c->agg_sum_has, ah, (size_t)R, st), "upload agg_sum_has");
-  DM_HIP(c, upload(c->agg_sum_wants, aw, (size_t)R, st), "upload agg_sum_wants");
+  std::vector<ResAgg> agg(R);
+  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], NAN};
+  DM_HIP(c, upload(c->agg, agg.data(), (size_t)R, st), "upload running sums");
   build_plan(c);
   int rc = upload_plan(c);
   if (rc) return rc;
@@ -466,13 +460,11 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
     }
   DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
   hipStream_t st = c->stream;
-  DM_HIP(c, upload(c->kind, cfg->kind, (size_t)R, st), "upload kind");
-  DM_HIP(c, upload(c->capacity, cfg->capacity, (size_t)R, st), "upload capacity");
-  DM_HIP(c, upload(c->lease_len, cfg->lease_length_s, (size_t)R, st), "upload lease_length");
-  DM_HIP(c, upload(c->refresh, cfg->refresh_interval_s, (size_t)R, st), "upload refresh");
-  DM_HIP(c, upload(c->learning_end, cfg->learning_end_ns, (size_t)R, st), "upload learning_end");
-  DM_HIP(c, upload(c->parent_expiry, cfg->parent_expiry_ns, (size_t)R, st), "upload parent_expiry");
-  DM_HIP(c, upload(c->safe_cap, cfg->safe_capacity, (size_t)R, st), "upload safe_capacity");
+  std::vector<ResCfg> rc(R);
+  for (int64_t r = 0; r < R; ++r)
+    rc[r] = ResCfg{cfg->capacity[r], cfg->safe_capacity[r], cfg->lease_length_s[r] * kNs, cfg->learning_end_ns[r],
+                   cfg->parent_expiry_ns[r], cfg->kind[r], 0};
+  DM_HIP(c, upload(c->cfg, rc.data(), (size_t)R, st), "upload config");
   c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
   DM_HIP(c, hipStreamSynchronize(st), "config load");
   c->cfg_loaded = true;
@@ -497,41 +489,23 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   p.has = c->has.p;
   p.sub = c->sub.p;
   p.expiry = c->expiry.p;
-  p.kind = c->kind.p;
-  p.capacity = c->capacity.p;
-  p.lease_len_s = c->lease_len.p;
-  p.refresh_s = c->refresh.p;
-  p.learning_end = c->learning_end.p;
-  p.parent_expiry = c->parent_expiry.p;
-  p.safe_cap = c->safe_cap.p;
-  p.agg_count = c->agg_count.p;
-  p.agg_sum_has = c->agg_sum_has.p;
-  p.agg_sum_wants = c->agg_sum_wants.p;
+  p.cfg = c->cfg.p;
+  p.agg = c->agg.p;
   if (wb) {
     p.out_gets = c->has.p;
     p.out_expiry = c->expiry.p;
     p.out_wants = c->wants.p;
     p.out_sub = c->sub.p;
-    p.res_count = c->agg_count.p;
-    p.res_sum_has = c->agg_sum_has.p;
-    p.res_sum_wants = c->agg_sum_wants.p;
-    DM_HIP(c, c->res_safe.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res_safe");
-    p.res_safe = c->res_safe.p;
+    p.res = c->agg.p;
   } else {
     DM_HIP(c, c->out_gets.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_gets");
     DM_HIP(c, c->out_expiry.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_expiry");
-    DM_HIP(c, c->res_count.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
-    DM_HIP(c, c->res_sum_has.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
-    DM_HIP(c, c->res_sum_wants.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
-    DM_HIP(c, c->res_safe.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
+    DM_HIP(c, c->res.ensure((size_t)std::max<int64_t>(c->R, 1)), "alloc res");
     p.out_gets = c->out_gets.p;
     p.out_expiry = c->out_expiry.p;
     p.out_wants = nullptr;
     p.out_sub = nullptr;
-    p.res_count = c->res_count.p;
-    p.res_sum_has = c->res_sum_has.p;
-    p.res_sum_wants = c->res_sum_wants.p;
-    p.res_safe = c->res_safe.p;
+    p.res = c->res.p;
   }
   p.now = now_ns;
   p.recompute = (flags & DM_AGG_RECOMPUTE) ? 1 : 0;
@@ -631,13 +605,17 @@ int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* 
   DM_CHECK_CTX(c);
   int rc = check_range(c, r0, n, c->R);
   if (rc) return rc;
-  const bool wb = !c->have_result || c->last_writeback;
   if (safe && !c->have_result) return c->fail(DM_E_STATE, "safe capacity needs a dm_apportion result");
-  DM_HIP(c, download(count, wb ? c->agg_count.p : c->res_count.p, r0, n, c->stream), "read count");
-  DM_HIP(c, download(sum_has, wb ? c->agg_sum_has.p : c->res_sum_has.p, r0, n, c->stream), "read sum_has");
-  DM_HIP(c, download(sum_wants, wb ? c->agg_sum_wants.p : c->res_sum_wants.p, r0, n, c->stream), "read sum_wants");
-  DM_HIP(c, download(safe, (const double*)c->res_safe.p, r0, n, c->stream), "read safe");
+  const bool wb = !c->have_result || c->last_writeback;
+  std::vector<ResAgg> v(n > 0 ? n : 0);
+  DM_HIP(c, download(v.data(), (const ResAgg*)(wb ? c->agg.p : c->res.p), r0, n, c->stream), "read resources");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read resources");
+  for (int64_t i = 0; i < n; ++i) {
+    if (count) count[i] = v[i].count;
+    if (sum_has) sum_has[i] = v[i].sum_has;
+    if (sum_wants) sum_wants[i] = v[i].sum_wants;
+    if (safe) safe[i] = v[i].safe;
+  }
   return DM_OK;
 }
 
@@ -677,6 +655,8 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
+  for (int64_t i = 0; i < n; ++i)
+    if (sub[i] < 0 || sub[i] > INT32_MAX) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
   int rc = stage_rows(c, n, rows);
   if (rc) return rc;
   DM_HIP(c, upload(c->st_has, has, (size_t)n, c->stream), "stage has");
@@ -687,8 +667,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   for (int64_t i = 0; i < n && !c->maybe_general; ++i)
     if (std::isnan(wants[i]) || sub[i] != 1 || !c->all_sub_one) c->maybe_general = true;
   DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->st_seg.p,
-                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg_count.p, c->agg_sum_has.p,
-                          c->agg_sum_wants.p, c->stream),
+                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->stream),
          "upsert");
   DM_HIP(c, hipStreamSynchronize(c->stream), "upsert");
   c->have_result = false;
@@ -702,8 +681,8 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   if (n == 0) return DM_OK;
   int rc = stage_rows(c, n, rows);
   if (rc) return rc;
-  DM_HIP(c, launch_release(n, c->st_rows.p, c->st_seg.p, c->has.p, c->wants.p, c->sub.p, c->expiry.p,
-                           c->agg_count.p, c->agg_sum_has.p, c->agg_sum_wants.p, c->stream),
+  DM_HIP(c, launch_release(n, c->st_rows.p, c->st_seg.p, c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
+                           c->stream),
          "release");
   DM_HIP(c, hipStreamSynchronize(c->stream), "release");
   c->have_result = false;
@@ -732,7 +711,7 @@ int dm_publish_totals(dm_ctx* c, void* dst) {
   DM_CHECK_CTX(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
-  DM_HIP(c, launch_publish(c->R, c->agg_sum_wants.p, c->agg_count.p, dst, c->stream), "publish");
+  DM_HIP(c, launch_publish(c->R, c->agg.p, dst, c->stream), "publish");
   return DM_OK;
 }
 

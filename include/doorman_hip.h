@@ -73,7 +73,7 @@ typedef struct {
   const int64_t* seg_off;    /* [R+1] resource r owns rows [seg_off[r], seg_off[r+1]) */
   const double* wants;       /* [N] Lease.Wants */
   const double* has;         /* [N] Lease.Has */
-  const int64_t* subclients; /* [N] Lease.Subclients */
+  const int64_t* subclients; /* [N] Lease.Subclients, 0 <= v < 2^31 (DM_E_INVAL otherwise) */
   const int64_t* expiry_ns;  /* [N] Lease.Expiry, unix ns */
   const int64_t* agg_count;  /* [R] or NULL: store.count     (running sum; NULL = recompute) */
   const double* agg_sum_has; /* [R] or NULL: store.sumHas */
