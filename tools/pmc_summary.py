@@ -1,0 +1,110 @@
+"""Summarise a tools/gpu_profile.sh run into profiles/.
+
+Reads rocprofv3 CSVs (kernel trace stats, FETCH_SIZE and WRITE_SIZE passes, and
+the same counters on tools/ubench's k_flat8 kernel whose traffic is known) and
+writes:
+  profiles/pmc_<workload>.json   per kernel class: avg duration, raw counters,
+                                 calibrated HBM bytes per launch (bench.py reads it)
+  profiles/rocprof_<workload>.md the kernel-stats table and the derivation
+Usage: python tools/pmc_summary.py gpurun_out/prof_<w> <w>
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+CLASS = [
+    (r"k_block<256, 1>", "block256x1"), (r"k_block<256, 2>", "block256x2"), (r"k_block<256, 4>", "block256x4"),
+    (r"k_block<512, 4>", "block512x4"), (r"k_block<1024, 4>", "block1024x4"), (r"k_wave\b", "wave64x1"),
+    (r"k_small\b", "small_packed"), (r"k_large_a\b", "large_a"), (r"k_large_b\b", "large_b"),
+    (r"k_large_c\b", "large_c"), (r"k_large_map\b", "large_map"), (r"k_large_fin\b", "large_fin"),
+    (r"k_general\b", "general"), (r"k_flat8\(", "ubench_flat8"), (r"k_flat8nt\(", "ubench_flat8nt"),
+]
+
+
+def cls(name):
+    for pat, c in CLASS:
+        if re.search(pat, name):
+            return c
+    return None
+
+
+def find(d, suffix):
+    hits = glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True)
+    return hits[0] if hits else None
+
+
+def counters(d):
+    """mean counter value per dispatch, by kernel class"""
+    f = find(d, "counter_collection.csv")
+    if not f:
+        return {}
+    acc = {}
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            c = cls(row.get("Kernel_Name", ""))
+            if c is None:
+                continue
+            v = float(row.get("Counter_Value", 0) or 0)
+            key = (c, row.get("Counter_Name"))
+            s, n = acc.get(key, (0.0, 0))
+            acc[key] = (s + v, n + 1)
+    return {k: s / n for k, (s, n) in acc.items()}
+
+
+def main(d, w):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stats_f = find(os.path.join(d, "trace"), "kernel_stats.csv")
+    stats = {}
+    rows = []
+    if stats_f:
+        with open(stats_f) as fh:
+            for row in csv.DictReader(fh):
+                rows.append(row)
+                c = cls(row["Name"])
+                if c:
+                    stats[c] = {"calls": int(row["Calls"]), "avg_us": float(row["AverageNs"]) / 1e3}
+    fetch = counters(os.path.join(d, "fetch"))
+    write = counters(os.path.join(d, "write"))
+    cf = counters(os.path.join(d, "cal_fetch"))
+    cw = counters(os.path.join(d, "cal_write"))
+    # k_flat8 over 1e7 rows reads 32 B and writes 16 B per row
+    known_r, known_w = 32 * 10_000_000, 16 * 10_000_000
+    fr = cf.get(("ubench_flat8", "FETCH_SIZE"))
+    wr = cw.get(("ubench_flat8", "WRITE_SIZE"))
+    read_cal = known_r / (fr * 1024) if fr else 2.0  # guide: FETCH_SIZE reads 1/2 of wide streams
+    write_cal = known_w / (wr * 1024) if wr else 1.0
+    out = {"_calibration": {"read_factor": read_cal, "write_factor": write_cal,
+                            "ubench_flat8_fetch_kb": fr, "ubench_flat8_write_kb": wr,
+                            "note": "HBM bytes = FETCH_SIZE*1024*read_factor + WRITE_SIZE*1024*write_factor; factors "
+                                    "from tools/ubench k_flat8 (8-byte lanes, 48 B/row known)"}}
+    for (c, name), v in fetch.items():
+        if name != "FETCH_SIZE" or c.startswith("ubench"):
+            continue
+        wv = write.get((c, "WRITE_SIZE"), 0.0)
+        out[c] = {"fetch_kb": v, "write_kb": wv, "avg_us": stats.get(c, {}).get("avg_us"),
+                  "hbm_bytes_per_launch": v * 1024 * read_cal + wv * 1024 * write_cal}
+    os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
+    with open(os.path.join(root, "profiles", f"pmc_{w}.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    with open(os.path.join(root, "profiles", f"rocprof_{w}.md"), "w") as fh:
+        fh.write(f"# rocprofv3 --kernel-trace --stats: bench.py --workload {w}\n\n")
+        fh.write("| kernel | calls | avg (us) | min (us) | max (us) | share |\n|---|---|---|---|---|---|\n")
+        for row in rows:
+            fh.write(f"| `{row['Name'][:70]}` | {row['Calls']} | {float(row['AverageNs']) / 1e3:.2f} | "
+                     f"{float(row['MinNs']) / 1e3:.2f} | {float(row['MaxNs']) / 1e3:.2f} | {row['Percentage']}% |\n")
+        fh.write("\n## HBM traffic from PMC counters (separate --pmc passes)\n\n")
+        fh.write(f"calibration (tools/ubench k_flat8, known 32 B read + 16 B written per row): "
+                 f"read x{read_cal:.3f}, write x{write_cal:.3f}\n\n")
+        fh.write("| kernel | FETCH_SIZE (KB) | WRITE_SIZE (KB) | HBM bytes / launch |\n|---|---|---|---|\n")
+        for c, v in out.items():
+            if c.startswith("_"):
+                continue
+            fh.write(f"| {c} | {v['fetch_kb']:.0f} | {v['write_kb']:.0f} | {v['hbm_bytes_per_launch']:.4g} |\n")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
