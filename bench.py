@@ -115,6 +115,9 @@ def main():
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--hier", action="store_true",
+                    help="every step runs the intermediate-server exchange first (SURVEY.md §8e, configs[3]): "
+                         "publish totals, RCCL all-gather, root apportionment, take grants, then the leaf tick")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,8 +144,24 @@ def main():
         if world > 1:
             dist.barrier()
 
+    step = lambda: eng.apportion(now, writeback=True, asynchronous=True)  # noqa: E731
+    root = None
+    if args.hier:
+        from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
+        root = Engine(local_rank)
+        root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world, lease_length_s=20))
+
+        def gather(src, dst):
+            if world > 1:
+                dist.all_gather_into_tensor(dst, src)
+            else:
+                dst.copy_(src)
+
+        ht = HierarchicalTick(torch, eng, root, R, world, rank, gather)
+        step = lambda: ht.tick(now, asynchronous=True)  # noqa: E731
+
     for _ in range(args.warmup):
-        eng.apportion(now, writeback=True, asynchronous=True)
+        step()
     eng.sync()
     eng.set_profiling(True)
     eng.reset_kernel_times()
@@ -150,7 +169,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.apportion(now, writeback=True, asynchronous=True)
+        step()
     eng.sync()
     torch.cuda.synchronize()
     barrier()
@@ -207,8 +226,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded numpy generators of SURVEY.md §8d)",
-            "config": {"workload": WORKLOADS[args.workload], "resources_per_gpu": R, "leases_per_gpu": N,
-                       "parallelism": f"resource-sharded x{world} (no data-path collective)",
+            "config": {"workload": WORKLOADS[args.workload] + (
+                           "; hierarchical: every GPU is an intermediate server of the same resources, RCCL "
+                           "all-gather of per-resource totals + root apportionment each step" if args.hier else ""),
+                       "resources_per_gpu": R, "leases_per_gpu": N,
+                       "parallelism": (f"intermediate-server hierarchy x{world} (all-gather 16 B x R per GPU)"
+                                       if args.hier else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in ktimes.items()},
@@ -217,6 +240,8 @@ def main():
         }
         print(json.dumps(line), flush=True)
     eng.close()
+    if root is not None:
+        root.close()
     if world > 1:
         dist.destroy_process_group()
 

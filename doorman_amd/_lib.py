@@ -79,6 +79,8 @@ _SIGS = {
     "dm_aggregate_bands": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "dm_publish_totals": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_hier_load_root": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
+    "dm_hier_take_grants": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),

@@ -1098,6 +1098,48 @@ __global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __
   dst[r] = v;
 }
 
+// Intermediate-server hierarchy (server.go:227-323 -> :822-901).  The root store
+// holds R resources x G server rows (resource r owns rows [r*G, r*G+G)); gathered
+// is the all-gather of every server's k_publish records, [G][R] x 16 B.  A server
+// requests a resource only when its SumWants > 0 (server.go:241) and its band
+// must have num_clients >= 1 (server.go:863-866); other rows are released.
+__global__ void k_hier_root(int64_t R, int G, const double2* __restrict__ gathered, double* r_wants, double* r_has,
+                            int64_t* r_sub, int64_t* r_exp, int64_t now) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * G) return;
+  const int64_t r = i / G;
+  const int g = (int)(i - r * G);
+  const double2 v = gathered[(int64_t)g * R + r];
+  const double sum_wants = v.x;
+  const long long count = __double_as_longlong(v.y);
+  if (sum_wants > 0.0 && count >= 1) {
+    r_wants[i] = sum_wants;  // GetServerCapacity: wantsTotal, subclientsTotal (:850-879)
+    r_sub[i] = count;
+    if (r_exp[i] == kReleased) r_has[i] = 0.0;  // a new lease has nothing yet
+    r_exp[i] = now;  // refreshing now: live for this tick's Clean
+  } else {
+    r_wants[i] = 0.0;
+    r_has[i] = 0.0;
+    r_sub[i] = 0;
+    r_exp[i] = kReleased;
+  }
+}
+
+// server.go:284-296: the intermediate's template for resource r takes the root's
+// grant as capacity and its expiry (Unix seconds) as the parent-lease expiry.
+// Resources the server did not request keep their previous template.
+__global__ void k_hier_grants(int64_t R, int G, int g, const double* __restrict__ gets,
+                              const int64_t* __restrict__ expiry, ResCfg* leaf_cfg) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int64_t i = r * G + g;
+  const int64_t e = expiry[i];
+  if (e == kReleased) return;
+  leaf_cfg[r].capacity = gets[i];
+  const int64_t sec = e >= 0 ? e / kNs : -((-e + kNs - 1) / kNs);  // time.Unix(sec, 0)
+  leaf_cfg[r].parent_expiry_ns = sec * kNs;
+}
+
 // --------------------------------------------------------------------------
 // host-side launchers (called by dm_runtime.cpp)
 // --------------------------------------------------------------------------
@@ -1162,6 +1204,21 @@ hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st) {
   if (R <= 0) return hipSuccess;
   k_publish<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, agg, (double2*)dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int64_t* r_sub,
+                            int64_t* r_exp, int64_t now, hipStream_t st) {
+  if (R * G <= 0) return hipSuccess;
+  k_hier_root<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, r_wants, r_has, r_sub,
+                                                               r_exp, now);
+  return hipGetLastError();
+}
+
+hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
+                              hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  k_hier_grants<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, G, g, gets, expiry, leaf_cfg);
   return hipGetLastError();
 }
 

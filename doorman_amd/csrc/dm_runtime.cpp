@@ -29,6 +29,10 @@ hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, cons
 hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
                           int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
+hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int64_t* r_sub,
+                            int64_t* r_exp, int64_t now, hipStream_t st);
+hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
+                              hipStream_t st);
 }  // namespace dm
 
 using namespace dm;
@@ -712,6 +716,46 @@ int dm_publish_totals(dm_ctx* c, void* dst) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
   DM_HIP(c, launch_publish(c->R, c->agg.p, dst, c->stream), "publish");
+  return DM_OK;
+}
+
+static bool root_layout_ok(dm_ctx* c, int G) {
+  if (G <= 0 || c->R <= 0 || c->N != c->R * (int64_t)G) return false;
+  for (int64_t r = 0; r <= c->R; ++r)
+    if (c->h_seg_off[r] != r * (int64_t)G) return false;
+  return true;
+}
+
+int dm_hier_load_root(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns) {
+  DM_CHECK_CTX(root);
+  if (!root->store_loaded) return root->fail(DM_E_STATE, "root store not loaded");
+  if (!gathered) return root->fail(DM_E_INVAL, "null gathered buffer");
+  if (!root_layout_ok(root, n_servers))
+    return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows");
+  DM_HIP(root, launch_hier_root(root->R, n_servers, gathered, root->wants.p, root->has.p, root->sub.p,
+                                root->expiry.p, now_ns, root->stream),
+         "hier root update");
+  // the rows changed: rebuild the running sums the next tick consumes
+  root->maybe_general = true;
+  root->have_result = false;
+  DM_HIP(root, hipStreamSynchronize(root->stream), "hier root update");
+  return DM_OK;
+}
+
+int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server) {
+  DM_CHECK_CTX(root);
+  if (!leaf) return root->fail(DM_E_INVAL, "null leaf context");
+  if (leaf->device != root->device) return root->fail(DM_E_INVAL, "root and leaf contexts must share a device");
+  if (!root->have_result) return root->fail(DM_E_STATE, "no root dm_apportion result");
+  const int G = (int)(root->R > 0 ? root->N / root->R : 0);
+  if (!root_layout_ok(root, G)) return root->fail(DM_E_STATE, "root store layout");
+  if (server < 0 || server >= G) return root->fail(DM_E_RANGE, "server index out of range");
+  if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
+  const double* gets = root->last_writeback ? root->has.p : root->out_gets.p;
+  const int64_t* exp = root->last_writeback ? root->expiry.p : root->out_expiry.p;
+  DM_HIP(root, hipStreamSynchronize(leaf->stream), "leaf sync");
+  DM_HIP(root, launch_hier_grants(root->R, G, server, gets, exp, leaf->cfg.p, root->stream), "hier grants");
+  DM_HIP(root, hipStreamSynchronize(root->stream), "hier grants");
   return DM_OK;
 }
 

@@ -1,0 +1,96 @@
+"""Multi-GPU orchestration: resource sharding and the intermediate-server hierarchy.
+
+* Sharding: resources are independent (no cross-resource term in
+  go/server/doorman/algorithm.go), so a node splits the resource-id range into
+  contiguous shards balanced by lease count, one per GPU, and every GPU runs its
+  ticks with no data-path communication.
+
+* Hierarchy (server.go:227-323 on the intermediate, :822-901 on the root): every
+  GPU is one intermediate server holding its own clients of the same R
+  resources.  Per tick each server publishes {SumWants, Count} per resource
+  (dm_publish_totals), one RCCL all-gather over xGMI shares them, every rank
+  evaluates the root's apportionment of the G server rows redundantly
+  (dm_hier_load_root + dm_apportion on a root store of R x G rows), takes its
+  own grant as leaf capacity (dm_hier_take_grants) and runs its leaf tick.
+
+torch is plumbing here (device buffers and torch.distributed); import it before
+doorman_amd so the HIP library binds to torch's HIP runtime.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import workloads as W
+
+
+def partition(seg_sizes, world: int) -> np.ndarray:
+    """Contiguous resource ranges balanced by lease count: boundaries b[0..world]
+    with shard k = resources [b[k], b[k+1])."""
+    sizes = np.asarray(seg_sizes, dtype=np.int64)
+    R = len(sizes)
+    if world <= 1 or R == 0:
+        return np.array([0, R], dtype=np.int64)
+    csum = np.concatenate([[0], np.cumsum(sizes)])
+    total = csum[-1]
+    bounds = [0]
+    for k in range(1, world):
+        target = total * k / world
+        b = int(np.searchsorted(csum, target, side="left"))
+        # pick the closer of b-1 / b, keep ranges monotone and non-empty where possible
+        if b > 0 and abs(csum[b - 1] - target) <= abs(csum[min(b, R)] - target):
+            b -= 1
+        b = max(b, bounds[-1] + (1 if R - bounds[-1] > world - k else 0))
+        bounds.append(min(b, R))
+    bounds.append(R)
+    return np.asarray(bounds, dtype=np.int64)
+
+
+def shard(snap: dict, world: int, rank: int) -> dict:
+    b = partition(np.diff(snap["seg_off"]), world)
+    return W.subset(snap, np.arange(b[rank], b[rank + 1]))
+
+
+def root_snapshot(n_resources: int, n_servers: int, kind, capacity, lease_length_s=20, refresh_interval_s=5) -> dict:
+    """The root server's store for the hierarchy: R resources x G server rows,
+    all released until the first dm_hier_load_root."""
+    G = n_servers
+    N = n_resources * G
+    return W.make_snapshot(np.full(n_resources, G), np.zeros(N), np.zeros(N), np.zeros(N, np.int64),
+                           np.full(N, W.RELEASED), kind, capacity, lease_length_s, refresh_interval_s,
+                           aggregates=True)
+
+
+class HierarchicalTick:
+    """One rank of the hierarchy: an intermediate server (leaf engine) plus a
+    redundant copy of the root (root engine), both on this rank's GPU.
+
+    gather(src, dst): all-gather of the [R, 2] float64 records of every server into
+    dst [G * R, 2] in server order (torch.distributed.all_gather_into_tensor over
+    RCCL on a node; a local copy in single-process tests)."""
+
+    def __init__(self, torch, leaf, root, n_resources: int, n_servers: int, server: int, gather):
+        self.torch = torch
+        self.leaf, self.root = leaf, root
+        self.R, self.G, self.g = n_resources, n_servers, server
+        self.gather = gather
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.totals = torch.empty((self.R, 2), dtype=torch.float64, device=dev)
+        self.gathered = torch.empty((self.G * self.R, 2), dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream().cuda_stream
+        # the library's kernels and torch's collectives share one stream: ordered
+        leaf.set_stream(stream)
+        root.set_stream(stream)
+
+    def exchange(self, now_ns: int):
+        """publish -> all-gather -> root apportionment -> take this server's grants."""
+        from . import _lib
+        self.leaf.publish_totals(self.totals.data_ptr())
+        self.gather(self.totals, self.gathered)
+        _lib.check(_lib.lib().dm_hier_load_root(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns)),
+                   self.root._ctx)
+        self.root.apportion(now_ns, writeback=True, recompute=True)
+        _lib.check(_lib.lib().dm_hier_take_grants(self.root._ctx, self.leaf._ctx, self.g), self.root._ctx)
+
+    def tick(self, now_ns: int, asynchronous: bool = False):
+        self.exchange(now_ns)
+        self.leaf.apportion(now_ns, writeback=True, asynchronous=asynchronous)

@@ -143,6 +143,18 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
  * device buffer (16 B x R, interleaved), ready for an RCCL all-gather */
 int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
 
+/* Root server of the hierarchy on one device: `root` holds R resources x n_servers rows
+ * (resource r owns rows [r*n_servers, (r+1)*n_servers)); dev_gathered is the all-gather of
+ * every intermediate server's dm_publish_totals ([n_servers][R] x 16 B).  Each row becomes that
+ * server's GetServerCapacity request (server.go:850-879): wants = SumWants, subclients = Count;
+ * a server whose SumWants <= 0 or Count < 1 does not request the resource (server.go:241,863)
+ * and its row is released.  Then call dm_apportion on `root`. */
+int dm_hier_load_root(dm_ctx* root, const void* dev_gathered, int n_servers, int64_t now_ns);
+/* server.go:284-296: the leaf (intermediate) store of `server` takes the root's grant as its
+ * capacity and the grant's expiry (Unix seconds) as parent expiry; resources it did not
+ * request keep their template.  Both contexts must be on the same device. */
+int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server);
+
 /* ---- profiling ---- */
 int dm_set_profiling(dm_ctx* ctx, int on);
 /* fills up to max entries; returns the number of kernel classes (>= 0) */

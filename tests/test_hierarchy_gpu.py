@@ -1,0 +1,73 @@
+"""The intermediate-server hierarchy on one GPU: G simulated servers publish
+their totals, the gathered records feed the root store (dm_hier_load_root), the
+root apportions its G server rows per resource, every server takes its grant
+(dm_hier_take_grants) and runs its leaf tick -- all checked against the oracle
+model of GetServerCapacity (tests/hier_model.py)."""
+import numpy as np
+import pytest
+
+from doorman_amd import hierarchy as H
+from doorman_amd import workloads as W
+from oracle import oracle as O
+import hier_model as M
+from parity_util import assert_leases_match
+
+pytestmark = pytest.mark.gpu
+NOW = W.NOW_NS
+
+
+@pytest.mark.parametrize("G", [2, 3, 8, 20])
+def test_hierarchy_round(G):
+    import torch
+    from doorman_amd.engine import Engine
+    R = 64
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(G)
+    leaves, snaps = [], []
+    for g in range(G):
+        s = W.uniform(R, int(rng.integers(5, 300)), kind=W.FAIR_SHARE, seed=10 * G + g, capacity=1000.0)
+        s["wants"] *= rng.uniform(0.2, 3.0)  # servers differ in appetite
+        if g == 1:
+            s["wants"][: len(s["wants"]) // 4] = 0.0  # some resources not requested by server 1
+        W.add_store_sums(s)
+        e = Engine(0)
+        e.load(s)
+        leaves.append(e)
+        snaps.append(s)
+    root = Engine(0)
+    rsnap = H.root_snapshot(R, G, W.FAIR_SHARE, 1000.0, lease_length_s=20)
+    root.load(rsnap)
+    dev = torch.device("cuda", 0)
+    gathered = torch.empty((G * R, 2), dtype=torch.float64, device=dev)
+    for g, e in enumerate(leaves):
+        e.publish_totals(gathered[g * R:(g + 1) * R].data_ptr())
+        e.sync()
+    from doorman_amd import _lib
+    _lib.check(_lib.lib().dm_hier_load_root(root._ctx, gathered.data_ptr(), G, NOW), root._ctx)
+    root.apportion(NOW, writeback=True, recompute=True)
+    rg, rexp = root.leases()
+    # model: totals as published (store SumWants / Count, server.go:241-249)
+    host = gathered.cpu().numpy()
+    totals = [(host[g * R:(g + 1) * R, 0].copy(), host[g * R:(g + 1) * R, 1].copy().view(np.int64))
+              for g in range(G)]
+    for g in range(G):
+        np.testing.assert_array_equal(totals[g][1], snaps[g]["agg_count"])
+    msnap = M.root_from_totals(totals, 1000.0, W.FAIR_SHARE, 20, np.zeros(R * G), NOW)
+    mout = O.apportion(msnap, NOW)
+    assert_leases_match(msnap, rg, rexp, mout, f"root G={G}")
+    for g, e in enumerate(leaves):
+        _lib.check(_lib.lib().dm_hier_take_grants(root._ctx, e._ctx, g), root._ctx)
+        cap, parent, live = M.grants(msnap, mout, G, g)
+        leaf = dict(snaps[g])
+        leaf["capacity"] = np.where(live, cap, snaps[g]["capacity"])
+        leaf["parent_expiry_ns"] = np.where(live, parent, snaps[g]["parent_expiry_ns"])
+        e.apportion(NOW, writeback=False)
+        gets, exp = e.leases()
+        assert_leases_match(leaf, gets, exp, O.apportion(leaf, NOW), f"leaf {g} of {G}")
+        # and past the grant's expiry the leaf's capacity is 0 (resource.go:62-70)
+        later = NOW + 25 * W.NS
+        e.apportion(later, writeback=False)
+        gets2, exp2 = e.leases()
+        assert_leases_match(leaf, gets2, exp2, O.apportion(leaf, later), f"leaf {g} after parent expiry")
+    for e in leaves + [root]:
+        e.close()

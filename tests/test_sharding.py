@@ -1,0 +1,95 @@
+"""Resource sharding and the hierarchy exchange on CPU (no GPU): the partition
+function, and a world_size-2 gloo run of the publish -> all-gather -> root ->
+grant exchange with the oracle as the evaluator."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from doorman_amd import hierarchy as H
+from doorman_amd import workloads as W
+from oracle import oracle as O
+import hier_model as M
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_partition_balanced_contiguous(world):
+    sizes = W.zipf_sizes(50_000, 50_000)
+    b = H.partition(sizes, world)
+    assert b[0] == 0 and b[-1] == len(sizes) and np.all(np.diff(b) >= 0)
+    loads = np.add.reduceat(sizes, b[:-1]) if world > 1 else [sizes.sum()]
+    # a shard can exceed the mean only by the single resource straddling its boundary
+    assert max(loads) <= sizes.sum() / world + sizes.max()
+
+
+def test_partition_uniform_is_even():
+    sizes = np.full(10_000, 1000)
+    b = H.partition(sizes, 8)
+    assert np.all(np.diff(b) == 1250)
+
+
+def test_shard_roundtrip():
+    rng = np.random.default_rng(0)
+    snap = W.random_snapshot(rng, 40, 30)
+    parts = [H.shard(snap, 3, k) for k in range(3)]
+    assert sum(len(p["wants"]) for p in parts) == len(snap["wants"])
+    full = O.apportion(snap, W.NOW_NS)
+    got = np.concatenate([O.apportion(p, W.NOW_NS)["gets"] for p in parts])
+    np.testing.assert_array_equal(got, full["gets"])  # resources are independent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, R, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    now = W.NOW_NS
+    leaf = W.uniform(R, 50 + 10 * rank, kind=W.FAIR_SHARE, seed=100 + rank)
+    sw, cnt = M.leaf_totals(leaf, now)
+    rec = torch.tensor(np.stack([sw, cnt.view(np.float64)], axis=1))  # the 16-byte device records
+    out = [torch.empty_like(rec) for _ in range(world)]
+    dist.all_gather(out, rec)
+    totals = [(o[:, 0].numpy().copy(), o[:, 1].numpy().copy().view(np.int64)) for o in out]
+    root = M.root_from_totals(totals, 1000.0, W.FAIR_SHARE, 20, np.zeros(R * world), now)
+    ro = O.apportion(root, now, "closed")
+    cap, parent, live = M.grants(root, ro, world, rank)
+    q.put((rank, cap, parent, live, sw, cnt))
+    dist.destroy_process_group()
+
+
+def test_hierarchy_exchange_gloo_world2():
+    import torch.multiprocessing as mp
+    R, world = 16, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, cap, parent, live, sw, cnt = q.get(timeout=120)
+        res[rank] = (cap, parent, live, sw, cnt)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the same root, evaluated centrally from both servers' totals
+    totals = [(res[g][3], res[g][4]) for g in range(world)]
+    root = M.root_from_totals(totals, 1000.0, W.FAIR_SHARE, 20, np.zeros(R * world), W.NOW_NS)
+    ro = O.apportion(root, W.NOW_NS)
+    for g in range(world):
+        cap, parent, live = M.grants(root, ro, world, g)
+        np.testing.assert_array_equal(res[g][0], cap)
+        np.testing.assert_array_equal(res[g][1], parent)
+    # every server asked for more than its share: FairShare splits the capacity by subclients
+    tot = res[0][0] + res[1][0]
+    assert np.all(tot <= 1000.0 + 1e-9)
