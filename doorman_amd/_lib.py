@@ -56,6 +56,7 @@ class KernelTime(ctypes.Structure):
 
 
 _lib = None
+_variants = {}
 
 _SIGS = {
     "dm_version": (ctypes.c_char_p, []),
@@ -94,24 +95,33 @@ def header_symbols() -> list[str]:
     return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(dm_\w+)\s*\(", text, flags=re.M)))
 
 
-def lib():
-    """Load the HIP library (raises if it was not built: there is no CPU fallback)."""
+def _bind(path):
+    L = ctypes.CDLL(path)  # RTLD_LOCAL: several builds can coexist in one process (A/B runs)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+def lib(path: str | None = None):
+    """Load the HIP library (raises if it was not built: there is no CPU fallback).
+    `path` selects another build of the same ABI (tools/ab.py)."""
     global _lib
+    if path is not None and os.path.abspath(path) != LIB_PATH:
+        if path not in _variants:
+            _variants[path] = _bind(path)
+        return _variants[path]
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                                "(make -C doorman_amd/csrc); there is no CPU fallback")
-        L = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGS.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = _bind(LIB_PATH)
     return _lib
 
 
-def check(rc: int, ctx=None) -> int:
+def check(rc: int, ctx=None, L=None) -> int:
     if rc < 0:
-        msg = lib().dm_last_error(ctx)
+        msg = (L or lib()).dm_last_error(ctx)
         raise DmError(rc, msg.decode() if msg else "")
     return rc

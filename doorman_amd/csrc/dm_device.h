@@ -15,7 +15,7 @@ constexpr int64_t kNs = 1000000000LL;
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
 constexpr int kSmallMax = 16;
 constexpr int kLargeMin = 4096;
-constexpr int kChunkRows = 4096;
+constexpr int kChunkRows = 2048;
 constexpr int kNumBins = 6;  // 64x1, 256x1, 256x2, 256x4, 512x4, 1024x4
 
 struct Pack {  // a run of consecutive small resources covering <= 64 rows

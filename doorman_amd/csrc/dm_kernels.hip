@@ -367,6 +367,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     s[k] = 0;
     if (i < n) {
       const unsigned u = (unsigned)i;
+      // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
       w[k] = wb[u];
       h[k] = hb[u];
       s[k] = (int)sb[u];
@@ -675,14 +676,19 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     const int lj = __shfl(lv, j & 63, 64);
     if (owner && j < ohi && lj) osh += gj - hj;
   }
+  // SetSafeCapacity inputs from the resource's first row lane (no second config load)
+  Res ors;
+  ors.cap_cfg = __shfl(rs.cap_cfg, olo & 63, 64);
+  ors.safe = __shfl(rs.safe, olo & 63, 64);
   if (owner) {
     const int oseg = pk.first_seg + lane;
     if (olo == ohi) {  // resource without rows
       ocount = p.recompute ? 0 : p.agg[oseg].count;
       osh = p.recompute ? 0.0 : p.agg[oseg].sum_has;
       osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
+      ors.cap_cfg = p.cfg[oseg].capacity;
+      ors.safe = p.cfg[oseg].safe_capacity;
     }
-    const Res ors = load_res(p, oseg);
     Clean oc{ocount, osh, osw};
     write_resource(p, oseg, ors, oc, 0.0);
   }
@@ -745,30 +751,62 @@ __device__ __forceinline__ AggC seg_c(const Partials& P, const LargeSeg& L, Lds<
   return group_reduce<G>(c, OpC(), lds.c);
 }
 
+// kChunkRows rows of one chunk, kLR per thread, loaded in one batch (all loads in
+// flight before the first use).
+constexpr int kLR = kChunkRows / 256;
+struct ChunkRows {
+  double w[kLR], h[kLR];
+  int s[kLR];
+  unsigned valid, live;
+};
+__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r) {
+  const double* __restrict__ wb = p.wants + ch.row0;
+  const double* __restrict__ hb = p.has + ch.row0;
+  const int64_t* __restrict__ sb = p.sub + ch.row0;
+  const int64_t* __restrict__ eb = p.expiry + ch.row0;
+  r.valid = 0;
+  r.live = 0;
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    const int i = k * 256 + threadIdx.x;
+    r.w[k] = 0.0;
+    r.h[k] = 0.0;
+    r.s[k] = 0;
+    if (i < ch.nrows) {
+      const unsigned u = (unsigned)i;
+      r.w[k] = wb[u];
+      r.h[k] = hb[u];
+      r.s[k] = (int)sb[u];
+      r.valid |= 1u << k;
+      if (!(p.now > eb[u])) r.live |= 1u << k;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
+  ChunkRows rw;
+  load_chunk(p, ch, rw);
   AggA a = zeroA();
-  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
-    const int64_t row = ch.row0 + i;
-    const double w = p.wants[row], h = p.has[row];
-    const long long s = p.sub[row];
-    const bool lv = !(p.now > p.expiry[row]);
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.valid >> k & 1)) continue;
+    const bool lv = rw.live >> k & 1;
     if (!lv) {
-      a.cnt += s;
-      a.h += h;
-      a.w += w;
+      a.cnt += rw.s[k];
+      a.h += rw.h[k];
+      a.w += rw.w[k];
     }
     if (p.recompute) {
-      a.all.cnt += s;
-      a.all.h += h;
-      a.all.w += w;
+      a.all.cnt += rw.s[k];
+      a.all.h += rw.h[k];
+      a.all.w += rw.w[k];
     }
     if (lv) {
-      const int si = (int)s;
-      a.smin = si < a.smin ? si : a.smin;
-      a.smax = si > a.smax ? si : a.smax;
-      a.nan |= __builtin_isnan(w) ? 1 : 0;
+      a.smin = rw.s[k] < a.smin ? rw.s[k] : a.smin;
+      a.smax = rw.s[k] > a.smax ? rw.s[k] : a.smax;
+      a.nan |= __builtin_isnan(rw.w[k]) ? 1 : 0;
     }
   }
   {
@@ -797,12 +835,14 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
   const SegState st = seg_state<256>(p, P, ls[ch.lseg], lds);
   if (st.general || st.rs.learning || st.rs.kind < 2) return;
   const double eq = st.rs.C / (double)st.cl.count;
+  ChunkRows rw;
+  load_chunk(p, ch, rw);
   AggB b{0.0, 0.0, 0};
-  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
-    const int64_t row = ch.row0 + i;
-    if (p.now > p.expiry[row]) continue;
-    const double w = p.wants[row];
-    const long long s = p.sub[row];
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.live >> k & 1)) continue;
+    const double w = rw.w[k];
+    const int s = rw.s[k];
     if (st.rs.kind == 2) {
       const double e = eq * (double)s;
       if (w < e)
@@ -836,12 +876,14 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
   const double eq = st.rs.C / (double)st.cl.count;
   const double s0 = (double)st.a.smin;
   const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
+  ChunkRows rw;
+  load_chunk(p, ch, rw);
   AggC c{0.0, 0};
-  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
-    const int64_t row = ch.row0 + i;
-    if (p.now > p.expiry[row]) continue;
-    const double w = p.wants[row];
-    const long long s = p.sub[row];
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.live >> k & 1)) continue;
+    const double w = rw.w[k];
+    const int s = rw.s[k];
     if (!(w > (double)s * eq)) continue;
     if (w < Tu)
       c.ee += Tu - w;
@@ -870,18 +912,22 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   if (!rs.learning && rs.kind >= 2) b = seg_b<256>(P, L, lds);
   if (!rs.learning && rs.kind == 3) c = seg_c<256>(P, L, lds);
   const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
+  ChunkRows rw;
+  load_chunk(p, ch, rw);
+  double* gb = p.out_gets + ch.row0;
+  int64_t* xb = p.out_expiry + ch.row0;
   SumD delta{0.0};
-  for (int i = threadIdx.x; i < ch.nrows; i += 256) {
-    const int64_t row = ch.row0 + i;
-    const double w = p.wants[row], h = p.has[row];
-    const long long s = p.sub[row];
-    const bool lv = !(p.now > p.expiry[row]);
-    if (!lv) {
-      __builtin_nontemporal_store(0.0, p.out_gets + row);
-      __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row);
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.valid >> k & 1)) continue;
+    const unsigned u = (unsigned)(k * 256 + threadIdx.x);
+    const double w = rw.w[k], h = rw.h[k];
+    if (!(rw.live >> k & 1)) {
+      __builtin_nontemporal_store(0.0, gb + u);
+      __builtin_nontemporal_store((int64_t)kReleased, xb + u);
       if (p.out_wants) {
-        p.out_wants[row] = 0.0;
-        p.out_sub[row] = 0;
+        p.out_wants[ch.row0 + u] = 0.0;
+        p.out_sub[ch.row0 + u] = 0;
       }
       continue;
     }
@@ -893,14 +939,14 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     } else if (rs.kind == 1) {
       g = minF(C, w);
     } else if (rs.kind == 2) {
-      const double epc = eq * (double)s;
+      const double epc = eq * (double)rw.s[k];
       const double unused = C - st.cl.sum_has + h;
       g = (st.cl.sum_wants <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (b.x / b.y), unused);
     } else {
       g = fs_uniform_row(w, h, C, st.cl.sum_has, fu);
     }
-    __builtin_nontemporal_store(g, p.out_gets + row);
-    __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
+    __builtin_nontemporal_store(g, gb + u);
+    __builtin_nontemporal_store((int64_t)rs.exp_out, xb + u);
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);

@@ -91,6 +91,10 @@ struct dm_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  // auxiliary streams: independent size bins of one tick run concurrently
+  static constexpr int kAux = 3;
+  hipStream_t aux[kAux] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[kAux] = {};
   std::string err;
 
   int64_t R = 0, N = 0;
@@ -353,6 +357,16 @@ int dm_create(int device, dm_ctx** out) {
     return DM_E_HIP;
   }
   c->stream = c->own_stream;
+  for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
+    e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
+    dm_destroy(c);
+    return DM_E_HIP;
+  }
   *out = c;
   return DM_OK;
 }
@@ -364,6 +378,14 @@ void dm_destroy(dm_ctx* c) {
   c->collect_profile();
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   c->free_all();
+  for (int i = 0; i < dm_ctx::kAux; ++i) {
+    if (c->aux[i]) {
+      (void)hipStreamSynchronize(c->aux[i]);
+      (void)hipStreamDestroy(c->aux[i]);
+    }
+    if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -518,12 +540,12 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p};
   hipStream_t st = c->stream;
-  auto timed = [&](int cls, auto&& fn) -> hipError_t {
+  auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t {
     if (!c->profiling) return fn();
     ProfEvent pe{cls, c->take_event(), c->take_event()};
-    (void)hipEventRecord(pe.a, st);
+    (void)hipEventRecord(pe.a, s);
     hipError_t e = fn();
-    (void)hipEventRecord(pe.b, st);
+    (void)hipEventRecord(pe.b, s);
     c->pending.push_back(pe);
     return e;
   };
@@ -531,22 +553,42 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
   if (c->maybe_general) DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
-  // large resources first (longest dependency chain), then the binned groups
+  // Independent work classes: large resources (a 5-kernel chain), big groups,
+  // small groups + packed.  With more than one class present they run on the
+  // auxiliary streams concurrently, forked from and joined back to the main stream.
+  int big_bins = 0, small_bins = 0;
+  for (int b = 3; b < kNumBins; ++b) big_bins += !c->h_bins[b].empty();
+  for (int b = 0; b < 3; ++b) small_bins += !c->h_bins[b].empty();
+  const bool has_small = small_bins > 0 || !c->h_packs.empty();
+  const int classes = (nch > 0) + (big_bins > 0) + has_small;
+  const bool fork = classes > 1;
+  hipStream_t s_large = fork ? c->aux[0] : st, s_big = fork ? c->aux[1] : st, s_small = fork ? c->aux[2] : st;
+  if (fork) {
+    DM_HIP(c, hipEventRecord(c->ev_fork, st), "fork");
+    for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork");
+  }
   for (int ph = 0; ph < 5 && nch > 0; ++ph)
-    DM_HIP(c, timed(KC_LARGE_A + ph,
-                    [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, st); }),
+    DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
+                    [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
            "large-resource kernels");
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    DM_HIP(c, timed(KC_BIN0 + b, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, st); }), "group kernel");
+    hipStream_t s = b >= 3 ? s_big : s_small;
+    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }), "group kernel");
   }
   if (!c->h_packs.empty())
-    DM_HIP(c, timed(KC_SMALL, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), st); }),
+    DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), s_small); }),
            "small kernel");
+  if (fork) {
+    for (int i = 0; i < dm_ctx::kAux; ++i) {
+      DM_HIP(c, hipEventRecord(c->ev_join[i], c->aux[i]), "join");
+      DM_HIP(c, hipStreamWaitEvent(st, c->ev_join[i], 0), "join");
+    }
+  }
   if (c->maybe_general && c->n_nonsmall > 0) {
     const int blocks = (int)std::min<int64_t>(c->n_nonsmall, 1024);
-    DM_HIP(c, timed(KC_GENERAL, [&] { return launch_general(p, gl, gc, blocks, st); }), "general kernel");
+    DM_HIP(c, timed(KC_GENERAL, st, [&] { return launch_general(p, gl, gc, blocks, st); }), "general kernel");
   }
   c->last_writeback = wb;
   c->have_result = true;
@@ -732,13 +774,13 @@ int dm_hier_load_root(dm_ctx* root, const void* gathered, int n_servers, int64_t
   if (!gathered) return root->fail(DM_E_INVAL, "null gathered buffer");
   if (!root_layout_ok(root, n_servers))
     return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows");
+  // stream-ordered (no host sync): the all-gather that produced `gathered` must be
+  // ordered before this call on the same stream (dm_set_stream)
   DM_HIP(root, launch_hier_root(root->R, n_servers, gathered, root->wants.p, root->has.p, root->sub.p,
                                 root->expiry.p, now_ns, root->stream),
          "hier root update");
-  // the rows changed: rebuild the running sums the next tick consumes
-  root->maybe_general = true;
+  root->maybe_general = true;  // rows now carry heterogeneous subclient counts
   root->have_result = false;
-  DM_HIP(root, hipStreamSynchronize(root->stream), "hier root update");
   return DM_OK;
 }
 
@@ -753,9 +795,17 @@ int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server) {
   if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
   const double* gets = root->last_writeback ? root->has.p : root->out_gets.p;
   const int64_t* exp = root->last_writeback ? root->expiry.p : root->out_expiry.p;
-  DM_HIP(root, hipStreamSynchronize(leaf->stream), "leaf sync");
+  // stream-ordered hand-off: root stream after leaf's prior work, leaf after the update
+  const bool same = root->stream == leaf->stream;
+  if (!same) {
+    DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
+    DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
+  }
   DM_HIP(root, launch_hier_grants(root->R, G, server, gets, exp, leaf->cfg.p, root->stream), "hier grants");
-  DM_HIP(root, hipStreamSynchronize(root->stream), "hier grants");
+  if (!same) {
+    DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
+    DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
+  }
   return DM_OK;
 }
 

@@ -30,9 +30,10 @@ def _c(a, dt):
 class Engine:
     """One GPU context owning a device-resident columnar lease store."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lib_path: str | None = None):
+        self._L = _lib.lib(lib_path)
         self._ctx = ctypes.c_void_p()
-        check(lib().dm_create(device, ctypes.byref(self._ctx)))
+        check(self._L.dm_create(device, ctypes.byref(self._ctx)), None, self._L)
         self.device = device
         self.n_resources = 0
         self.n_leases = 0
@@ -40,7 +41,7 @@ class Engine:
     # -- lifetime --
     def close(self):
         if self._ctx:
-            lib().dm_destroy(self._ctx)
+            self._L.dm_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
 
     def __del__(self):
@@ -56,17 +57,17 @@ class Engine:
         self.close()
 
     def _chk(self, rc):
-        return check(rc, self._ctx)
+        return check(rc, self._ctx, self._L)
 
     @property
     def stream(self) -> int:
-        return lib().dm_get_stream(self._ctx) or 0
+        return self._L.dm_get_stream(self._ctx) or 0
 
     def set_stream(self, stream_ptr: int | None):
-        self._chk(lib().dm_set_stream(self._ctx, stream_ptr))
+        self._chk(self._L.dm_set_stream(self._ctx, stream_ptr))
 
     def sync(self):
-        self._chk(lib().dm_sync(self._ctx))
+        self._chk(self._L.dm_sync(self._ctx))
 
     # -- LeaseStore --
     def load(self, snap: dict):
@@ -96,7 +97,7 @@ class Engine:
             s.agg_count = _ptr(keep["agg_count"])
             s.agg_sum_has = _ptr(keep["agg_sum_has"])
             s.agg_sum_wants = _ptr(keep["agg_sum_wants"])
-        self._chk(lib().dm_store_load(self._ctx, ctypes.byref(s)))
+        self._chk(self._L.dm_store_load(self._ctx, ctypes.byref(s)))
         self.n_resources, self.n_leases = s.n_resources, s.n_leases
 
     def load_config(self, snap: dict):
@@ -111,24 +112,24 @@ class Engine:
             "safe_capacity": _c(snap["safe_capacity"], np.float64),
         }
         cfg = _lib.ResourceCfg(*[_ptr(keep[k]) for k in CFG_FIELDS])
-        self._chk(lib().dm_config_load(self._ctx, R, ctypes.byref(cfg)))
+        self._chk(self._L.dm_config_load(self._ctx, R, ctypes.byref(cfg)))
 
     def upsert(self, rows, has, wants, subclients, expiry_ns):
         """Assign on existing rows (store.go:153-167)."""
         rows = _c(rows, np.int64)
         a = [_c(has, np.float64), _c(wants, np.float64), _c(subclients, np.int64), _c(expiry_ns, np.int64)]
-        self._chk(lib().dm_store_upsert(self._ctx, len(rows), _ptr(rows), *[_ptr(x) for x in a]))
+        self._chk(self._L.dm_store_upsert(self._ctx, len(rows), _ptr(rows), *[_ptr(x) for x in a]))
 
     def release(self, rows):
         """Release (store.go:142-151)."""
         rows = _c(rows, np.int64)
-        self._chk(lib().dm_store_release(self._ctx, len(rows), _ptr(rows)))
+        self._chk(self._L.dm_store_release(self._ctx, len(rows), _ptr(rows)))
 
     def read_store(self, off: int = 0, n: int | None = None) -> dict:
         n = self.n_leases - off if n is None else n
         out = {"has": np.empty(n), "wants": np.empty(n), "subclients": np.empty(n, np.int64),
                "expiry_ns": np.empty(n, np.int64)}
-        self._chk(lib().dm_read_store(self._ctx, off, n, _ptr(out["has"]), _ptr(out["wants"]),
+        self._chk(self._L.dm_read_store(self._ctx, off, n, _ptr(out["has"]), _ptr(out["wants"]),
                                       _ptr(out["subclients"]), _ptr(out["expiry_ns"])))
         return out
 
@@ -136,18 +137,18 @@ class Engine:
     def apportion(self, now_ns: int, writeback: bool = False, recompute: bool = False, asynchronous: bool = False):
         flags = ((_lib.DM_WRITEBACK if writeback else 0) | (_lib.DM_AGG_RECOMPUTE if recompute else 0)
                  | (_lib.DM_ASYNC if asynchronous else 0))
-        self._chk(lib().dm_apportion(self._ctx, int(now_ns), flags))
+        self._chk(self._L.dm_apportion(self._ctx, int(now_ns), flags))
 
     def leases(self, off: int = 0, n: int | None = None):
         n = self.n_leases - off if n is None else n
         gets, exp = np.empty(n), np.empty(n, np.int64)
-        self._chk(lib().dm_read_leases(self._ctx, off, n, _ptr(gets), _ptr(exp)))
+        self._chk(self._L.dm_read_leases(self._ctx, off, n, _ptr(gets), _ptr(exp)))
         return gets, exp
 
     def leases_proto(self, off: int = 0, n: int | None = None):
         n = self.n_leases - off if n is None else n
         cap, exp, ref = np.empty(n), np.empty(n, np.int64), np.empty(n, np.int64)
-        self._chk(lib().dm_read_leases_proto(self._ctx, off, n, _ptr(cap), _ptr(exp), _ptr(ref)))
+        self._chk(self._L.dm_read_leases_proto(self._ctx, off, n, _ptr(cap), _ptr(exp), _ptr(ref)))
         return cap, exp, ref
 
     def resources(self, r0: int = 0, n: int | None = None, safe: bool = True) -> dict:
@@ -155,29 +156,29 @@ class Engine:
         out = {"count": np.empty(n, np.int64), "sum_has": np.empty(n), "sum_wants": np.empty(n)}
         if safe:
             out["safe_capacity"] = np.empty(n)
-        self._chk(lib().dm_read_resources(self._ctx, r0, n, _ptr(out["count"]), _ptr(out["sum_has"]),
+        self._chk(self._L.dm_read_resources(self._ctx, r0, n, _ptr(out["count"]), _ptr(out["sum_has"]),
                                           _ptr(out["sum_wants"]), _ptr(out.get("safe_capacity"))))
         return out
 
     def publish_totals(self, dev_ptr: int):
         """{SumWants, Count} per resource into a 16 B x R device buffer (server.go:234-255)."""
-        self._chk(lib().dm_publish_totals(self._ctx, ctypes.c_void_p(dev_ptr)))
+        self._chk(self._L.dm_publish_totals(self._ctx, ctypes.c_void_p(dev_ptr)))
 
     # -- profiling --
     def set_profiling(self, on: bool):
-        self._chk(lib().dm_set_profiling(self._ctx, 1 if on else 0))
+        self._chk(self._L.dm_set_profiling(self._ctx, 1 if on else 0))
 
     def kernel_times(self) -> dict:
         arr = (_lib.KernelTime * 32)()
-        n = self._chk(lib().dm_kernel_times(self._ctx, arr, 32))
+        n = self._chk(self._L.dm_kernel_times(self._ctx, arr, 32))
         return {arr[i].name.decode(): (arr[i].launches, arr[i].total_ms) for i in range(n) if arr[i].launches}
 
     def reset_kernel_times(self):
-        self._chk(lib().dm_reset_kernel_times(self._ctx))
+        self._chk(self._L.dm_reset_kernel_times(self._ctx))
 
     def plan_info(self) -> dict:
         arr = (ctypes.c_int64 * 16)()
-        n = self._chk(lib().dm_plan_info(self._ctx, arr, 16))
+        n = self._chk(self._L.dm_plan_info(self._ctx, arr, 16))
         return {_BIN_NAMES[i]: int(arr[i]) for i in range(min(n, len(_BIN_NAMES)))}
 
 

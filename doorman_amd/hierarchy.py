@@ -86,10 +86,11 @@ class HierarchicalTick:
         from . import _lib
         self.leaf.publish_totals(self.totals.data_ptr())
         self.gather(self.totals, self.gathered)
-        _lib.check(_lib.lib().dm_hier_load_root(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns)),
-                   self.root._ctx)
-        self.root.apportion(now_ns, writeback=True, recompute=True)
-        _lib.check(_lib.lib().dm_hier_take_grants(self.root._ctx, self.leaf._ctx, self.g), self.root._ctx)
+        L = self.root._L
+        _lib.check(L.dm_hier_load_root(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns)),
+                   self.root._ctx, L)
+        self.root.apportion(now_ns, writeback=True, recompute=True, asynchronous=True)
+        _lib.check(L.dm_hier_take_grants(self.root._ctx, self.leaf._ctx, self.g), self.root._ctx, L)
 
     def tick(self, now_ns: int, asynchronous: bool = False):
         self.exchange(now_ns)

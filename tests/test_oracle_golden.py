@@ -143,3 +143,39 @@ def test_unknown_kind_is_an_error():
     snap = W.make_snapshot([2], [1, 2], [0, 0], 1, NOW + W.NS, 7, 10.0)
     with pytest.raises(ValueError):
         O.apportion(snap, NOW, "closed")
+
+
+@pytest.mark.parametrize("case", [c for c in KATS["server"] if "error" not in c], ids=lambda c: c["name"])
+def test_server_kats_as_one_row_snapshots(case):
+    """For a single client, Decide on an empty store (the reference's first request)
+    and the snapshot tick of a store holding only that client agree: count,
+    unused capacity, SumWants test and Learn all coincide.  This is what lets the
+    GPU tests replay these KATs through dm_apportion (test_parity_gpu.py)."""
+    for snap, expect in server_kat_snapshots(case):
+        assert O.apportion(snap, NOW)["gets"][0] == expect
+        assert O.apportion(snap, NOW, "literal")["gets"][0] == expect
+
+
+def server_kat_snapshots(case):
+    """(one-row snapshot, expected gets) for every step of a server KAT."""
+    master_at = NOW - W.NS // 2
+    out = []
+    if "bands" in case:
+        wt, st = O.aggregate_bands([b[0] for b in case["bands"]], [b[1] for b in case["bands"]])
+        cfg = _cfg(case, master_at)
+        out.append((W.make_snapshot([1], [wt], [case["has"]], [st], [NOW + W.NS], cfg["kind"], cfg["capacity"],
+                                    cfg["lease_length_s"], cfg["refresh_interval_s"], cfg["learning_end_ns"]),
+                    case["gets"]))
+        return out
+    cfg = _cfg(case, master_at)
+    for step in case["steps"]:
+        if step.get("new_resource"):
+            cfg = _cfg(case, NOW - step["age_s"] * W.NS)
+        if step.get("after_reload"):
+            new = _cfg(dict(case["reload"]), master_at)
+            new["learning_end_ns"] = cfg["learning_end_ns"]
+            cfg = new
+        out.append((W.make_snapshot([1], [step["wants"]], [step["has"]], [1], [NOW + W.NS], cfg["kind"],
+                                    cfg["capacity"], cfg["lease_length_s"], cfg["refresh_interval_s"],
+                                    cfg["learning_end_ns"]), step["gets"]))
+    return out

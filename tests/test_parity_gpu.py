@@ -252,3 +252,33 @@ def test_c2_zipf_full_size_sampled(eng):
     sample = np.unique(np.concatenate([[0, 1, 2, 3, 7, 100, 121, 122, 243, 244],
                                        rng.choice(1_000_000, 300, replace=False)]))
     _sample_check(eng, snap, sample, "C2")
+
+
+@pytest.mark.parametrize("case", [c for c in KATS["server"] if "error" not in c], ids=lambda c: c["name"])
+def test_server_kats_through_the_abi(eng, case):
+    """server_test.go:339-553 (learning mode 20/90/100, learning persists across
+    LoadConfig, GetServerCapacity bands -> 100) as one-client ticks on the device."""
+    from test_oracle_golden import server_kat_snapshots
+    for snap, expect in server_kat_snapshots(case):
+        gets, exp, _ = run(eng, snap)
+        assert gets[0] == expect
+
+
+def test_wrong_number_of_clients_through_the_abi():
+    """server_test.go:483-503: num_clients < 1 is codes.InvalidArgument."""
+    from doorman_amd._lib import DM_E_ARGUMENT, DmError
+    from doorman_amd.engine import aggregate_bands
+    with pytest.raises(DmError) as e:
+        aggregate_bands([10.0], [0])
+    assert e.value.code == DM_E_ARGUMENT
+
+
+def test_lease_length_and_refresh_interval_through_the_abi(eng):
+    """algorithm_test.go:495-522: expiry = now + lease_length, refresh as configured."""
+    k = KATS["lease_length"]
+    snap = W.make_snapshot([1], [k["wants"]], [0.0], [k["sub"]], NOW + W.NS, k["kind"], k["capacity"],
+                           k["lease_length"], k["refresh_interval"])
+    run(eng, snap)
+    cap, exp_s, ref_s = eng.leases_proto()
+    assert exp_s[0] - NOW // W.NS == k["expiry_minus_now_s"]
+    assert ref_s[0] == k["refresh_s"]

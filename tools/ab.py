@@ -1,0 +1,67 @@
+"""Interleaved A/B timing of library builds in ONE process (cdna guide §5.4 rule 24).
+
+  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so ...
+
+Every build gets its own context with the same snapshot; rounds alternate between
+builds; per build the per-launch kernel time (HIP events) and the tick wall time
+are reported as median and min over rounds.
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402,F401  (one HIP runtime)
+
+from bench import algorithmic_bytes, make_workload  # noqa: E402
+from doorman_amd import workloads as W  # noqa: E402
+from doorman_amd.engine import Engine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--workload", default="c1")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    snap = make_workload(args.workload, 0)
+    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
+    engines = []
+    for p in args.libs:
+        e = Engine(0, os.path.abspath(p))
+        e.load(snap)
+        for _ in range(3):
+            e.apportion(W.NOW_NS, writeback=True)
+        engines.append(e)
+    res = {p: {"tick_us": [], "kern_us": []} for p in args.libs}
+    for _ in range(args.rounds):
+        for p, e in zip(args.libs, engines):
+            e.set_profiling(True)
+            e.reset_kernel_times()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                e.apportion(W.NOW_NS, writeback=True, asynchronous=True)
+            e.sync()
+            dt = time.perf_counter() - t0
+            kt = e.kernel_times()
+            e.set_profiling(False)
+            res[p]["tick_us"].append(dt / args.steps * 1e6)
+            res[p]["kern_us"].append(sum(v[1] for v in kt.values()) / args.steps * 1e3)
+    alg = algorithmic_bytes(N, R)
+    for p in args.libs:
+        k = res[p]["kern_us"]
+        t = res[p]["tick_us"]
+        print(f"{os.path.basename(p):34s} kernel med {statistics.median(k):8.2f} us min {min(k):8.2f} "
+              f"({alg / min(k) / 1e3:7.1f} GB/s best) | tick med {statistics.median(t):8.2f} us")
+    for e in engines:
+        e.close()
+
+
+if __name__ == "__main__":
+    main()
