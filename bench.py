@@ -32,6 +32,9 @@ WORKLOADS = {
     "c1ps": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), ProportionalShare",
     "c2": "C2 (BASELINE configs[2]): 1M resources, Zipf 1..1M clients (13,970,034 leases), mixed kinds, 5% learning",
     "c3": "C3 shape on one GPU (north-star target): 100,000 resources x 1,000 clients (100M leases), FairShare",
+    "c4": "C4 (BASELINE configs[4]) per GPU: 125M-lease device-resident store (1B over 8 GPUs), 125k resources x "
+          "1k client slots, FS/PS mixed, 5% learning; every step = 5 s refresh tick: 10% wants updates and 1% "
+          "departures + 1% new clients over PCIe, then the tick",
 }
 
 
@@ -45,6 +48,19 @@ def make_workload(name: str, rank: int):
         return W.c2(seed=2 + 1000 * rank)
     if name == "c3":
         return W.uniform(100_000, 1_000, kind=W.FAIR_SHARE, seed=3 + 1000 * rank)
+    if name == "c4":
+        snap = W.uniform(125_000, 1_000, kind="mixed", seed=4 + 1000 * rank)
+        rng = np.random.default_rng(40 + rank)
+        R = len(snap["seg_off"]) - 1
+        snap["learning_end_ns"] = np.where(rng.random(R) < 0.05, W.NOW_NS + 3600 * W.NS,
+                                           W.INT64_MIN).astype(np.int64)
+        free = rng.random(len(snap["wants"])) < 0.02  # slack slots for new clients
+        snap["wants"][free] = 0.0
+        snap["has"][free] = 0.0
+        snap["subclients"] = np.where(free, 0, 1).astype(np.int64)
+        snap["expiry_ns"][free] = W.RELEASED
+        snap["expiry_ns"][~free] = W.NOW_NS + 3600 * W.NS
+        return W.add_store_sums(snap)
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -70,6 +86,44 @@ def kernel_units(eng, snap):
     for name in ("large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
         units[name] = (int(sizes[big].sum()), int(big.sum()))
     return units
+
+
+def streaming_step(eng, snap, rank):
+    """configs[4]: one 5 s refresh tick of a device-resident store.  The host keeps
+    only which rows are live; per tick it sends 10% wants updates
+    (dm_store_update_wants, 12 B each), releases 1% of the clients (departures,
+    store.go:142-151) and inserts 1% new clients into free slots (dm_store_upsert
+    onto released rows), then the tick runs with writeback."""
+    from doorman_amd import workloads as W
+    rng = np.random.default_rng(400 + rank)
+    N = len(snap["wants"])
+    alive = snap["expiry_ns"] != W.RELEASED
+    state = {"now": W.NOW_NS, "tick": 0, "pool": np.flatnonzero(~alive)}
+    fair = 1.0  # C/n of the uniform generator
+
+    def step():
+        state["tick"] += 1
+        off = int(rng.integers(0, 10))
+        upd = np.arange(off, N, 10, dtype=np.int64)
+        upd = upd[alive[upd]]
+        eng.update_wants(upd, rng.uniform(0.5, 1.5, len(upd)) * fair)
+        off = int(rng.integers(0, 100))
+        gone = np.arange(off, N, 100, dtype=np.int64)
+        gone = gone[alive[gone]]
+        pool = state["pool"]
+        new = pool[: len(gone)]
+        state["pool"] = np.concatenate([pool[len(gone):], gone])  # departed slots are reused later
+        eng.release(gone)
+        alive[gone] = False
+        if len(new):
+            k = len(new)
+            eng.upsert(new, np.zeros(k), rng.uniform(0.5, 1.5, k) * fair, np.ones(k, np.int64),
+                       np.full(k, state["now"] + 3600 * W.NS, np.int64))
+            alive[new] = True
+        state["now"] += 5 * W.NS
+        eng.apportion(state["now"], writeback=True, asynchronous=True)
+
+    return step
 
 
 def cpu_baseline(snap, now_ns, budget_s=12.0):
@@ -146,6 +200,8 @@ def main():
 
     step = lambda: eng.apportion(now, writeback=True, asynchronous=True)  # noqa: E731
     root = None
+    if args.workload == "c4":
+        step = streaming_step(eng, snap, rank)
     if args.hier:
         from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
         root = Engine(local_rank)
@@ -163,20 +219,30 @@ def main():
     for _ in range(args.warmup):
         step()
     eng.sync()
-    eng.set_profiling(True)
-    eng.reset_kernel_times()
+    # timed region: only a start/stop HIP event pair on the engine's stream
+    ext = torch.cuda.ExternalStream(eng.stream)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(ext)
     for _ in range(args.steps):
         step()
+    ev1.record(ext)
     eng.sync()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    stream_ms = ev0.elapsed_time(ev1)
+    # profiled region (same steps): HIP events around every kernel launch, on the
+    # stream each kernel runs on, for the per-kernel roofline
+    eng.set_profiling(True)
+    eng.reset_kernel_times()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
     ktimes = eng.kernel_times()
     eng.set_profiling(False)
-
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     n = torch.tensor([N], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -205,7 +271,8 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2),
-                    "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3)}
+                    "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
+                    "timed_region_stream_us_per_step": round(stream_ms * 1e3 / args.steps, 2)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1100,14 +1100,27 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
 // Assign on existing rows (store.go:153-167): running sums += new - old.
 // Rows are applied in order by one thread per resource group? No: rows may hit
 // the same resource, so sums are accumulated with 64-bit atomics of the deltas.
+// resource owning row r: last s with seg_off[s] <= r (binary search, R+1 offsets)
+__device__ __forceinline__ int seg_of_row(const int64_t* __restrict__ seg_off, int64_t R, int64_t r) {
+  int64_t lo = 0, hi = R;  // invariant: seg_off[lo] <= r < seg_off[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= r)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return (int)lo;
+}
+
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
-                         const int64_t* __restrict__ expiry, const int32_t* __restrict__ row_seg, double* s_has,
-                         double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
+                         const int64_t* __restrict__ expiry, const int64_t* __restrict__ seg_off, int64_t R,
+                         double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = rows[i];
-  const int seg = row_seg[i];
+  const int seg = seg_of_row(seg_off, R, r);
   const double dh = has[i] - s_has[r], dw = wants[i] - s_wants[r];
   const long long ds = sub[i] - s_sub[r];
   s_has[r] = has[i];
@@ -1119,12 +1132,12 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
   atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)ds);
 }
 
-__global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int32_t* __restrict__ row_seg,
+__global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int64_t* __restrict__ seg_off, int64_t R,
                           double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = rows[i];
-  const int seg = row_seg[i];
+  const int seg = seg_of_row(seg_off, R, r);
   atomicAdd(&agg[seg].sum_has, -s_has[r]);
   atomicAdd(&agg[seg].sum_wants, -s_wants[r]);
   atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)(-s_sub[r]));
@@ -1132,6 +1145,19 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int
   s_wants[r] = 0.0;
   s_sub[r] = 0;
   s_exp[r] = kReleased;
+}
+
+// Narrow Assign for a refresh that only changes wants (store.go:157):
+// sumWants += new - old.  Rows are unique within one call.
+__global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ wants,
+                               const int64_t* __restrict__ seg_off, int64_t R, double* s_wants, ResAgg* agg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  const int seg = seg_of_row(seg_off, R, r);
+  const double d = wants[i] - s_wants[r];
+  s_wants[r] = wants[i];
+  atomicAdd(&agg[seg].sum_wants, d);
 }
 
 // server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
@@ -1232,18 +1258,25 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 }
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
-                         const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
+                         const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
                          int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, row_seg, s_has, s_wants,
-                                                        s_sub, s_exp, agg);
+  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, seg_off, R, s_has,
+                                                        s_wants, s_sub, s_exp, agg);
   return hipGetLastError();
 }
 
-hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
-                          int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
+hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
+                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, row_seg, s_has, s_wants, s_sub, s_exp, agg);
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, seg_off, R, s_has, s_wants, s_sub, s_exp, agg);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
+                               double* s_wants, ResAgg* agg, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, seg_off, R, s_wants, agg);
   return hipGetLastError();
 }
 

@@ -24,11 +24,13 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
                           hipStream_t st);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
-                         const int64_t* expiry, const int32_t* row_seg, double* s_has, double* s_wants,
+                         const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
                          int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
-hipError_t launch_release(int64_t n, const int64_t* rows, const int32_t* row_seg, double* s_has, double* s_wants,
-                          int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
+hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
+                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
+hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
+                               double* s_wants, ResAgg* agg, hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int64_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
@@ -136,7 +138,7 @@ struct dm_ctx {
   // staging for upsert / release
   DBuf<int64_t> st_rows, st_sub, st_exp;
   DBuf<double> st_has, st_wants;
-  DBuf<int32_t> st_seg;
+  std::vector<uint64_t> seen;  // row bitmap for the uniqueness check, all-zero between calls
   // profiling
   bool profiling = false;
   std::vector<ProfEvent> pending;
@@ -183,7 +185,7 @@ struct dm_ctx {
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
     pa_nan.release();
     glist.release(); gcount.release();
-    st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release(); st_seg.release();
+    st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
   }
 };
 
@@ -678,20 +680,29 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
   return DM_OK;
 }
 
+// Rows of one upsert/release call: in range and unique (a bitmap over the table,
+// O(n + N/64)); the resource of each row is found on the device.
 static int stage_rows(dm_ctx* c, int64_t n, const int64_t* rows) {
-  std::vector<int32_t> seg(n);
-  const auto& so = c->h_seg_off;
-  for (int64_t i = 0; i < n; ++i) {
-    if (rows[i] < 0 || rows[i] >= c->N) return c->fail(DM_E_RANGE, "row out of range");
-    seg[i] = (int32_t)(std::upper_bound(so.begin(), so.end(), rows[i]) - so.begin() - 1);
+  if (c->seen.size() != (size_t)(c->N / 64 + 1)) c->seen.assign((size_t)(c->N / 64 + 1), 0);
+  int rc = DM_OK;
+  int64_t i = 0;
+  for (; i < n; ++i) {
+    const int64_t r = rows[i];
+    if (r < 0 || r >= c->N) {
+      rc = c->fail(DM_E_RANGE, "row out of range");
+      break;
+    }
+    uint64_t& w = c->seen[(size_t)(r >> 6)];
+    const uint64_t bit = 1ull << (r & 63);
+    if (w & bit) {
+      rc = c->fail(DM_E_INVAL, "rows must be unique within one call");
+      break;
+    }
+    w |= bit;
   }
-  std::vector<int64_t> sorted(rows, rows + n);
-  std::sort(sorted.begin(), sorted.end());
-  if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
-    return c->fail(DM_E_INVAL, "rows must be unique within one call");
+  for (int64_t j = 0; j < i; ++j) c->seen[(size_t)(rows[j] >> 6)] = 0;  // O(n) reset
+  if (rc) return rc;
   DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
-  DM_HIP(c, upload(c->st_seg, seg.data(), (size_t)n, c->stream), "stage seg");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "stage");
   return DM_OK;
 }
 
@@ -712,10 +723,27 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   // an upsert can make a resource's subclients heterogeneous: stay conservative
   for (int64_t i = 0; i < n && !c->maybe_general; ++i)
     if (std::isnan(wants[i]) || sub[i] != 1 || !c->all_sub_one) c->maybe_general = true;
-  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->st_seg.p,
+  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->seg_off.p, c->R,
                           c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->stream),
          "upsert");
   DM_HIP(c, hipStreamSynchronize(c->stream), "upsert");
+  c->have_result = false;
+  return DM_OK;
+}
+
+int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants) {
+  DM_CHECK_CTX(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
+  if (n == 0) return DM_OK;
+  for (int64_t i = 0; i < n && !c->maybe_general; ++i)
+    if (std::isnan(wants[i])) c->maybe_general = true;
+  int rc = stage_rows(c, n, rows);
+  if (rc) return rc;
+  DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
+  DM_HIP(c, launch_update_wants(n, c->st_rows.p, c->st_wants.p, c->seg_off.p, c->R, c->wants.p, c->agg.p, c->stream),
+         "update wants");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "update wants");
   c->have_result = false;
   return DM_OK;
 }
@@ -727,8 +755,8 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   if (n == 0) return DM_OK;
   int rc = stage_rows(c, n, rows);
   if (rc) return rc;
-  DM_HIP(c, launch_release(n, c->st_rows.p, c->st_seg.p, c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
-                           c->stream),
+  DM_HIP(c, launch_release(n, c->st_rows.p, c->seg_off.p, c->R, c->has.p, c->wants.p, c->sub.p, c->expiry.p,
+                           c->agg.p, c->stream),
          "release");
   DM_HIP(c, hipStreamSynchronize(c->stream), "release");
   c->have_result = false;

@@ -120,6 +120,11 @@ class Engine:
         a = [_c(has, np.float64), _c(wants, np.float64), _c(subclients, np.int64), _c(expiry_ns, np.int64)]
         self._chk(self._L.dm_store_upsert(self._ctx, len(rows), _ptr(rows), *[_ptr(x) for x in a]))
 
+    def update_wants(self, rows, wants):
+        """Refresh that only changes wants (store.go:153-167, narrow form)."""
+        rows, wants = _c(rows, np.int64), _c(wants, np.float64)
+        self._chk(self._L.dm_store_update_wants(self._ctx, len(rows), _ptr(rows), _ptr(wants)))
+
     def release(self, rows):
         """Release (store.go:142-151)."""
         rows = _c(rows, np.int64)

@@ -282,3 +282,74 @@ def test_lease_length_and_refresh_interval_through_the_abi(eng):
     cap, exp_s, ref_s = eng.leases_proto()
     assert exp_s[0] - NOW // W.NS == k["expiry_minus_now_s"]
     assert ref_s[0] == k["refresh_s"]
+
+
+def test_insert_new_clients_into_free_slots(eng):
+    """New clients: a store keeps released rows (tombstones) as free slots; an upsert
+    onto one is LeaseStore.Assign of a new client (store.go:153-167: sums += new - 0)."""
+    rng = np.random.default_rng(21)
+    sizes = binned_sizes(rng, large=True)
+    snap = snapshot_with_sizes(rng, sizes, expired_frac=0.0, kinds=(2, 3))
+    N = len(snap["wants"])
+    free = rng.choice(N, N // 8, replace=False)  # slack rows, released
+    for k in ("wants", "has"):
+        snap[k][free] = 0.0
+    snap["subclients"][free] = 0
+    snap["expiry_ns"][free] = W.RELEASED
+    W.add_store_sums(snap)
+    eng.load(snap)
+    new = rng.choice(free, len(free) // 2, replace=False)
+    seg_of = np.repeat(np.arange(len(sizes)), sizes)
+    cap_row = snap["capacity"][seg_of[new]]
+    n_row = np.maximum(sizes[seg_of[new]], 1)
+    w = rng.uniform(0, 2, len(new)) * cap_row / n_row
+    h = np.zeros(len(new))
+    s = np.ones(len(new), np.int64)
+    e = np.full(len(new), NOW + 60 * W.NS)
+    eng.upsert(new, h, w, s, e)
+    snap2 = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    snap2["wants"][new], snap2["has"][new], snap2["subclients"][new], snap2["expiry_ns"][new] = w, h, s, e
+    np.add.at(snap2["agg_sum_wants"], seg_of[new], w)
+    np.add.at(snap2["agg_count"], seg_of[new], s)
+    agg = eng.resources(safe=False)
+    np.testing.assert_array_equal(agg["count"], snap2["agg_count"])
+    snap2["agg_sum_wants"], snap2["agg_sum_has"] = agg["sum_wants"], agg["sum_has"]
+    eng.apportion(NOW)
+    gets, exp = eng.leases()
+    ref = O.apportion(snap2, NOW)
+    assert_leases_match(snap2, gets, exp, ref, "after inserts")
+    assert (exp[np.setdiff1d(free, new)] == W.RELEASED).all()
+
+
+def test_upsert_rejects_duplicate_and_out_of_range_rows(eng):
+    from doorman_amd._lib import DM_E_INVAL, DM_E_RANGE, DmError
+    snap = W.make_snapshot([4, 4], np.ones(8), np.zeros(8), 1, NOW + W.NS, 3, 10.0)
+    eng.load(snap)
+    one = np.ones(2)
+    with pytest.raises(DmError) as e:
+        eng.upsert([1, 1], one, one, [1, 1], [NOW, NOW])
+    assert e.value.code == DM_E_INVAL
+    with pytest.raises(DmError) as e:
+        eng.upsert([1, 8], one, one, [1, 1], [NOW, NOW])
+    assert e.value.code == DM_E_RANGE
+
+
+def test_update_wants_narrow_assign(eng):
+    """dm_store_update_wants: Assign of a refresh that changes only wants."""
+    rng = np.random.default_rng(22)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=True), expired_frac=0.0, kinds=(2, 3))
+    eng.load(snap)
+    N = len(snap["wants"])
+    rows = rng.choice(N, N // 5, replace=False)
+    neww = snap["wants"][rows] * rng.uniform(0.5, 2.0, len(rows))
+    eng.update_wants(rows, neww)
+    snap2 = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    seg_of = np.repeat(np.arange(len(snap["seg_off"]) - 1), np.diff(snap["seg_off"]))
+    np.add.at(snap2["agg_sum_wants"], seg_of[rows], neww - snap["wants"][rows])
+    snap2["wants"][rows] = neww
+    agg = eng.resources(safe=False)
+    assert float_close(agg["sum_wants"], snap2["agg_sum_wants"], np.maximum(snap["capacity"], 1.0), 1e-12).all()
+    snap2["agg_sum_wants"] = agg["sum_wants"]
+    eng.apportion(NOW)
+    gets, exp = eng.leases()
+    assert_leases_match(snap2, gets, exp, O.apportion(snap2, NOW), "after update_wants")
