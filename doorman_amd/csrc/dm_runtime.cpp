@@ -683,6 +683,14 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
 // Rows of one upsert/release call: in range and unique (a bitmap over the table,
 // O(n + N/64)); the resource of each row is found on the device.
 static int stage_rows(dm_ctx* c, int64_t n, const int64_t* rows) {
+  // fast path: strictly increasing rows are unique
+  bool sorted = n > 0 && rows[0] >= 0;
+  for (int64_t i = 1; i < n && sorted; ++i) sorted = rows[i] > rows[i - 1];
+  if (sorted) {
+    if (rows[n - 1] >= c->N) return c->fail(DM_E_RANGE, "row out of range");
+    DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
+    return DM_OK;
+  }
   if (c->seen.size() != (size_t)(c->N / 64 + 1)) c->seen.assign((size_t)(c->N / 64 + 1), 0);
   int rc = DM_OK;
   int64_t i = 0;
