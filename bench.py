@@ -172,6 +172,9 @@ def main():
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) on a node; gloo + --same-device rehearses N>1 on one GPU")
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
     ap.add_argument("--hier", action="store_true",
                     help="every step runs the intermediate-server exchange first (SURVEY.md §8e, configs[3]): "
                          "publish totals, RCCL all-gather, root apportionment, take grants, then the leaf tick")
@@ -184,16 +187,21 @@ def main():
     import torch  # loaded first: libdoorman_hip then binds to torch's HIP runtime
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    dev_index = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_index)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 
     from doorman_amd import workloads as W
     from doorman_amd.engine import Engine
 
     snap = make_workload(args.workload, rank)
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
-    eng = Engine(local_rank)
+    eng = Engine(dev_index)
     eng.load(snap)
     now = W.NOW_NS
 
@@ -207,12 +215,16 @@ def main():
         step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup)
     if args.hier:
         from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
-        root = Engine(local_rank)
+        root = Engine(dev_index)
         root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world, lease_length_s=20))
 
         def gather(src, dst):
-            if world > 1:
-                dist.all_gather_into_tensor(dst, src)
+            if world > 1 and not gloo:
+                dist.all_gather_into_tensor(dst, src)  # RCCL over xGMI
+            elif world > 1:  # rehearsal: through host memory
+                parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
+                dist.all_gather(parts, src.cpu())
+                dst.copy_(torch.cat(parts).to(dst.device))
             else:
                 dst.copy_(src)
 
@@ -246,8 +258,9 @@ def main():
     eng.sync()
     ktimes = eng.kernel_times()
     eng.set_profiling(False)
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    n = torch.tensor([N], dtype=torch.float64, device="cuda")
+    red_dev = "cpu" if gloo else "cuda"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    n = torch.tensor([N], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
