@@ -68,8 +68,6 @@ struct Partials {
   int64_t* c_sgt;
   // map pass: sum of (gets - has) over live rows
   double* d_delta;
-  // per large resource: chunks of the map pass that have finished (last one finalises)
-  int32_t* done;
 };
 
 // Per-resource configuration, AoS (one scalar burst per resource).

@@ -829,17 +829,11 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
 }
 
 __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __restrict__ chunks,
-                                                 const LargeSeg* __restrict__ ls, Partials P,
-                                                 int32_t* general_list, int32_t* general_count) {
+                                                 const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
-  const LargeSeg L = ls[ch.lseg];
-  const SegState st = seg_state<256>(p, P, L, lds);
-  if (st.general) {  // heterogeneous FairShare: k_general takes the whole resource
-    if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) general_list[atomicAdd(general_count, 1)] = L.seg;
-    return;
-  }
-  if (st.rs.learning || st.rs.kind < 2) return;
+  const SegState st = seg_state<256>(p, P, ls[ch.lseg], lds);
+  if (st.general || st.rs.learning || st.rs.kind < 2) return;
   const double eq = st.rs.C / (double)st.cl.count;
   ChunkRows rw;
   load_chunk(p, ch, rw);
@@ -956,34 +950,22 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);
-  // The chunk that finishes last writes the resource's results (no extra launch).
-  // Hand-off per MI355X_MICROARCH.md "Valid forms": the partial's store, agent
-  // release, vmcnt(0), relaxed agent atomic; the last arriver acquires before
-  // reading the other chunks' partials.  Every chunk reduces the partials with the
-  // same tree, so the result does not depend on which chunk is last.
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    P.d_delta[blockIdx.x] = delta.v;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int arrived = __hip_atomic_fetch_add(P.done + ch.lseg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = arrived == L.chunk_end - L.chunk_begin - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
+}
+
+__global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P,
+                                                   int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<256> lds;
+  const LargeSeg L = ls[blockIdx.x];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (st.general) {
+    if (threadIdx.x == 0) general_list[atomicAdd(general_count, 1)] = L.seg;
+    return;
   }
-  __syncthreads();
-  if (!last) return;
   SumD d{0.0};
-  for (int q = L.chunk_begin + (int)threadIdx.x; q < L.chunk_end; q += 256) {
-    d.v += __hip_atomic_load(P.d_delta + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 256) d.v += P.d_delta[c];
   d = group_reduce<256>(d, OpSumD(), lds.d);
-  if (threadIdx.x == 0) {
-    write_resource(p, L.seg, rs, st.cl, d.v);
-    P.done[ch.lseg] = 0;  // ready for the next tick (kernel boundary orders it)
-  }
+  if (threadIdx.x == 0) write_resource(p, L.seg, st.rs, st.cl, d.v);
 }
 
 // General FairShare: resources with heterogeneous subclients or NaN wants, from
@@ -1259,9 +1241,10 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
   if (nchunks <= 0) return hipSuccess;
   switch (phase) {
     case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
-    case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, glist, gcount); break;
+    case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -94,7 +94,7 @@ struct dm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   // auxiliary streams: independent size bins of one tick run concurrently
-  static constexpr int kAux = 4;
+  static constexpr int kAux = 3;
   hipStream_t aux[kAux] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kAux] = {};
   std::string err;
@@ -129,7 +129,7 @@ struct dm_ctx {
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
-  DBuf<int32_t> pa_nan, pl_done;
+  DBuf<int32_t> pa_nan;
   // worklist of resources for k_general (heterogeneous-subclient FairShare)
   DBuf<int32_t> glist, gcount;
   bool maybe_general = false;
@@ -183,7 +183,7 @@ struct dm_ctx {
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pl_done.release();
+    pa_nan.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
   }
@@ -286,9 +286,6 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pc_ee.ensure(nc), "partials");
   DM_HIP(c, c->pd_delta.ensure(nc), "partials");
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
-  const size_t nl = std::max<size_t>(c->h_large.size(), 1);
-  DM_HIP(c, c->pl_done.ensure(nl), "partials");
-  DM_HIP(c, hipMemsetAsync(c->pl_done.p, 0, nl * sizeof(int32_t), st), "partials");
   c->n_nonsmall = 0;
   for (int64_t r = 0; r < c->R; ++r)
     if (c->h_seg_off[r + 1] - c->h_seg_off[r] > kSmallMax) ++c->n_nonsmall;
@@ -543,7 +540,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
 
   Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
-             c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p, c->pl_done.p};
+             c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p};
   hipStream_t st = c->stream;
   auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t {
     if (!c->profiling) return fn();
@@ -558,31 +555,28 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
   if (c->maybe_general) DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
-  // Independent work classes, each on its own auxiliary stream when more than one
-  // is present: large resources (a 4-kernel chain) | 1024x4, 512x4 | 256x{4,2,1} |
-  // wave64 + the packed small resources.  Forked from and joined to the main stream.
-  auto cls_of_bin = [](int b) { return b >= 4 ? 1 : (b >= 1 ? 2 : 3); };
-  bool used[dm_ctx::kAux] = {nch > 0, false, false, !c->h_packs.empty()};
-  for (int b = 0; b < kNumBins; ++b)
-    if (!c->h_bins[b].empty()) used[cls_of_bin(b)] = true;
-  int classes = 0;
-  for (int i = 0; i < dm_ctx::kAux; ++i) classes += used[i];
+  // Independent work classes: large resources (a 5-kernel chain), big groups,
+  // small groups + packed.  With more than one class present they run on the
+  // auxiliary streams concurrently, forked from and joined back to the main stream.
+  int big_bins = 0, small_bins = 0;
+  for (int b = 3; b < kNumBins; ++b) big_bins += !c->h_bins[b].empty();
+  for (int b = 0; b < 3; ++b) small_bins += !c->h_bins[b].empty();
+  const bool has_small = small_bins > 0 || !c->h_packs.empty();
+  const int classes = (nch > 0) + (big_bins > 0) + has_small;
   const bool fork = classes > 1;
-  auto stream_of = [&](int cls) { return fork ? c->aux[cls] : st; };
-  hipStream_t s_large = stream_of(0), s_small = stream_of(3);
+  hipStream_t s_large = fork ? c->aux[0] : st, s_big = fork ? c->aux[1] : st, s_small = fork ? c->aux[2] : st;
   if (fork) {
     DM_HIP(c, hipEventRecord(c->ev_fork, st), "fork");
-    for (int i = 0; i < dm_ctx::kAux; ++i)
-      if (used[i]) DM_HIP(c, hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork");
+    for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork");
   }
-  for (int ph = 0; ph < 4 && nch > 0; ++ph)
+  for (int ph = 0; ph < 5 && nch > 0; ++ph)
     DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
                     [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
            "large-resource kernels");
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    hipStream_t s = stream_of(cls_of_bin(b));
+    hipStream_t s = b >= 3 ? s_big : s_small;
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }), "group kernel");
   }
   if (!c->h_packs.empty())
@@ -590,7 +584,6 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
            "small kernel");
   if (fork) {
     for (int i = 0; i < dm_ctx::kAux; ++i) {
-      if (!used[i]) continue;
       DM_HIP(c, hipEventRecord(c->ev_join[i], c->aux[i]), "join");
       DM_HIP(c, hipStreamWaitEvent(st, c->ev_join[i], 0), "join");
     }
