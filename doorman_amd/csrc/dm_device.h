@@ -9,14 +9,14 @@ constexpr int64_t kNs = 1000000000LL;
 
 // Dispatch bins.  A segment of n rows goes to:
 //   n <= kSmallMax            : wave-packed literal path (many resources per wave)
-//   n <= 64                   : one wave per resource (64x1)
-//   n <= 1024                 : one 256-thread workgroup, R = 1, 2, 4 rows per thread in VGPRs
+//   n <= 64 / 128 / 256       : one wave per resource, R = 1, 2, 4 rows per lane (4 resources per workgroup)
+//   n <= 512 / 1024           : one 256-thread workgroup, R = 2, 4 rows per thread in VGPRs
 //   n <= 2048 / 4096          : one 512- / 1024-thread workgroup, 4 rows per thread
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
 constexpr int kSmallMax = 16;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
-constexpr int kNumBins = 6;  // 64x1, 256x1, 256x2, 256x4, 512x4, 1024x4
+constexpr int kNumBins = 7;  // wave64x{1,2,4}, block256x{2,4}, block512x4, block1024x4
 
 struct Pack {  // a run of consecutive small resources covering <= 64 rows
   int32_t first_seg;
@@ -24,6 +24,7 @@ struct Pack {  // a run of consecutive small resources covering <= 64 rows
   int64_t row0;
   int32_t nrows;  // <= 64
   int32_t maxlen;  // longest resource in the pack
+  uint8_t rel[64];  // rel[k] = seg_off[first_seg + k] - row0, k <= nseg (inline: no dependent load)
 };
 
 struct WorkItem {  // one resource of a size bin: no dependent load before its rows

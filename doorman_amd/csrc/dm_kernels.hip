@@ -509,13 +509,15 @@ __global__ __launch_bounds__(G) void k_block(DevParams p, const WorkItem* __rest
   group_segment<G, R>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
 }
 
-// One wave per resource (n <= 64), four independent waves per workgroup.
+// One wave per resource (n <= 64 R), four independent waves per workgroup: wave
+// reductions only (DPP, no barriers), four resources in flight per workgroup.
+template <int R>
 __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                               int32_t* general_list, int32_t* general_count) {
   Lds<64> lds;  // unused by wave reductions
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nitems) return;
-  group_segment<64, 1>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
+  group_segment<64, R>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -528,8 +530,14 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wv >= npacks) return;
   const int lane = threadIdx.x & 63;
-  const Pack pk = packs[wv];
-  const int64_t offk = lane <= pk.nseg ? p.seg_off[pk.first_seg + lane] : INT64_MAX;
+  const Pack& pkr = packs[wv];
+  Pack pk;
+  pk.first_seg = pkr.first_seg;
+  pk.nseg = pkr.nseg;
+  pk.row0 = pkr.row0;
+  pk.nrows = pkr.nrows;
+  pk.maxlen = pkr.maxlen;
+  const int64_t offk = lane <= pk.nseg ? pk.row0 + pkr.rel[lane] : INT64_MAX;
   const int64_t row = pk.row0 + lane;
   const bool valid = lane < pk.nrows;
   // resource of this row: last k < nseg with seg_off[first+k] <= row
@@ -1225,12 +1233,13 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
                       hipStream_t st) {
   if (n <= 0) return hipSuccess;
   switch (bin) {
-    case 0: k_wave<<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 1: k_block<256, 1><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 2: k_block<256, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 3: k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 4: k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 5: k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 0: k_wave<1><<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 1: k_wave<2><<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 2: k_wave<4><<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 3: k_block<256, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 4: k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 5: k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 6: k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

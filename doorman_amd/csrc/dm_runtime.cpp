@@ -57,9 +57,10 @@ enum KClass {
   KC_RELEASE,
   KC_COUNT
 };
-const char* kClassNames[KC_COUNT] = {"small_packed", "wave64x1",   "block256x1", "block256x2",  "block256x4",
-                                     "block512x4",   "block1024x4", "large_a",    "large_b",     "large_c",
-                                     "large_map",    "large_fin",  "general",    "store_upsert", "store_release"};
+const char* kClassNames[KC_COUNT] = {"small_packed", "wave64x1",   "wave64x2",   "wave64x4",   "block256x2",
+                                     "block256x4",   "block512x4", "block1024x4", "large_a",   "large_b",
+                                     "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
+                                     "store_release"};
 
 template <typename T>
 struct DBuf {
@@ -216,11 +217,12 @@ static hipError_t upload(DBuf<T>& b, const T* src, size_t n, hipStream_t st) {
 // ---------------------------------------------------------------------------
 static int bin_of(int64_t n) {
   if (n <= 64) return 0;
-  if (n <= 256) return 1;
-  if (n <= 512) return 2;
-  if (n <= 1024) return 3;
-  if (n <= 2048) return 4;
-  return 5;
+  if (n <= 128) return 1;
+  if (n <= 256) return 2;
+  if (n <= 512) return 3;
+  if (n <= 1024) return 4;
+  if (n <= 2048) return 5;
+  return 6;
 }
 
 static void build_plan(dm_ctx* c) {
@@ -240,10 +242,14 @@ static void build_plan(dm_ctx* c) {
     if (n <= kSmallMax) {
       if (open && (cur.nrows + n > 64 || cur.nseg >= 63)) close();
       if (!open) {
-        cur = Pack{(int32_t)r, 0, off[r], 0, 0};
+        cur = Pack{};
+        cur.first_seg = (int32_t)r;
+        cur.row0 = off[r];
         open = true;
       }
+      cur.rel[cur.nseg] = (uint8_t)(off[r] - cur.row0);
       cur.nseg += 1;
+      cur.rel[cur.nseg] = (uint8_t)(off[r] + n - cur.row0);
       cur.nrows += (int32_t)n;
       cur.maxlen = std::max<int32_t>(cur.maxlen, (int32_t)n);
       continue;
@@ -559,8 +565,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // small groups + packed.  With more than one class present they run on the
   // auxiliary streams concurrently, forked from and joined back to the main stream.
   int big_bins = 0, small_bins = 0;
-  for (int b = 3; b < kNumBins; ++b) big_bins += !c->h_bins[b].empty();
-  for (int b = 0; b < 3; ++b) small_bins += !c->h_bins[b].empty();
+  for (int b = 4; b < kNumBins; ++b) big_bins += !c->h_bins[b].empty();
+  for (int b = 0; b < 4; ++b) small_bins += !c->h_bins[b].empty();
   const bool has_small = small_bins > 0 || !c->h_packs.empty();
   const int classes = (nch > 0) + (big_bins > 0) + has_small;
   const bool fork = classes > 1;
@@ -576,7 +582,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    hipStream_t s = b >= 3 ? s_big : s_small;
+    hipStream_t s = b >= 4 ? s_big : s_small;
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }), "group kernel");
   }
   if (!c->h_packs.empty())
