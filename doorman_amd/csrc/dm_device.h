@@ -69,6 +69,9 @@ struct Partials {
   int64_t* c_sgt;
   // map pass: sum of (gets - has) over live rows
   double* d_delta;
+  // pass A: live-row mask, one byte per thread of each chunk (bit k = row k*256+tid),
+  // so passes B and C read wants (+ subclients for ProportionalShare) and not expiry
+  uint8_t* live;
 };
 
 // Per-resource configuration, AoS (one scalar burst per resource).

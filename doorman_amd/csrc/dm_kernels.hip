@@ -791,6 +791,31 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   }
 }
 
+// Passes B, C and the map: wants (plus has / subclients where the pass uses them)
+// of the chunk's rows and the live mask pass A left instead of re-reading expiry.
+__device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials& P, const Chunk& ch,
+                                             ChunkRows& r, bool with_sub, bool with_has = false) {
+  const double* __restrict__ wb = p.wants + ch.row0;
+  const double* __restrict__ hb = p.has + ch.row0;
+  const int64_t* __restrict__ sb = p.sub + ch.row0;
+  r.valid = 0;
+  r.live = P.live[(size_t)blockIdx.x * 256 + threadIdx.x];
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    const int i = k * 256 + threadIdx.x;
+    r.w[k] = 0.0;
+    r.h[k] = 0.0;
+    r.s[k] = 0;
+    if (i < ch.nrows) {
+      const unsigned u = (unsigned)i;
+      r.w[k] = wb[u];
+      if (with_has) r.h[k] = hb[u];
+      if (with_sub) r.s[k] = (int)sb[u];
+      r.valid |= 1u << k;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
@@ -817,6 +842,7 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
       a.nan |= __builtin_isnan(rw.w[k]) ? 1 : 0;
     }
   }
+  P.live[(size_t)blockIdx.x * 256 + threadIdx.x] = (uint8_t)rw.live;
   {
     const AggR all_part = a.all;
     a = group_reduce<256>(a, OpA(), lds.a);
@@ -840,11 +866,21 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
                                                  const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
+  bool ps;
+  {  // only ProportionalShare / FairShare outside learning mode need this pass
+    const ResCfg cf = p.cfg[ch.seg];
+    if (cf.learning_end_ns > p.now || cf.kind < 2) return;
+    ps = cf.kind == 2;
+  }
+  ChunkRows rw;
+  load_chunk_w(p, P, ch, rw, ps);  // rows in flight while the resource's partials are reduced
   const SegState st = seg_state<256>(p, P, ls[ch.lseg], lds);
   if (st.general || st.rs.learning || st.rs.kind < 2) return;
   const double eq = st.rs.C / (double)st.cl.count;
-  ChunkRows rw;
-  load_chunk(p, ch, rw);
+  if (!ps) {  // FairShare reaches here only with uniform subclients
+#pragma unroll
+    for (int k = 0; k < kLR; ++k) rw.s[k] = st.a.smin;
+  }
   AggB b{0.0, 0.0, 0};
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
@@ -877,15 +913,21 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
                                                  const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
+  {  // only FairShare outside learning mode has a round 2
+    const ResCfg cf = p.cfg[ch.seg];
+    if (cf.learning_end_ns > p.now || cf.kind != 3) return;
+  }
+  ChunkRows rw;
+  load_chunk_w(p, P, ch, rw, false);  // rows in flight while the resource's partials are reduced
   const LargeSeg L = ls[ch.lseg];
   const SegState st = seg_state<256>(p, P, L, lds);
   if (st.general || st.rs.learning || st.rs.kind != 3) return;
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) rw.s[k] = st.a.smin;  // uniform subclients here
   const AggB b = seg_b<256>(P, L, lds);
   const double eq = st.rs.C / (double)st.cl.count;
   const double s0 = (double)st.a.smin;
   const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
-  ChunkRows rw;
-  load_chunk(p, ch, rw);
   AggC c{0.0, 0};
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
@@ -909,6 +951,13 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
                                                    const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
+  bool ps;
+  {
+    const ResCfg cf = p.cfg[ch.seg];
+    ps = !(cf.learning_end_ns > p.now) && cf.kind == 2;
+  }
+  ChunkRows rw;
+  load_chunk_w(p, P, ch, rw, ps, true);  // rows in flight while the resource's partials are reduced
   const LargeSeg L = ls[ch.lseg];
   const SegState st = seg_state<256>(p, P, L, lds);
   if (st.general) return;
@@ -920,8 +969,6 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   if (!rs.learning && rs.kind >= 2) b = seg_b<256>(P, L, lds);
   if (!rs.learning && rs.kind == 3) c = seg_c<256>(P, L, lds);
   const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
-  ChunkRows rw;
-  load_chunk(p, ch, rw);
   double* gb = p.out_gets + ch.row0;
   int64_t* xb = p.out_expiry + ch.row0;
   SumD delta{0.0};
