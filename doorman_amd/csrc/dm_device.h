@@ -72,7 +72,12 @@ struct Partials {
   // pass A: live-row mask, one byte per thread of each chunk (bit k = row k*256+tid),
   // so passes B and C read wants (+ subclients for ProportionalShare) and not expiry
   uint8_t* live;
+  // per large resource (kSegTotBytes each): pass A totals left by pass B's first
+  // chunk, pass B totals left by pass C's first chunk, so the map reduces at most
+  // one set of partials
+  uint8_t* tot;
 };
+constexpr int kSegTotBytes = 128;
 
 // Per-resource configuration, AoS (one scalar burst per resource).
 struct ResCfg {

@@ -714,6 +714,24 @@ struct SegState {
   int general;  // FairShare with heterogeneous subclients / NaN wants -> k_general
 };
 
+__device__ __forceinline__ SegState seg_state_of(const DevParams& p, const LargeSeg& L, const AggA& a) {
+  SegState st;
+  st.a = a;
+  st.rs = load_res(p, L.seg);
+  st.cl = clean_from(p, st.rs, a);
+  st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin >= a.smax && !a.nan)) ? 1 : 0;
+  return st;
+}
+
+struct SegTot {
+  AggA a;
+  AggB b;
+};
+static_assert(sizeof(SegTot) <= kSegTotBytes, "SegTot slot");
+__device__ __forceinline__ SegTot* seg_tot(const Partials& P, int lseg) {
+  return reinterpret_cast<SegTot*>(P.tot + (size_t)lseg * kSegTotBytes);
+}
+
 template <int G>
 __device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials& P, const LargeSeg& L,
                                               Lds<G>& lds) {
@@ -737,12 +755,7 @@ __device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials
     a = group_reduce<G>(a, OpA(), lds.a);
     if (p.recompute) a.all = group_reduce<G>(all_part, OpR(), lds.r);
   }
-  SegState st;
-  st.a = a;
-  st.rs = load_res(p, L.seg);
-  st.cl = clean_from(p, st.rs, a);
-  st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin >= a.smax && !a.nan)) ? 1 : 0;
-  return st;
+  return seg_state_of(p, L, a);
 }
 
 template <int G>
@@ -874,7 +887,9 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
   }
   ChunkRows rw;
   load_chunk_w(p, P, ch, rw, ps);  // rows in flight while the resource's partials are reduced
-  const SegState st = seg_state<256>(p, P, ls[ch.lseg], lds);
+  const LargeSeg L = ls[ch.lseg];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->a = st.a;
   if (st.general || st.rs.learning || st.rs.kind < 2) return;
   const double eq = st.rs.C / (double)st.cl.count;
   if (!ps) {  // FairShare reaches here only with uniform subclients
@@ -920,11 +935,12 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
   ChunkRows rw;
   load_chunk_w(p, P, ch, rw, false);  // rows in flight while the resource's partials are reduced
   const LargeSeg L = ls[ch.lseg];
-  const SegState st = seg_state<256>(p, P, L, lds);
+  const SegState st = seg_state_of(p, L, seg_tot(P, ch.lseg)->a);  // left by pass B
   if (st.general || st.rs.learning || st.rs.kind != 3) return;
 #pragma unroll
   for (int k = 0; k < kLR; ++k) rw.s[k] = st.a.smin;  // uniform subclients here
   const AggB b = seg_b<256>(P, L, lds);
+  if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->b = b;
   const double eq = st.rs.C / (double)st.cl.count;
   const double s0 = (double)st.a.smin;
   const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
@@ -951,23 +967,29 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
                                                    const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
-  bool ps;
+  bool ps, fs;
   {
     const ResCfg cf = p.cfg[ch.seg];
-    ps = !(cf.learning_end_ns > p.now) && cf.kind == 2;
+    const bool lrn = cf.learning_end_ns > p.now;
+    ps = !lrn && cf.kind == 2;
+    fs = !lrn && cf.kind == 3;
   }
   ChunkRows rw;
   load_chunk_w(p, P, ch, rw, ps, true);  // rows in flight while the resource's partials are reduced
   const LargeSeg L = ls[ch.lseg];
-  const SegState st = seg_state<256>(p, P, L, lds);
+  // pass A totals: left by pass B for ProportionalShare / FairShare
+  const SegState st = (ps || fs) ? seg_state_of(p, L, seg_tot(P, ch.lseg)->a) : seg_state<256>(p, P, L, lds);
   if (st.general) return;
   const Res& rs = st.rs;
   const double C = rs.C;
   const double eq = C / (double)st.cl.count;
   AggB b{0.0, 0.0, 0};
   AggC c{0.0, 0};
-  if (!rs.learning && rs.kind >= 2) b = seg_b<256>(P, L, lds);
-  if (!rs.learning && rs.kind == 3) c = seg_c<256>(P, L, lds);
+  if (ps) b = seg_b<256>(P, L, lds);
+  if (fs) {
+    b = seg_tot(P, ch.lseg)->b;  // left by pass C
+    c = seg_c<256>(P, L, lds);
+  }
   const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
   double* gb = p.out_gets + ch.row0;
   int64_t* xb = p.out_expiry + ch.row0;

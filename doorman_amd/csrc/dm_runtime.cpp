@@ -131,7 +131,7 @@ struct dm_ctx {
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
   DBuf<int32_t> pa_nan;
-  DBuf<uint8_t> pa_live;
+  DBuf<uint8_t> pa_live, p_tot;
   // worklist of resources for k_general (heterogeneous-subclient FairShare)
   DBuf<int32_t> glist, gcount;
   bool maybe_general = false;
@@ -185,7 +185,7 @@ struct dm_ctx {
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pa_live.release();
+    pa_nan.release(); pa_live.release(); p_tot.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
   }
@@ -294,6 +294,7 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pd_delta.ensure(nc), "partials");
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
   DM_HIP(c, c->pa_live.ensure(nc * 256), "partials");
+  DM_HIP(c, c->p_tot.ensure(std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes), "partials");
   c->n_nonsmall = 0;
   for (int64_t r = 0; r < c->R; ++r)
     if (c->h_seg_off[r + 1] - c->h_seg_off[r] > kSmallMax) ++c->n_nonsmall;
@@ -549,7 +550,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p,
-             c->pa_live.p};
+             c->pa_live.p, c->p_tot.p};
   hipStream_t st = c->stream;
   auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t {
     if (!c->profiling) return fn();

@@ -38,7 +38,7 @@ def main():
         for _ in range(3):
             e.apportion(W.NOW_NS, writeback=True)
         engines.append(e)
-    res = {p: {"tick_us": [], "kern_us": []} for p in args.libs}
+    res = {p: {"tick_us": [], "kern_us": [], "plain_us": []} for p in args.libs}
     for _ in range(args.rounds):
         for p, e in zip(args.libs, engines):
             e.set_profiling(True)
@@ -52,13 +52,20 @@ def main():
             kt = e.kernel_times()
             e.set_profiling(False)
             res[p]["tick_us"].append(dt / args.steps * 1e6)
+            torch.cuda.synchronize()  # the same ticks without per-kernel events
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                e.apportion(W.NOW_NS, writeback=True, asynchronous=True)
+            e.sync()
+            res[p]["plain_us"].append((time.perf_counter() - t0) / args.steps * 1e6)
             res[p]["kern_us"].append(sum(v[1] for v in kt.values()) / args.steps * 1e3)
     alg = algorithmic_bytes(N, R)
     for p in args.libs:
         k = res[p]["kern_us"]
         t = res[p]["tick_us"]
         print(f"{os.path.basename(p):34s} kernel med {statistics.median(k):8.2f} us min {min(k):8.2f} "
-              f"({alg / min(k) / 1e3:7.1f} GB/s best) | tick med {statistics.median(t):8.2f} us")
+              f"({alg / min(k) / 1e3:7.1f} GB/s best) | tick med {statistics.median(t):8.2f} us | "
+              f"unprofiled tick med {statistics.median(res[p]['plain_us']):8.2f} min {min(res[p]['plain_us']):8.2f} us")
     for e in engines:
         e.close()
 

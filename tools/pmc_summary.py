@@ -66,6 +66,8 @@ def main(d, w):
                 c = cls(row["Name"])
                 if c:
                     stats[c] = {"calls": int(row["Calls"]), "avg_us": float(row["AverageNs"]) / 1e3}
+    if not rows:
+        sys.exit(f"no kernel stats under {d}/trace: not overwriting profiles/")
     fetch = counters(os.path.join(d, "fetch"))
     write = counters(os.path.join(d, "write"))
     cf = counters(os.path.join(d, "cal_fetch"))
