@@ -129,6 +129,14 @@ def streaming_step(eng, snap, rank, n_ticks):
     return step
 
 
+def subset_rows(snap, max_rows):
+    """the leading resources of a snapshot holding at most max_rows leases"""
+    from doorman_amd import workloads as W
+    so = snap["seg_off"]
+    k = int(np.searchsorted(so, max_rows, side="right")) - 1
+    return W.subset(snap, np.arange(max(k, 1)))
+
+
 def cpu_baseline(snap, now_ns, budget_s=12.0):
     """Reference algorithm restated in C (oracle, literal per-request Resource.Decide on a
     private copy of the store, single thread), timed on a bounded sample of this workload."""
@@ -153,6 +161,16 @@ def cpu_baseline(snap, now_ns, budget_s=12.0):
         if t_total > budget_s:
             break
     del order
+    # the closed form (same outputs) over all resources on the
+    # host's cores, the optimised-CPU comparator, timed on the whole snapshot
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    O.apportion(subset_rows(snap, 2000), now_ns, "closed", threads=threads)  # warm the pool
+    reps, t_mt = 0, 0.0
+    while reps < 3 and t_mt < 5.0:
+        t0 = time.perf_counter()
+        O.apportion(snap, now_ns, "closed", threads=threads)
+        t_mt += time.perf_counter() - t0
+        reps += 1
     return {
         "value": done_rows / t_total if t_total > 0 else None,
         "unit": "leases/s",
@@ -161,6 +179,12 @@ def cpu_baseline(snap, now_ns, budget_s=12.0):
         "sample": f"{done_rows} leases of {len(used)} resources of the same workload, each decided by the literal "
                   f"C restatement of Resource.Decide (go/server/doorman/resource.go:100-113) on a private store copy "
                   f"(O(n) per request as in the reference), single thread, {t_total:.1f} s",
+        "closed_form_mt": {
+            "value": reps * len(snap["wants"]) / t_mt,
+            "unit": "leases/s",
+            "cores": threads,
+            "sample": f"whole snapshot x{reps}: oracle/ closed form (SURVEY.md §8a), OpenMP over resources",
+        },
     }
 
 

@@ -394,12 +394,13 @@ typedef struct {
   int64_t sgt;
 } t_entry;
 
-int or_apportion_closed(const or_snapshot* sn, int64_t now_ns, or_outputs* out) {
-  for (int64_t r = 0; r < sn->n_resources; ++r)
-    if (sn->cfg[r].kind < OR_NO_ALGORITHM || sn->cfg[r].kind > OR_FAIR_SHARE) return -2;
-  t_entry* cache = NULL;
-  int64_t cache_cap = 0;
-  for (int64_t r = 0; r < sn->n_resources; ++r) {
+/* One resource of the closed form; *cache / *cache_cap: the caller's scratch for
+ * distinct round-2 thresholds (one per thread in the threaded variant). */
+static void closed_resource(const or_snapshot* sn, int64_t r, int64_t now_ns, or_outputs* out, t_entry** cache_p,
+                            int64_t* cache_cap_p) {
+  t_entry* cache = *cache_p;
+  int64_t cache_cap = *cache_cap_p;
+  {
     const or_resource_cfg* cfg = &sn->cfg[r];
     int64_t lo = sn->seg_off[r], hi = sn->seg_off[r + 1];
     /* store sums: Assign per row in order, parity override, Clean in order */
@@ -521,6 +522,37 @@ int or_apportion_closed(const or_snapshot* sn, int64_t now_ns, or_outputs* out) 
     }
     finish_resource(sn, r, count, sum_has, sum_wants, out->gets, out->expiry_ns, out);
   }
+  *cache_p = cache;
+  *cache_cap_p = cache_cap;
+}
+
+static int check_kinds(const or_snapshot* sn) {
+  for (int64_t r = 0; r < sn->n_resources; ++r)
+    if (sn->cfg[r].kind < OR_NO_ALGORITHM || sn->cfg[r].kind > OR_FAIR_SHARE) return -2;
+  return 0;
+}
+
+int or_apportion_closed(const or_snapshot* sn, int64_t now_ns, or_outputs* out) {
+  if (check_kinds(sn)) return -2;
+  t_entry* cache = NULL;
+  int64_t cache_cap = 0;
+  for (int64_t r = 0; r < sn->n_resources; ++r) closed_resource(sn, r, now_ns, out, &cache, &cache_cap);
   free(cache);
+  return 0;
+}
+
+/* The closed form over resources in parallel (OpenMP, `threads` threads): the
+ * optimised-CPU comparator of SURVEY.md §8(d)(iii).  Resources are independent,
+ * so the outputs are identical to or_apportion_closed. */
+int or_apportion_closed_mt(const or_snapshot* sn, int64_t now_ns, or_outputs* out, int threads) {
+  if (check_kinds(sn)) return -2;
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+  {
+    t_entry* cache = NULL;
+    int64_t cache_cap = 0;
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = 0; r < sn->n_resources; ++r) closed_resource(sn, r, now_ns, out, &cache, &cache_cap);
+    free(cache);
+  }
   return 0;
 }

@@ -135,6 +135,8 @@ typedef struct {
 
 int or_apportion_literal(const or_snapshot* snap, int64_t now_ns, or_outputs* out);
 int or_apportion_closed(const or_snapshot* snap, int64_t now_ns, or_outputs* out);
+/* Same outputs, resources spread over `threads` OpenMP threads. */
+int or_apportion_closed_mt(const or_snapshot* snap, int64_t now_ns, or_outputs* out, int threads);
 
 /* literal evaluation restricted to rows [row_lo,row_hi) of one resource
  * (bounded CPU-baseline samples); returns number of rows evaluated */

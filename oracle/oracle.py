@@ -128,6 +128,8 @@ def lib():
         L.or_apportion_literal.argtypes = [ctypes.POINTER(_Snapshot), i64, ctypes.POINTER(_Outputs)]
         L.or_apportion_closed.restype = ctypes.c_int
         L.or_apportion_closed.argtypes = [ctypes.POINTER(_Snapshot), i64, ctypes.POINTER(_Outputs)]
+        L.or_apportion_closed_mt.restype = ctypes.c_int
+        L.or_apportion_closed_mt.argtypes = [ctypes.POINTER(_Snapshot), i64, ctypes.POINTER(_Outputs), i32]
         L.or_apportion_literal_rows.restype = i64
         L.or_apportion_literal_rows.argtypes = [ctypes.POINTER(_Snapshot), i64, i64, i64, i64, vp]
         _lib = L
@@ -271,9 +273,10 @@ def _mk_snapshot(snap, keep):
     return s
 
 
-def apportion(snap: dict, now_ns: int, mode: str = "closed") -> dict:
+def apportion(snap: dict, now_ns: int, mode: str = "closed", threads: int = 1) -> dict:
     """Evaluate every row of a snapshot (dict of numpy columns, see
-    doorman_amd.workloads) against the frozen store.  mode: 'closed' | 'literal'."""
+    doorman_amd.workloads) against the frozen store.  mode: 'closed' | 'literal';
+    threads > 1 runs the closed form over resources on that many OpenMP threads."""
     keep = []
     s = _mk_snapshot(snap, keep)
     R, N = s.n_resources, s.n_leases
@@ -287,8 +290,11 @@ def apportion(snap: dict, now_ns: int, mode: str = "closed") -> dict:
     }
     o = _Outputs(*[out[k].ctypes.data for k in
                    ("gets", "expiry_ns", "res_count", "res_sum_has", "res_sum_wants", "res_safe_capacity")])
-    fn = lib().or_apportion_closed if mode == "closed" else lib().or_apportion_literal
-    rc = fn(ctypes.byref(s), now_ns, ctypes.byref(o))
+    if mode == "closed" and threads > 1:
+        rc = lib().or_apportion_closed_mt(ctypes.byref(s), now_ns, ctypes.byref(o), threads)
+    else:
+        fn = lib().or_apportion_closed if mode == "closed" else lib().or_apportion_literal
+        rc = fn(ctypes.byref(s), now_ns, ctypes.byref(o))
     if rc != 0:
         raise ValueError("unknown algorithm kind in snapshot")
     return out

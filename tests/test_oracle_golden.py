@@ -139,6 +139,16 @@ def test_closed_form_equals_literal(seed):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
+def test_threaded_closed_form_matches():
+    """The OpenMP comparator (bench.py cpu_baseline 'closed_mt') gives the same bits."""
+    rng = np.random.default_rng(7)
+    snap = W.random_snapshot(rng, 300, 40, hetero=True, edge=True)
+    a = O.apportion(snap, NOW, "closed")
+    b = O.apportion(snap, NOW, "closed", threads=4)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
 def test_unknown_kind_is_an_error():
     snap = W.make_snapshot([2], [1, 2], [0, 0], 1, NOW + W.NS, 7, 10.0)
     with pytest.raises(ValueError):
