@@ -115,8 +115,16 @@ def streaming_step(eng, snap, rank, n_ticks):
         alive[new] = True
         now += 5 * W.NS
         k = len(new)
-        batches.append((upd, rng.uniform(0.5, 1.5, len(upd)), gone, new, np.zeros(k), rng.uniform(0.5, 1.5, k),
-                        np.ones(k, np.int64), np.full(k, now + 3600 * W.NS, np.int64), now))
+        cols = (upd, rng.uniform(0.5, 1.5, len(upd)), gone, new, np.zeros(k), rng.uniform(0.5, 1.5, k),
+                np.ones(k, np.int64), np.full(k, now + 3600 * W.NS, np.int64))
+        # the RPC layer would decode requests straight into page-locked buffers
+        # (dm_host_alloc), which then cross PCIe by DMA
+        pinned = []
+        for a in cols:
+            h = eng.host_empty(len(a), a.dtype)
+            h[:] = a
+            pinned.append(h)
+        batches.append((*pinned, now))
     it = iter(batches)
 
     def step():

@@ -71,6 +71,8 @@ _SIGS = {
     "dm_config_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ResourceCfg)]),
     "dm_store_upsert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5),
     "dm_store_release": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "dm_host_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "dm_host_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dm_store_update_wants": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "dm_read_store": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 4),
     "dm_apportion": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32]),

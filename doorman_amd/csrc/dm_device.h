@@ -79,6 +79,14 @@ struct Partials {
 };
 constexpr int kSegTotBytes = 128;
 
+// store-update validation flags (k_check_rows)
+constexpr uint32_t kUpdRange = 1u;   // row outside [0, N)
+constexpr uint32_t kUpdDup = 2u;     // row twice in one call
+constexpr uint32_t kUpdSub = 4u;     // subclients outside [0, 2^31)
+constexpr uint32_t kUpdNaN = 8u;     // NaN wants (FairShare then needs k_general)
+constexpr uint32_t kUpdNotOne = 16u; // subclients != 1 (may make a resource heterogeneous)
+constexpr uint32_t kUpdReject = kUpdRange | kUpdDup | kUpdSub;
+
 // Per-resource configuration, AoS (one scalar burst per resource).
 struct ResCfg {
   double capacity;          // ResourceTemplate.capacity

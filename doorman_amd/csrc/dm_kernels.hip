@@ -1190,12 +1190,53 @@ __device__ __forceinline__ int seg_of_row(const int64_t* __restrict__ seg_off, i
   return (int)lo;
 }
 
+// Validation of one store-update call on the device (no O(n) host pass): rows in
+// range and unique within the call (a row bitmap, all-zero between calls), and
+// the value flags the planner needs.  The apply kernels run only if no error bit
+// is set, so a rejected call leaves the store untouched.
+__global__ void k_check_rows(int64_t n, const int64_t* __restrict__ rows, int64_t N, uint32_t* bitmap,
+                             const double* __restrict__ wants, const int64_t* __restrict__ sub, uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t f = 0;
+  if (i < n) {
+    const int64_t r = rows[i];
+    if (r < 0 || r >= N) {
+      f |= kUpdRange;
+    } else {
+      const uint32_t bit = 1u << (r & 31);
+      if (atomicOr(&bitmap[r >> 5], bit) & bit) f |= kUpdDup;
+    }
+    if (wants && __builtin_isnan(wants[i])) f |= kUpdNaN;
+    if (sub) {
+      const int64_t v = sub[i];
+      if (v < 0 || v > 2147483647LL) f |= kUpdSub;
+      if (v != 1) f |= kUpdNotOne;
+    }
+  }
+  // one atomic per wave and flag value
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(f);
+  if (__all(f == lo)) {
+    if ((threadIdx.x & 63) == 0 && lo) atomicOr(flags, lo);
+  } else if (f) {
+    atomicOr(flags, f);
+  }
+}
+
+// Return the bitmap words of this call's rows to zero.
+__global__ void k_clear_rows(int64_t n, const int64_t* __restrict__ rows, int64_t N, uint32_t* bitmap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  if (r >= 0 && r < N) bitmap[r >> 5] = 0u;
+}
+
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
                          const int64_t* __restrict__ expiry, const int64_t* __restrict__ seg_off, int64_t R,
-                         double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
+                         double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg,
+                         const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (*flags & kUpdReject)) return;
   const int64_t r = rows[i];
   const int seg = seg_of_row(seg_off, R, r);
   const double dh = has[i] - s_has[r], dw = wants[i] - s_wants[r];
@@ -1210,9 +1251,10 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
 }
 
 __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int64_t* __restrict__ seg_off, int64_t R,
-                          double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg) {
+                          double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg,
+                         const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (*flags & kUpdReject)) return;
   const int64_t r = rows[i];
   const int seg = seg_of_row(seg_off, R, r);
   atomicAdd(&agg[seg].sum_has, -s_has[r]);
@@ -1227,9 +1269,10 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int
 // Narrow Assign for a refresh that only changes wants (store.go:157):
 // sumWants += new - old.  Rows are unique within one call.
 __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ wants,
-                               const int64_t* __restrict__ seg_off, int64_t R, double* s_wants, ResAgg* agg) {
+                               const int64_t* __restrict__ seg_off, int64_t R, double* s_wants, ResAgg* agg,
+                               const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (*flags & kUpdReject)) return;
   const int64_t r = rows[i];
   const int seg = seg_of_row(seg_off, R, r);
   const double d = wants[i] - s_wants[r];
@@ -1337,24 +1380,39 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
-                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
+                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, seg_off, R, s_has,
-                                                        s_wants, s_sub, s_exp, agg);
+                                                        s_wants, s_sub, s_exp, agg, flags);
   return hipGetLastError();
 }
 
 hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
-                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st) {
+                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
+                          hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, seg_off, R, s_has, s_wants, s_sub, s_exp, agg);
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, seg_off, R, s_has, s_wants, s_sub, s_exp, agg,
+                                                         flags);
   return hipGetLastError();
 }
 
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
-                               double* s_wants, ResAgg* agg, hipStream_t st) {
+                               double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, seg_off, R, s_wants, agg);
+  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, seg_off, R, s_wants, agg, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
+                             const int64_t* sub, uint32_t* flags, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_check_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, N, bitmap, wants, sub, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_clear_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, N, bitmap);
   return hipGetLastError();
 }
 

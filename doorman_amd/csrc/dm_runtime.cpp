@@ -25,12 +25,16 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
                           hipStream_t st);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
-                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
+                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
-                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, hipStream_t st);
+                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
+                          hipStream_t st);
+hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
+                             const int64_t* sub, uint32_t* flags, hipStream_t st);
+hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st);
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
-                               double* s_wants, ResAgg* agg, hipStream_t st);
+                               double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int64_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
@@ -140,7 +144,9 @@ struct dm_ctx {
   // staging for upsert / release
   DBuf<int64_t> st_rows, st_sub, st_exp;
   DBuf<double> st_has, st_wants;
-  std::vector<uint64_t> seen;  // row bitmap for the uniqueness check, all-zero between calls
+  DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
+  DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
+  uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
   bool profiling = false;
   std::vector<ProfEvent> pending;
@@ -188,6 +194,9 @@ struct dm_ctx {
     pa_nan.release(); pa_live.release(); p_tot.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
+    row_bits.release(); upd_flags.release();
+    if (h_flags) (void)hipHostFree(h_flags);
+    h_flags = nullptr;
   }
 };
 
@@ -305,12 +314,19 @@ static int upload_plan(dm_ctx* c) {
 
 // Could some non-small resource need k_general (heterogeneous subclients or NaN
 // wants among its rows)?  Conservative: expiry is ignored.
-static bool scan_maybe_general(const int64_t* off, int64_t R, const int64_t* sub, const double* wants) {
+// Could any FairShare resource need k_general (live subclients not all equal, or NaN
+// wants)?  Released rows (DM_RELEASED) are never live, so they do not count.
+static bool scan_maybe_general(const int64_t* off, int64_t R, const int64_t* sub, const double* wants,
+                               const int64_t* exp) {
   for (int64_t r = 0; r < R; ++r) {
     if (off[r + 1] - off[r] <= kSmallMax) continue;
-    const int64_t s0 = sub[off[r]];
-    for (int64_t i = off[r]; i < off[r + 1]; ++i)
-      if (sub[i] != s0 || std::isnan(wants[i])) return true;
+    int64_t s0 = -1;
+    for (int64_t i = off[r]; i < off[r + 1]; ++i) {
+      if (exp[i] == DM_RELEASED) continue;
+      if (std::isnan(wants[i])) return true;
+      if (s0 < 0) s0 = sub[i];
+      if (sub[i] != s0) return true;
+    }
   }
   return false;
 }
@@ -470,9 +486,11 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   build_plan(c);
   int rc = upload_plan(c);
   if (rc) return rc;
-  c->maybe_general = scan_maybe_general(s->seg_off, R, s->subclients, s->wants);
+  c->maybe_general = scan_maybe_general(s->seg_off, R, s->subclients, s->wants, s->expiry_ns);
+  // released rows never take part in a tick, so they do not count against this
   c->all_sub_one = true;
-  for (int64_t i = 0; i < N && c->all_sub_one; ++i) c->all_sub_one = s->subclients[i] == 1;
+  for (int64_t i = 0; i < N && c->all_sub_one; ++i)
+    c->all_sub_one = s->subclients[i] == 1 || s->expiry_ns[i] == DM_RELEASED;
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
   c->have_result = false;
@@ -692,35 +710,38 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
 
 // Rows of one upsert/release call: in range and unique (a bitmap over the table,
 // O(n + N/64)); the resource of each row is found on the device.
-static int stage_rows(dm_ctx* c, int64_t n, const int64_t* rows) {
-  // fast path: strictly increasing rows are unique
-  bool sorted = n > 0 && rows[0] >= 0;
-  for (int64_t i = 1; i < n && sorted; ++i) sorted = rows[i] > rows[i - 1];
-  if (sorted) {
-    if (rows[n - 1] >= c->N) return c->fail(DM_E_RANGE, "row out of range");
-    DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
-    return DM_OK;
+// Stage one update call's rows and validate them on the device (k_check_rows):
+// no O(n) host pass, so host buffers go to the GPU by DMA only (pinned buffers from
+// dm_host_alloc at full PCIe rate).  Returns the flags via finish_update().
+static int begin_update(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants_dev,
+                        const int64_t* sub_dev) {
+  if (!c->row_bits.p || c->row_bits.n < (size_t)(c->N / 32 + 1)) {
+    DM_HIP(c, c->row_bits.ensure((size_t)(c->N / 32 + 1)), "row bitmap");
+    DM_HIP(c, hipMemsetAsync(c->row_bits.p, 0, c->row_bits.n * sizeof(uint32_t), c->stream), "row bitmap");
   }
-  if (c->seen.size() != (size_t)(c->N / 64 + 1)) c->seen.assign((size_t)(c->N / 64 + 1), 0);
-  int rc = DM_OK;
-  int64_t i = 0;
-  for (; i < n; ++i) {
-    const int64_t r = rows[i];
-    if (r < 0 || r >= c->N) {
-      rc = c->fail(DM_E_RANGE, "row out of range");
-      break;
-    }
-    uint64_t& w = c->seen[(size_t)(r >> 6)];
-    const uint64_t bit = 1ull << (r & 63);
-    if (w & bit) {
-      rc = c->fail(DM_E_INVAL, "rows must be unique within one call");
-      break;
-    }
-    w |= bit;
+  if (!c->upd_flags.p) {
+    DM_HIP(c, c->upd_flags.ensure(1), "update flags");
+    DM_HIP(c, hipHostMalloc((void**)&c->h_flags, sizeof(uint32_t), hipHostMallocDefault), "update flags");
   }
-  for (int64_t j = 0; j < i; ++j) c->seen[(size_t)(rows[j] >> 6)] = 0;  // O(n) reset
-  if (rc) return rc;
-  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
+  DM_HIP(c, hipMemsetAsync(c->upd_flags.p, 0, sizeof(uint32_t), c->stream), "update flags");
+  (void)rows;
+  DM_HIP(c, launch_check_rows(n, c->st_rows.p, c->N, c->row_bits.p, wants_dev, sub_dev, c->upd_flags.p, c->stream),
+         "check rows");
+  return DM_OK;
+}
+
+// After the apply kernel: clear the bitmap, fetch the flags, wait (the call is
+// synchronous on return, so the caller may free its buffers), map errors.
+static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
+  DM_HIP(c, launch_clear_rows(n, c->st_rows.p, c->N, c->row_bits.p, c->stream), "clear rows");
+  DM_HIP(c, hipMemcpyAsync(c->h_flags, c->upd_flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream),
+         "update flags");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "update");
+  const uint32_t f = *c->h_flags;
+  *flags_out = f;
+  if (f & kUpdRange) return c->fail(DM_E_RANGE, "row out of range");
+  if (f & kUpdDup) return c->fail(DM_E_INVAL, "rows must be unique within one call");
+  if (f & kUpdSub) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
   return DM_OK;
 }
 
@@ -730,21 +751,22 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
-  for (int64_t i = 0; i < n; ++i)
-    if (sub[i] < 0 || sub[i] > INT32_MAX) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
-  int rc = stage_rows(c, n, rows);
-  if (rc) return rc;
+  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
   DM_HIP(c, upload(c->st_has, has, (size_t)n, c->stream), "stage has");
   DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
   DM_HIP(c, upload(c->st_sub, sub, (size_t)n, c->stream), "stage sub");
   DM_HIP(c, upload(c->st_exp, exp, (size_t)n, c->stream), "stage expiry");
-  // an upsert can make a resource's subclients heterogeneous: stay conservative
-  for (int64_t i = 0; i < n && !c->maybe_general; ++i)
-    if (std::isnan(wants[i]) || sub[i] != 1 || !c->all_sub_one) c->maybe_general = true;
+  int rc = begin_update(c, n, rows, c->st_wants.p, c->st_sub.p);
+  if (rc) return rc;
   DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->seg_off.p, c->R,
-                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->stream),
+                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->upd_flags.p, c->stream),
          "upsert");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "upsert");
+  uint32_t f = 0;
+  rc = finish_update(c, n, &f);
+  if (rc) return rc;
+  // an upsert can make a resource's subclients heterogeneous: stay conservative
+  if ((f & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one) c->maybe_general = true;
+  if (f & kUpdNotOne) c->all_sub_one = false;
   c->have_result = false;
   return DM_OK;
 }
@@ -754,14 +776,17 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
-  for (int64_t i = 0; i < n && !c->maybe_general; ++i)
-    if (std::isnan(wants[i])) c->maybe_general = true;
-  int rc = stage_rows(c, n, rows);
-  if (rc) return rc;
+  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
   DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
-  DM_HIP(c, launch_update_wants(n, c->st_rows.p, c->st_wants.p, c->seg_off.p, c->R, c->wants.p, c->agg.p, c->stream),
+  int rc = begin_update(c, n, rows, c->st_wants.p, nullptr);
+  if (rc) return rc;
+  DM_HIP(c, launch_update_wants(n, c->st_rows.p, c->st_wants.p, c->seg_off.p, c->R, c->wants.p, c->agg.p,
+                                c->upd_flags.p, c->stream),
          "update wants");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "update wants");
+  uint32_t f = 0;
+  rc = finish_update(c, n, &f);
+  if (rc) return rc;
+  if (f & kUpdNaN) c->maybe_general = true;
   c->have_result = false;
   return DM_OK;
 }
@@ -771,13 +796,31 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
-  int rc = stage_rows(c, n, rows);
+  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
+  int rc = begin_update(c, n, rows, nullptr, nullptr);
   if (rc) return rc;
   DM_HIP(c, launch_release(n, c->st_rows.p, c->seg_off.p, c->R, c->has.p, c->wants.p, c->sub.p, c->expiry.p,
-                           c->agg.p, c->stream),
+                           c->agg.p, c->upd_flags.p, c->stream),
          "release");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "release");
+  uint32_t f = 0;
+  rc = finish_update(c, n, &f);
+  if (rc) return rc;
   c->have_result = false;
+  return DM_OK;
+}
+
+int dm_host_alloc(dm_ctx* c, size_t bytes, void** out) {
+  DM_CHECK_CTX(c);
+  if (!out) return c->fail(DM_E_INVAL, "null out");
+  *out = nullptr;
+  if (bytes == 0) return DM_OK;
+  DM_HIP(c, hipHostMalloc(out, bytes, hipHostMallocDefault), "pinned host buffer");
+  return DM_OK;
+}
+
+int dm_host_free(dm_ctx* c, void* p) {
+  DM_CHECK_CTX(c);
+  if (p) DM_HIP(c, hipHostFree(p), "pinned host buffer");
   return DM_OK;
 }
 

@@ -37,10 +37,25 @@ class Engine:
         self.device = device
         self.n_resources = 0
         self.n_leases = 0
+        self._pinned = []
 
     # -- lifetime --
+    def host_empty(self, n: int, dtype=np.float64) -> np.ndarray:
+        """A page-locked host array (dm_host_alloc), for update batches that should cross
+        PCIe by DMA at full rate.  Valid until close()."""
+        dtype = np.dtype(dtype)
+        nbytes = max(int(n), 1) * dtype.itemsize
+        ptr = ctypes.c_void_p()
+        self._chk(self._L.dm_host_alloc(self._ctx, nbytes, ctypes.byref(ptr)))
+        self._pinned.append(ptr.value)
+        buf = (ctypes.c_byte * nbytes).from_address(ptr.value)
+        return np.frombuffer(buf, dtype=dtype, count=int(n))
+
     def close(self):
         if self._ctx:
+            for ptr in getattr(self, "_pinned", []):
+                self._L.dm_host_free(self._ctx, ctypes.c_void_p(ptr))
+            self._pinned = []
             self._L.dm_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
 

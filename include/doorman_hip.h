@@ -31,6 +31,7 @@
 #ifndef DOORMAN_HIP_H
 #define DOORMAN_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -120,6 +121,13 @@ int dm_store_update_wants(dm_ctx* ctx, int64_t n, const int64_t* rows, const dou
 /* Release (store.go:142-151): sums -= row; row zeroed and marked DM_RELEASED.  A released
  * row is a free slot: dm_store_upsert onto it is Assign of a new client. */
 int dm_store_release(dm_ctx* ctx, int64_t n, const int64_t* rows);
+/* The three update calls validate on the device (rows in [0, N), unique within the
+ * call, subclients in [0, 2^31)); a rejected call (DM_E_RANGE / DM_E_INVAL) leaves the
+ * store untouched.  They return after the update is applied, so the caller may reuse
+ * its buffers.  Buffers from dm_host_alloc (page-locked) go over PCIe by DMA at full
+ * rate; ordinary host memory is staged by the HIP runtime. */
+int dm_host_alloc(dm_ctx* ctx, size_t bytes, void** out);
+int dm_host_free(dm_ctx* ctx, void* ptr);
 /* read back stored rows (has/wants/subclients/expiry_ns) — any pointer may be NULL */
 int dm_read_store(dm_ctx* ctx, int64_t off, int64_t n, double* has, double* wants, int64_t* subclients,
                   int64_t* expiry_ns);

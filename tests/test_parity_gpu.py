@@ -334,6 +334,50 @@ def test_upsert_rejects_duplicate_and_out_of_range_rows(eng):
     assert e.value.code == DM_E_RANGE
 
 
+def test_rejected_update_leaves_store_untouched(eng):
+    """Validation runs on the device before the apply kernel: duplicate, out-of-range
+    rows and bad subclients reject the whole call; the store and its sums are unchanged
+    and the row bitmap is clean for the next call."""
+    from doorman_amd._lib import DM_E_INVAL, DM_E_RANGE, DmError
+    snap = W.make_snapshot([4, 4], np.ones(8), np.zeros(8), 1, NOW + W.NS, 3, 10.0)
+    eng.load(snap)
+    before = eng.read_store()
+    for call, code in [(lambda: eng.update_wants([0, 5, 5], [2.0, 2.0, 2.0]), DM_E_INVAL),
+                       (lambda: eng.update_wants([0, 9], [2.0, 2.0]), DM_E_RANGE),
+                       (lambda: eng.release([3, -1]), DM_E_RANGE),
+                       (lambda: eng.upsert([2], [1.0], [1.0], [-3], [NOW]), DM_E_INVAL),
+                       (lambda: eng.upsert([2, 6], [1.0, 1.0], [1.0, 1.0], [1, 2 ** 31], [NOW, NOW]), DM_E_INVAL)]:
+        with pytest.raises(DmError) as e:
+            call()
+        assert e.value.code == code
+        after = eng.read_store()
+        for k in before:
+            np.testing.assert_array_equal(before[k], after[k], err_msg=k)
+    # the same rows are accepted afterwards (bitmap cleared), unsorted order is fine
+    eng.update_wants([5, 0], [3.0, 4.0])
+    assert eng.read_store()["wants"][[0, 5]].tolist() == [4.0, 3.0]
+
+
+def test_pinned_update_buffers(eng):
+    """dm_host_alloc buffers feed the update calls like ordinary host arrays."""
+    rng = np.random.default_rng(5)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=False), expired_frac=0.0, kinds=(2, 3))
+    eng.load(snap)
+    N = len(snap["wants"])
+    n = N // 7
+    rows = eng.host_empty(n, np.int64)
+    rows[:] = np.sort(rng.choice(N, n, replace=False))
+    w = eng.host_empty(n)
+    w[:] = snap["wants"][rows] * rng.uniform(0.5, 2.0, n)
+    eng.update_wants(rows, w)
+    snap2 = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    snap2["wants"][rows] = w
+    snap2["agg_sum_wants"] = eng.resources(safe=False)["sum_wants"]
+    eng.apportion(NOW)
+    gets, exp = eng.leases()
+    assert_leases_match(snap2, gets, exp, O.apportion(snap2, NOW), "pinned update")
+
+
 def test_update_wants_narrow_assign(eng):
     """dm_store_update_wants: Assign of a refresh that changes only wants."""
     rng = np.random.default_rng(22)

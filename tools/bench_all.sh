@@ -1,0 +1,13 @@
+#!/bin/bash
+# Every bench workload once (one GPU), JSON lines into gpurun_out/bench_all/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/bench_all
+for w in ${WORKLOADS:-c1 c1ps c2 c3 c4}; do
+  timeout -k 10 600 python bench.py --workload $w --steps ${STEPS:-20} --warmup 3 $( [ "$w" = c1 ] || echo --no-cpu-baseline ) \
+    > gpurun_out/bench_all/$w.json 2> gpurun_out/bench_all/$w.err
+  s=$?; echo "$w status $s"; [ $s -ne 0 ] && { tail -3 gpurun_out/bench_all/$w.err; exit $s; }
+done
+timeout -k 10 600 python bench.py --hier --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline \
+  > gpurun_out/bench_all/hier.json 2> gpurun_out/bench_all/hier.err
+s=$?; echo "hier status $s"; exit $s
