@@ -17,6 +17,9 @@ constexpr int kSmallMax = 16;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
 constexpr int kNumBins = 7;  // wave64x{1,2,4}, block256x{2,4}, block512x4, block1024x4
+// Lease-table footprint (48 B per lease) above which a tick is taken to stream
+// from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
+constexpr int64_t kStreamBytes = 1LL << 30;
 
 struct Pack {  // a run of consecutive small resources covering <= 64 rows
   int32_t first_seg;

@@ -114,7 +114,10 @@ __device__ __forceinline__ T wave_reduce(T v, Op op) {
 // Group reduction (G = 64: one wave; G >= 256: the waves' totals through LDS).
 // Every thread combines the wave totals in the same fixed order, so all threads
 // (and all workgroups reducing the same inputs) agree bit for bit.
-template <int G, typename T, typename Op>
+// REUSE = false: the LDS slots are written once per workgroup (group_segment
+// gives every reduction its own slots), so the barrier that protects them from
+// the next reduction's writes is dropped.
+template <int G, typename T, typename Op, bool REUSE = true>
 __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
   v = wave_reduce(v, op);
   if constexpr (G == 64) {
@@ -130,7 +133,7 @@ __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
       const T x = lds[i];
       r = op(r, x);
     }
-    __syncthreads();
+    if constexpr (REUSE) __syncthreads();
     return r;
   }
 }
@@ -342,7 +345,11 @@ __device__ __forceinline__ double fs_stage2(double w, double h, long long s, dou
 // Resource-per-group kernel: G threads (a wave or a 256-thread workgroup) own
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
-template <int G, int R>
+// BATCH = row-blocks whose loads share one memory round trip (R: all at once).
+// All at once wins while repeated ticks are partly served by the Infinity Cache
+// (C1, 480 MB: +14%); on a store that streams from HBM (C3, 4.8 GB) two
+// round trips of half the requests each are ~10% faster (tools/ab.py).
+template <int G, int R, int BATCH>
 __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, int t, Lds<G>& lds,
                                               int32_t* general_list, int32_t* general_count) {
   const int seg = wi.seg;
@@ -358,23 +365,28 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // the rows stay in VGPRs for every pass: 6 registers per row
   double w[R], h[R];
   int s[R];  // subclients < 2^31 (checked by the host at load/upsert)
+  int64_t e[R];
   unsigned valid = 0, live = 0;
+  // Every load is issued before any is consumed: lanes past the segment end
+  // re-read row n-1 (same cache line, n >= 1 in every bin) instead of branching
+  // around the load, which made the compiler wait on each row's expiry before
+  // issuing the next row (R serial memory latencies per workgroup).
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     const int i = k * G + t;
-    w[k] = 0.0;
-    h[k] = 0.0;
-    s[k] = 0;
-    if (i < n) {
-      const unsigned u = (unsigned)i;
-      // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
-      w[k] = wb[u];
-      h[k] = hb[u];
-      s[k] = (int)sb[u];
-      const int64_t e = eb[u];
-      valid |= 1u << k;
-      if (!(p.now > e)) live |= 1u << k;  // store.go:174 when.After(expiry)
-    }
+    const unsigned u = (unsigned)(i < n ? i : n - 1);
+    // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
+    w[k] = wb[u];
+    h[k] = hb[u];
+    s[k] = (int)sb[u];
+    e[k] = eb[u];
+    if (BATCH < R && (k + 1) % BATCH == 0 && k + 1 < R) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) {  // rows past the end stay out of valid/live, so every pass skips them
+    const unsigned vk = (k * G + t < n) ? 1u : 0u;
+    valid |= vk << k;
+    live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;  // store.go:174 when.After(expiry)
   }
   const Res rs = load_res(p, seg);
 
@@ -402,8 +414,8 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   }
   {
     const AggR all_part = a.all;
-    a = group_reduce<G>(a, OpA(), lds.a);
-    if (p.recompute) a.all = group_reduce<G>(all_part, OpR(), lds.r);
+    a = group_reduce<G, AggA, OpA, false>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce<G, AggR, OpR, false>(all_part, OpR(), lds.r);
   }
   const Clean cl = clean_from(p, rs, a);
   const double C = rs.C;
@@ -439,7 +451,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
           b.i += s[k];  // :168
       }
     }
-    b = group_reduce<G>(b, OpB(), lds.b);
+    b = group_reduce<G, AggB, OpB, false>(b, OpB(), lds.b);
   }
 
   // ---- pass C (uniform subclients): FairShare round 2 at the resource's one threshold ----
@@ -457,7 +469,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       else if (w[k] > Tu)
         cu.sgt += s[k];  // :199-200
     }
-    cu = group_reduce<G>(cu, OpC(), lds.c);
+    cu = group_reduce<G, AggC, OpC, false>(cu, OpC(), lds.c);
     fu = make_fsu(eq, a.smin, b.x, b.i, cu);
   }
 
@@ -496,28 +508,28 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     delta.v += g - h[k];
   }
 
-  delta = group_reduce<G>(delta, OpSumD(), lds.d);
+  delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
   if (t == 0) write_resource(p, seg, rs, cl, delta.v);
 }
 
 // One G-thread workgroup per resource (G = 256..1024, R <= 4 rows per thread).
-template <int G, int R>
+template <int G, int R, int BATCH = R>
 __global__ __launch_bounds__(G) void k_block(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nitems) return;
-  group_segment<G, R>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
+  group_segment<G, R, BATCH>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
 }
 
 // One wave per resource (n <= 64 R), four independent waves per workgroup: wave
 // reductions only (DPP, no barriers), four resources in flight per workgroup.
-template <int R>
+template <int R, int BATCH = R>
 __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                               int32_t* general_list, int32_t* general_count) {
   Lds<64> lds;  // unused by wave reductions
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nitems) return;
-  group_segment<64, R>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
+  group_segment<64, R, BATCH>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -787,20 +799,22 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   const int64_t* __restrict__ eb = p.expiry + ch.row0;
   r.valid = 0;
   r.live = 0;
+  int64_t e[kLR];
+  // all loads in flight before the first is consumed (see group_segment)
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
-    r.w[k] = 0.0;
-    r.h[k] = 0.0;
-    r.s[k] = 0;
-    if (i < ch.nrows) {
-      const unsigned u = (unsigned)i;
-      r.w[k] = wb[u];
-      r.h[k] = hb[u];
-      r.s[k] = (int)sb[u];
-      r.valid |= 1u << k;
-      if (!(p.now > eb[u])) r.live |= 1u << k;
-    }
+    const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
+    r.w[k] = wb[u];
+    r.h[k] = hb[u];
+    r.s[k] = (int)sb[u];
+    e[k] = eb[u];
+  }
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    const unsigned vk = (k * 256 + (int)threadIdx.x < ch.nrows) ? 1u : 0u;
+    r.valid |= vk << k;
+    r.live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;
   }
 }
 
@@ -1342,16 +1356,29 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
 }
 
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
-                      hipStream_t st) {
+                      bool hbm_stream, hipStream_t st) {
   if (n <= 0) return hipSuccess;
+  const unsigned wg4 = (unsigned)((n + 3) / 4);
   switch (bin) {
-    case 0: k_wave<1><<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 1: k_wave<2><<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 2: k_wave<4><<<(n + 3) / 4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 0: k_wave<1><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 1: k_wave<2><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 2:
+      if (hbm_stream) k_wave<4, 2><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount);
+      else k_wave<4><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount);
+      break;
     case 3: k_block<256, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 4: k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 5: k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 6: k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 4:
+      if (hbm_stream) k_block<256, 4, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount);
+      else k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount);
+      break;
+    case 5:
+      if (hbm_stream) k_block<512, 4, 2><<<n, 512, 0, st>>>(p, segs, n, glist, gcount);
+      else k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount);
+      break;
+    case 6:
+      if (hbm_stream) k_block<1024, 4, 2><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
+      else k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -18,7 +18,7 @@
 namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
-                      hipStream_t st);
+                      bool hbm_stream, hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
@@ -601,11 +601,15 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
                     [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
            "large-resource kernels");
+  // a store well beyond the Infinity Cache streams from HBM every tick: group
+  // kernels then keep half their row loads in flight (dm_kernels.hip, BATCH)
+  const bool hbm_stream = c->N * 48 > kStreamBytes;
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
     hipStream_t s = b >= 4 ? s_big : s_small;
-    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }), "group kernel");
+    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, hbm_stream, s); }),
+           "group kernel");
   }
   if (!c->h_packs.empty())
     DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), s_small); }),

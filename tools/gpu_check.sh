@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=${STEPS:-30}
 WORKLOAD=${WORKLOAD:-c1}
-PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -x -q"}
+PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -x -q --timeout 120 --timeout-method thread"}
 
 stop_if_fatal() {  # $1 = exit status, $2 = step
   case "$1" in
@@ -17,7 +17,7 @@ stop_if_fatal() {  # $1 = exit status, $2 = step
 }
 
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 900 python -m pytest $PYTEST_ARGS > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest $PYTEST_ARGS > gpurun_out/pytest_gpu.log 2>&1
   s=$?; tail -5 gpurun_out/pytest_gpu.log; stop_if_fatal $s pytest
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   s=$?; tail -3 gpurun_out/smoke.log; stop_if_fatal $s smoke
