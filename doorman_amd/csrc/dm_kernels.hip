@@ -537,46 +537,55 @@ __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __res
 // resources; every lane evaluates its own client literally, looping over its
 // resource's rows in row order (shuffles).  Sums are taken in the same order as
 // the oracle, so this path is bit-exact against it.
+// Shuffle budget per loop step: wants (2 dwords) + one int carrying subclients
+// and the live bit (sl = live ? s : ~s); Clean's loop runs only when a row of the
+// pack expired; the owners' sumHas loop moves gets - has as one double.
 // --------------------------------------------------------------------------
+__device__ __forceinline__ int shfl_i(int v, int lane) { return __shfl(v, lane, 64); }
+__device__ __forceinline__ double shfl_d(double v, int lane) { return shfl_any(v, lane); }
+
 __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restrict__ packs, int npacks) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wv >= npacks) return;
   const int lane = threadIdx.x & 63;
   const Pack& pkr = packs[wv];
-  Pack pk;
-  pk.first_seg = pkr.first_seg;
-  pk.nseg = pkr.nseg;
-  pk.row0 = pkr.row0;
-  pk.nrows = pkr.nrows;
-  pk.maxlen = pkr.maxlen;
-  const int64_t offk = lane <= pk.nseg ? pk.row0 + pkr.rel[lane] : INT64_MAX;
-  const int64_t row = pk.row0 + lane;
-  const bool valid = lane < pk.nrows;
-  // resource of this row: last k < nseg with seg_off[first+k] <= row
+  const int first_seg = pkr.first_seg, nseg = pkr.nseg, nrows = pkr.nrows, maxlen = pkr.maxlen;
+  const int64_t row0 = pkr.row0;
+  const bool valid = lane < nrows;
+  // rows first (every lane loads; lanes past the pack re-read its last row), so
+  // their latency overlaps the segment search and the config gathers
+  double w = 0.0, h = 0.0;
+  int s = 0;
+  int64_t e = 0;
+  if (nrows > 0) {
+    const int64_t row = row0 + (valid ? lane : nrows - 1);
+    w = p.wants[row];
+    h = p.has[row];
+    s = (int)p.sub[row];
+    e = p.expiry[row];
+  }
+  // resource of this row: last k < nseg with rel[k] <= lane (offsets relative to row0)
+  const int offk = lane <= nseg ? (int)pkr.rel[lane] : INT32_MAX;
   int k = 0;
 #pragma unroll
   for (int step = 32; step > 0; step >>= 1) {
     const int c = k + step;
-    const long long oc = __shfl((long long)offk, c < 64 ? c : 63, 64);
-    if (c < pk.nseg && oc <= row) k = c;
+    const int oc = shfl_i(offk, c < 64 ? c : 63);
+    if (c < nseg && oc <= lane) k = c;
   }
-  const long long seg_lo = __shfl((long long)offk, k, 64);
-  const long long seg_hi = __shfl((long long)offk, k + 1 < 64 ? k + 1 : 63, 64);
-  const int lo = valid ? (int)(seg_lo - pk.row0) : 0;
-  const int hi = valid ? (int)(seg_hi - pk.row0) : 0;
-  const int seg = pk.first_seg + k;
-  const int maxlen = pk.maxlen;
-
-  double w = 0.0, h = 0.0;
-  long long s = 0;
-  int lv = 0;
-  if (valid) {
-    w = p.wants[row];
-    h = p.has[row];
-    s = p.sub[row];
-    lv = !(p.now > p.expiry[row]) ? 1 : 0;
-  }
+  // shuffles run on the full wave (a masked-off source lane would read stale LDS)
+  const int seg_lo = shfl_i(offk, k), seg_hi = shfl_i(offk, k + 1 < 64 ? k + 1 : 63);
+  const int lo = valid ? seg_lo : 0;
+  const int hi = valid ? seg_hi : 0;
+  const int seg = first_seg + k;
   const Res rs = load_res(p, seg);
+  const int lv = (valid && !(p.now > e)) ? 1 : 0;  // store.go:174
+  if (!valid) {
+    w = 0.0;
+    h = 0.0;
+    s = 0;
+  }
+  const int sl = lv ? s : ~s;  // subclients and the live bit in one shuffle
 
   // Clean, in row order (store.go:169-181)
   long long count = 0;
@@ -584,12 +593,12 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   if (p.recompute) {
     for (int q = 0; q < maxlen; ++q) {
       const int j = lo + q;
-      const double hj = __shfl(h, j & 63, 64), wj = __shfl(w, j & 63, 64);
-      const long long sj = __shfl(s, j & 63, 64);
+      const double hj = shfl_d(h, j & 63), wj = shfl_d(w, j & 63);
+      const int sj = shfl_i(sl, j & 63);
       if (j < hi) {
         sh += hj - 0.0;
         sw += wj - 0.0;
-        count += sj;
+        count += sj >= 0 ? sj : ~sj;
       }
     }
   } else {
@@ -597,15 +606,16 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     sh = rs.agg_has;
     sw = rs.agg_wants;
   }
-  for (int q = 0; q < maxlen; ++q) {
-    const int j = lo + q;
-    const double hj = __shfl(h, j & 63, 64), wj = __shfl(w, j & 63, 64);
-    const long long sj = __shfl(s, j & 63, 64);
-    const int lj = __shfl(lv, j & 63, 64);
-    if (j < hi && !lj) {
-      sw -= wj;
-      sh -= hj;
-      count -= sj;
+  if (__any(valid && !lv)) {  // some row of the pack expired
+    for (int q = 0; q < maxlen; ++q) {
+      const int j = lo + q;
+      const double hj = shfl_d(h, j & 63), wj = shfl_d(w, j & 63);
+      const int sj = shfl_i(sl, j & 63);
+      if (j < hi && sj < 0) {
+        sw -= wj;
+        sh -= hj;
+        count -= ~sj;
+      }
     }
   }
 
@@ -617,24 +627,25 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   double x = 0.0, y = 0.0;
   long long wi = 0;
   const bool ps = !rs.learning && rs.kind == 2, fs = !rs.learning && rs.kind == 3;
-  for (int q = 0; q < maxlen; ++q) {
-    const int j = lo + q;
-    const double wj = __shfl(w, j & 63, 64);
-    const long long sj = __shfl(s, j & 63, 64);
-    const int lj = __shfl(lv, j & 63, 64);
-    if (j < hi && lj) {
-      if (ps) {
-        const double e = eq * (double)sj;
-        if (wj < e)
-          x += e - wj;
-        else
-          y += wj - e;
-      } else if (fs) {
-        const double d = (double)sj * eq;
-        if (wj < d)
-          x += d - wj;
-        else if (wj > d)
-          wi += sj;
+  if (__any(ps || fs)) {
+    for (int q = 0; q < maxlen; ++q) {
+      const int j = lo + q;
+      const double wj = shfl_d(w, j & 63);
+      const int sj = shfl_i(sl, j & 63);
+      if (j < hi && sj >= 0) {
+        if (ps) {
+          const double e2 = eq * (double)sj;
+          if (wj < e2)
+            x += e2 - wj;
+          else
+            y += wj - e2;
+        } else if (fs) {
+          const double d = (double)sj * eq;
+          if (wj < d)
+            x += d - wj;
+          else if (wj > d)
+            wi += sj;
+        }
       }
     }
   }
@@ -658,10 +669,9 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     AggC c{0.0, 0};
     for (int q = 0; q < maxlen; ++q) {
       const int j = lo + q;
-      const double wj = __shfl(w, j & 63, 64);
-      const long long sj = __shfl(s, j & 63, 64);
-      const int lj = __shfl(lv, j & 63, 64);
-      if (j < hi && lj && wj > (double)sj * eq) {
+      const double wj = shfl_d(w, j & 63);
+      const int sj = shfl_i(sl, j & 63);
+      if (j < hi && sj >= 0 && wj > (double)sj * eq) {
         if (wj < T)
           c.ee += T - wj;
         else if (wj > T)
@@ -672,36 +682,36 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   }
   if (valid) {
     if (lv) {
-      __builtin_nontemporal_store(g, p.out_gets + row);
-      __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
+      __builtin_nontemporal_store(g, p.out_gets + row0 + lane);
+      __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row0 + lane);
     } else {
-      __builtin_nontemporal_store(0.0, p.out_gets + row);
-      __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row);
+      __builtin_nontemporal_store(0.0, p.out_gets + row0 + lane);
+      __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row0 + lane);
       if (p.out_wants) {
-        p.out_wants[row] = 0.0;
-        p.out_sub[row] = 0;
+        p.out_wants[row0 + lane] = 0.0;
+        p.out_sub[row0 + lane] = 0;
       }
     }
   }
   // per-resource results: lane k (< nseg) owns resource first_seg + k
-  const bool owner = lane < pk.nseg;
-  const int olo = (int)(offk - pk.row0);
-  const int ohi = (int)(__shfl((long long)offk, lane + 1 < 64 ? lane + 1 : 63, 64) - pk.row0);
+  const bool owner = lane < nseg;
+  const int olo = offk;
+  const int ohi = shfl_i(offk, lane + 1 < 64 ? lane + 1 : 63);
   long long ocount = __shfl(count, olo & 63, 64);
-  double osh = __shfl(sh, olo & 63, 64), osw = __shfl(sw, olo & 63, 64);
-  const double gl = lv ? g : 0.0;
+  double osh = shfl_d(sh, olo & 63), osw = shfl_d(sw, olo & 63);
+  const double gh = g - h;  // Assign: sumHas += gets - has (store.go:156)
   for (int q = 0; q < maxlen; ++q) {
     const int j = olo + q;
-    const double gj = __shfl(gl, j & 63, 64), hj = __shfl(h, j & 63, 64);
-    const int lj = __shfl(lv, j & 63, 64);
-    if (owner && j < ohi && lj) osh += gj - hj;
+    const double dj = shfl_d(gh, j & 63);
+    const int sj = shfl_i(sl, j & 63);
+    if (owner && j < ohi && sj >= 0) osh += dj;
   }
   // SetSafeCapacity inputs from the resource's first row lane (no second config load)
   Res ors;
-  ors.cap_cfg = __shfl(rs.cap_cfg, olo & 63, 64);
-  ors.safe = __shfl(rs.safe, olo & 63, 64);
+  ors.cap_cfg = shfl_d(rs.cap_cfg, olo & 63);
+  ors.safe = shfl_d(rs.safe, olo & 63);
   if (owner) {
-    const int oseg = pk.first_seg + lane;
+    const int oseg = first_seg + lane;
     if (olo == ohi) {  // resource without rows
       ocount = p.recompute ? 0 : p.agg[oseg].count;
       osh = p.recompute ? 0.0 : p.agg[oseg].sum_has;
