@@ -75,9 +75,10 @@ def kernel_units(eng, snap):
     so = snap["seg_off"]
     sizes = np.diff(so)
     units = {}
-    edges = [("wave64x1", 17, 64), ("wave64x2", 65, 128), ("wave64x4", 129, 256), ("block256x2", 257, 512),
-             ("block256x4", 513, 1024), ("block512x4", 1025, 2048), ("block1024x4", 2049, 4096)]
-    small = sizes <= 16
+    edges = [("group16", 9, 16), ("group32", 17, 32), ("wave64x1", 33, 64), ("wave64x2", 65, 128),
+             ("wave64x4", 129, 256), ("block256x2", 257, 512), ("block256x4", 513, 1024), ("block512x4", 1025, 2048),
+             ("block1024x4", 2049, 4096)]
+    small = sizes <= 8
     units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
     for name, lo, hi in edges:
         m = (sizes >= lo) & (sizes <= hi)

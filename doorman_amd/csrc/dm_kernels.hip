@@ -101,14 +101,30 @@ __device__ __forceinline__ T readlane_any(const T& v, int lane) {
 // mirror, mirror: partner lanes compute a+b and b+a, so every lane of a row holds
 // the same row total), then the four row totals combined in a fixed order from
 // scalar readlanes.  Requires all 64 lanes active.
-template <typename T, typename Op>
-__device__ __forceinline__ T wave_reduce(T v, Op op) {
+// Sub-wave groups (G = 16: one DPP row, G = 32: half a wave) reduce within
+// themselves: every lane of the group gets its group's total.
+template <int G, typename T, typename Op>
+__device__ __forceinline__ T wave_reduce_g(T v, Op op) {
+  static_assert(G == 16 || G == 32 || G == 64, "sub-wave group");
   v = op(v, dpp_any<0xB1>(v));   // quad_perm [1,0,3,2]
   v = op(v, dpp_any<0x4E>(v));   // quad_perm [2,3,0,1]
   v = op(v, dpp_any<0x141>(v));  // row_half_mirror
   v = op(v, dpp_any<0x140>(v));  // row_mirror
-  const T r0 = readlane_any(v, 0), r1 = readlane_any(v, 16), r2 = readlane_any(v, 32), r3 = readlane_any(v, 48);
-  return op(op(r0, r1), op(r2, r3));
+  if constexpr (G == 16) {
+    return v;
+  } else {
+    const T r0 = readlane_any(v, 0), r1 = readlane_any(v, 16), r2 = readlane_any(v, 32), r3 = readlane_any(v, 48);
+    if constexpr (G == 32) {
+      const T lo = op(r0, r1), hi = op(r2, r3);
+      return (threadIdx.x & 32) ? hi : lo;
+    } else {
+      return op(op(r0, r1), op(r2, r3));
+    }
+  }
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+  return wave_reduce_g<64>(v, op);
 }
 
 // Group reduction (G = 64: one wave; G >= 256: the waves' totals through LDS).
@@ -119,8 +135,8 @@ __device__ __forceinline__ T wave_reduce(T v, Op op) {
 // the next reduction's writes is dropped.
 template <int G, typename T, typename Op, bool REUSE = true>
 __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
-  v = wave_reduce(v, op);
-  if constexpr (G == 64) {
+  v = wave_reduce_g<(G < 64 ? G : 64)>(v, op);
+  if constexpr (G <= 64) {
     (void)lds;
     return v;
   } else {
@@ -247,13 +263,14 @@ struct OpSumD {
 };
 
 template <int G>
-struct Lds {
-  AggA a[G / 64];
-  AggR r[G / 64];
-  AggB b[G / 64];
-  AggC c[G / 64];
-  TMin t[G / 64];
-  SumD d[G / 64];
+struct Lds {  // one slot per wave (unused by groups of one wave or less)
+  static constexpr int W = G >= 64 ? G / 64 : 1;
+  AggA a[W];
+  AggR r[W];
+  AggB b[W];
+  AggC c[W];
+  TMin t[W];
+  SumD d[W];
 };
 
 // Cleaned store sums from pass A (store.go:169-181 applied to the snapshot).
@@ -530,6 +547,18 @@ __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __res
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nitems) return;
   group_segment<64, R, BATCH>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
+}
+
+// Sub-wave groups: G = 16 or 32 lanes own one resource of up to G rows, so a
+// wave decides 64 / G resources with one set of reduction chains (DPP inside
+// each 16-lane row, plus one readlane combine for G = 32).
+template <int G>
+__global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __restrict__ items, int nitems,
+                                             int32_t* general_list, int32_t* general_count) {
+  Lds<G> lds;  // unused by sub-wave reductions
+  const int i = blockIdx.x * (256 / G) + (int)(threadIdx.x / G);
+  if (i >= nitems) return;  // whole groups only: reductions never cross a group
+  group_segment<G, 1, 1>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -1389,6 +1418,8 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
       if (hbm_stream) k_block<1024, 4, 2><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
       else k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
       break;
+    case 7: k_sub<16><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 8: k_sub<32><<<(unsigned)((n + 7) / 8), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

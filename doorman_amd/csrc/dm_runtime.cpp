@@ -62,7 +62,8 @@ enum KClass {
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "wave64x1",   "wave64x2",   "wave64x4",   "block256x2",
-                                     "block256x4",   "block512x4", "block1024x4", "large_a",   "large_b",
+                                     "block256x4",   "block512x4", "block1024x4", "group16",   "group32",
+                                     "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release"};
 
@@ -226,6 +227,8 @@ static hipError_t upload(DBuf<T>& b, const T* src, size_t n, hipStream_t st) {
 // plan: size-binned dispatch
 // ---------------------------------------------------------------------------
 static int bin_of(int64_t n) {
+  if (n <= 16) return 7;
+  if (n <= 32) return 8;
   if (n <= 64) return 0;
   if (n <= 128) return 1;
   if (n <= 256) return 2;
@@ -587,8 +590,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // small groups + packed.  With more than one class present they run on the
   // auxiliary streams concurrently, forked from and joined back to the main stream.
   int big_bins = 0, small_bins = 0;
-  for (int b = 4; b < kNumBins; ++b) big_bins += !c->h_bins[b].empty();
-  for (int b = 0; b < 4; ++b) small_bins += !c->h_bins[b].empty();
+  auto is_big = [](int b) { return b >= 4 && b <= 6; };  // block256x4, block512x4, block1024x4
+  for (int b = 0; b < kNumBins; ++b) (is_big(b) ? big_bins : small_bins) += !c->h_bins[b].empty();
   const bool has_small = small_bins > 0 || !c->h_packs.empty();
   const int classes = (nch > 0) + (big_bins > 0) + has_small;
   const bool fork = classes > 1;
@@ -607,7 +610,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    hipStream_t s = b >= 4 ? s_big : s_small;
+    hipStream_t s = is_big(b) ? s_big : s_small;
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, hbm_stream, s); }),
            "group kernel");
   }

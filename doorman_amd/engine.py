@@ -16,7 +16,7 @@ from ._lib import check, lib
 from .workloads import CFG_FIELDS
 
 _BIN_NAMES = ("small_packs", "wave64x1", "wave64x2", "wave64x4", "block256x2", "block256x4", "block512x4",
-              "block1024x4", "large_resources", "large_chunks", "leases")
+              "block1024x4", "group16", "group32", "large_resources", "large_chunks", "leases")
 
 
 def _ptr(a):

@@ -54,13 +54,14 @@ def assert_resources_match(snap, res, ref, label=""):
 
 def binned_sizes(rng, per_bin=3, large=True):
     """Resource sizes that exercise every dispatch bin, incl. empty resources."""
-    edges = [(0, 0), (1, 16), (17, 64), (65, 256), (257, 512), (513, 1024), (1025, 2048), (2049, 4096)]
+    edges = [(0, 0), (1, 8), (9, 16), (17, 32), (33, 64), (65, 256), (257, 512), (513, 1024), (1025, 2048),
+             (2049, 4096)]
     if large:
         edges.append((4097, 13000))
     sizes = []
     for lo, hi in edges:
         sizes += list(rng.integers(lo, hi + 1, per_bin))
-    sizes += [64, 65, 256, 257, 4096]
+    sizes += [8, 9, 16, 17, 32, 33, 64, 65, 256, 257, 4096]
     if large:
         sizes += [4097, 8192]
     rng.shuffle(sizes)
