@@ -64,10 +64,15 @@ def make_workload(name: str, rank: int):
     raise SystemExit(f"unknown workload {name}")
 
 
+LEASE_BYTES = 44  # read wants 8 + has 8 + subclients 4 + expiry 8, write gets 8 + expiry 8
+
+
 def algorithmic_bytes(n_leases: int, n_resources: int) -> int:
-    # per lease read wants/has/subclients/expiry, write gets/expiry (48 B);
+    # BASELINE.md §3 / SURVEY.md §8(d) per lease: read wants, has, subclients, expiry; write
+    # gets, expiry.  The device table holds subclients as int32 (the boundary already
+    # restricts them to [0, 2^31)), so a lease is 44 B, not the 48 B of an int64 column;
     # per resource config + offsets + outputs (64 B).  Re-reads are not counted.
-    return 48 * n_leases + 64 * n_resources
+    return LEASE_BYTES * n_leases + 64 * n_resources
 
 
 def kernel_units(eng, snap):

@@ -115,7 +115,7 @@ struct DevParams {
   // lease table (SoA).  out_* alias these in writeback mode, so no __restrict__.
   const double* wants;
   const double* has;
-  const int64_t* sub;
+  const int32_t* sub;   // subclients < 2^31 (checked at the boundary): 4 B per lease
   const int64_t* expiry;
   const ResCfg* cfg;
   const ResAgg* agg;  // running sums read by the tick (parity mode)
@@ -123,7 +123,7 @@ struct DevParams {
   double* out_gets;
   int64_t* out_expiry;
   double* out_wants;  // writeback only: released rows zeroed (else nullptr)
-  int64_t* out_sub;   // writeback only
+  int32_t* out_sub;   // writeback only
   ResAgg* res;        // per-resource results (== agg in writeback mode)
   int64_t now;
   int32_t recompute;

@@ -375,7 +375,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // wave-uniform bases + 32-bit per-lane offsets: one VGPR addresses every column
   const double* __restrict__ wb = p.wants + lo;
   const double* __restrict__ hb = p.has + lo;
-  const int64_t* __restrict__ sb = p.sub + lo;
+  const int32_t* __restrict__ sb = p.sub + lo;
   const int64_t* __restrict__ eb = p.expiry + lo;
   double* gb = p.out_gets + lo;
   int64_t* xb = p.out_expiry + lo;
@@ -395,7 +395,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
     w[k] = wb[u];
     h[k] = hb[u];
-    s[k] = (int)sb[u];
+    s[k] = sb[u];
     e[k] = eb[u];
     if (BATCH < R && (k + 1) % BATCH == 0 && k + 1 < R) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
@@ -590,7 +590,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     const int64_t row = row0 + (valid ? lane : nrows - 1);
     w = p.wants[row];
     h = p.has[row];
-    s = (int)p.sub[row];
+    s = p.sub[row];
     e = p.expiry[row];
   }
   // resource of this row: last k < nseg with rel[k] <= lane (offsets relative to row0)
@@ -834,7 +834,7 @@ struct ChunkRows {
 __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r) {
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;
-  const int64_t* __restrict__ sb = p.sub + ch.row0;
+  const int32_t* __restrict__ sb = p.sub + ch.row0;
   const int64_t* __restrict__ eb = p.expiry + ch.row0;
   r.valid = 0;
   r.live = 0;
@@ -846,7 +846,7 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
     r.w[k] = wb[u];
     r.h[k] = hb[u];
-    r.s[k] = (int)sb[u];
+    r.s[k] = sb[u];
     e[k] = eb[u];
   }
 #pragma unroll
@@ -863,7 +863,7 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
                                              ChunkRows& r, bool with_sub, bool with_has = false) {
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;
-  const int64_t* __restrict__ sb = p.sub + ch.row0;
+  const int32_t* __restrict__ sb = p.sub + ch.row0;
   r.valid = 0;
   r.live = P.live[(size_t)blockIdx.x * 256 + threadIdx.x];
 #pragma unroll
@@ -876,7 +876,7 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
       const unsigned u = (unsigned)i;
       r.w[k] = wb[u];
       if (with_has) r.h[k] = hb[u];
-      if (with_sub) r.s[k] = (int)sb[u];
+      if (with_sub) r.s[k] = sb[u];
       r.valid |= 1u << k;
     }
   }
@@ -1286,7 +1286,7 @@ __global__ void k_clear_rows(int64_t n, const int64_t* __restrict__ rows, int64_
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
                          const int64_t* __restrict__ expiry, const int64_t* __restrict__ seg_off, int64_t R,
-                         double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg,
+                         double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg,
                          const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || (*flags & kUpdReject)) return;
@@ -1296,7 +1296,7 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
   const long long ds = sub[i] - s_sub[r];
   s_has[r] = has[i];
   s_wants[r] = wants[i];
-  s_sub[r] = sub[i];
+  s_sub[r] = (int32_t)sub[i];  // in [0, 2^31) (k_check_rows)
   s_exp[r] = expiry[i];
   atomicAdd(&agg[seg].sum_has, dh);
   atomicAdd(&agg[seg].sum_wants, dw);
@@ -1304,7 +1304,7 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
 }
 
 __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int64_t* __restrict__ seg_off, int64_t R,
-                          double* s_has, double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg,
+                          double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg,
                          const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || (*flags & kUpdReject)) return;
@@ -1349,7 +1349,7 @@ __global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __
 // requests a resource only when its SumWants > 0 (server.go:241) and its band
 // must have num_clients >= 1 (server.go:863-866); other rows are released.
 __global__ void k_hier_root(int64_t R, int G, const double2* __restrict__ gathered, double* r_wants, double* r_has,
-                            int64_t* r_sub, int64_t* r_exp, int64_t now) {
+                            int32_t* r_sub, int64_t* r_exp, int64_t now) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R * G) return;
   const int64_t r = i / G;
@@ -1359,7 +1359,7 @@ __global__ void k_hier_root(int64_t R, int G, const double2* __restrict__ gather
   const long long count = __double_as_longlong(v.y);
   if (sum_wants > 0.0 && count >= 1) {
     r_wants[i] = sum_wants;  // GetServerCapacity: wantsTotal, subclientsTotal (:850-879)
-    r_sub[i] = count;
+    r_sub[i] = (int32_t)(count < INT32_MAX ? count : INT32_MAX);  // rows hold subclients < 2^31
     if (r_exp[i] == kReleased) r_has[i] = 0.0;  // a new lease has nothing yet
     r_exp[i] = now;  // refreshing now: live for this tick's Clean
   } else {
@@ -1448,7 +1448,7 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
-                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, seg_off, R, s_has,
                                                         s_wants, s_sub, s_exp, agg, flags);
@@ -1456,7 +1456,7 @@ hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, cons
 }
 
 hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
-                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
+                          double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, seg_off, R, s_has, s_wants, s_sub, s_exp, agg,
@@ -1490,7 +1490,7 @@ hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int64_t* r_sub,
+hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st) {
   if (R * G <= 0) return hipSuccess;
   k_hier_root<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, r_wants, r_has, r_sub,

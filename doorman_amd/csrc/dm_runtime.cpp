@@ -25,9 +25,9 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
                           hipStream_t st);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
-                         int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
-                          double* s_wants, int64_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
+                          double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
                           hipStream_t st);
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
                              const int64_t* sub, uint32_t* flags, hipStream_t st);
@@ -35,7 +35,7 @@ hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
-hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int64_t* r_sub,
+hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
                               hipStream_t st);
@@ -113,7 +113,8 @@ struct dm_ctx {
   // lease table
   DBuf<int64_t> seg_off;
   DBuf<double> wants, has;
-  DBuf<int64_t> sub, expiry;
+  DBuf<int32_t> sub;  // subclients, 4 B per lease on the device (the ABI carries int64)
+  DBuf<int64_t> expiry;
   // running sums (+ the last writeback tick's safe capacity), AoS
   DBuf<ResAgg> agg;
   // config, AoS
@@ -462,7 +463,12 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_HIP(c, upload(c->seg_off, s->seg_off, (size_t)R + 1, st), "upload seg_off");
   DM_HIP(c, upload(c->wants, s->wants, (size_t)N, st), "upload wants");
   DM_HIP(c, upload(c->has, s->has, (size_t)N, st), "upload has");
-  DM_HIP(c, upload(c->sub, s->subclients, (size_t)N, st), "upload subclients");
+  {
+    std::vector<int32_t> sub32((size_t)N);
+    for (int64_t i = 0; i < N; ++i) sub32[i] = (int32_t)s->subclients[i];  // range checked above
+    DM_HIP(c, upload(c->sub, sub32.data(), (size_t)N, st), "upload subclients");
+    DM_HIP(c, hipStreamSynchronize(st), "upload subclients");  // sub32 leaves scope
+  }
   DM_HIP(c, upload(c->expiry, s->expiry_ns, (size_t)N, st), "upload expiry");
   std::vector<int64_t> cnt;
   std::vector<double> sh, sw;
@@ -709,9 +715,11 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
   if (rc) return rc;
   DM_HIP(c, download(has, (const double*)c->has.p, off, n, c->stream), "read has");
   DM_HIP(c, download(wants, (const double*)c->wants.p, off, n, c->stream), "read wants");
-  DM_HIP(c, download(sub, (const int64_t*)c->sub.p, off, n, c->stream), "read sub");
+  std::vector<int32_t> sub32(sub ? (size_t)n : 0);
+  DM_HIP(c, download(sub ? sub32.data() : nullptr, (const int32_t*)c->sub.p, off, n, c->stream), "read sub");
   DM_HIP(c, download(exp, (const int64_t*)c->expiry.p, off, n, c->stream), "read expiry");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read store");
+  for (int64_t i = 0; sub && i < n; ++i) sub[i] = sub32[i];
   return DM_OK;
 }
 
