@@ -83,6 +83,15 @@ struct Partials {
 };
 constexpr int kSegTotBytes = 128;
 
+// row -> resource lookup for store updates: seg_off plus, for every block of
+// 2^kRowBlkShift rows, the resource holding its first row
+constexpr int kRowBlkShift = 12;
+struct RowIndex {
+  const int64_t* seg_off;
+  const int32_t* blk_seg;  // (N >> kRowBlkShift) + 2 entries
+  int64_t R;
+};
+
 // store-update validation flags (k_check_rows)
 constexpr uint32_t kUpdRange = 1u;   // row outside [0, N)
 constexpr uint32_t kUpdDup = 2u;     // row twice in one call

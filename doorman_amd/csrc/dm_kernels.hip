@@ -1228,11 +1228,17 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
 // store maintenance
 // --------------------------------------------------------------------------
 // Assign on existing rows (store.go:153-167): running sums += new - old.
-// Rows are applied in order by one thread per resource group? No: rows may hit
-// the same resource, so sums are accumulated with 64-bit atomics of the deltas.
-// resource owning row r: last s with seg_off[s] <= r (binary search, R+1 offsets)
-__device__ __forceinline__ int seg_of_row(const int64_t* __restrict__ seg_off, int64_t R, int64_t r) {
-  int64_t lo = 0, hi = R;  // invariant: seg_off[lo] <= r < seg_off[hi]
+// Rows of one call may hit the same resource, so the deltas reach the sums
+// through atomics — one per run of a resource within a wave (wave_seg_add).
+// resource owning row r: last s with seg_off[s] <= r.  A coarse index (the
+// resource holding the first row of every 2^kRowBlkShift-row block) narrows the
+// binary search to the few resources of r's block.
+__device__ __forceinline__ int seg_of_row(const RowIndex& ix, int64_t r) {
+  const int64_t* __restrict__ seg_off = ix.seg_off;
+  const int64_t b = r >> kRowBlkShift;
+  int64_t lo = ix.blk_seg[b];
+  int64_t hi = (int64_t)ix.blk_seg[b + 1] + 1;  // invariant: seg_off[lo] <= r < seg_off[hi]
+  if (hi > ix.R) hi = ix.R;
   while (hi - lo > 1) {
     const int64_t mid = (lo + hi) >> 1;
     if (seg_off[mid] <= r)
@@ -1241,6 +1247,40 @@ __device__ __forceinline__ int seg_of_row(const int64_t* __restrict__ seg_off, i
       hi = mid;
   }
   return (int)lo;
+}
+
+// Add per-row deltas to their resources' running sums: lanes of a wave that hit
+// the same resource are summed first (DPP) and add once; a wave whose rows spread
+// over many resources adds per lane.  Every lane of the wave must call this.
+__device__ __forceinline__ void wave_seg_add(ResAgg* agg, bool active, int seg, double dh, double dw, long long ds,
+                                             bool with_has, bool with_count) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long act = __ballot(active);
+  const int prev = __shfl(seg, lane > 0 ? lane - 1 : 0, 64);
+  const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != seg);
+  if (__popcll(__ballot(head)) > 8) {
+    if (active) {
+      if (with_has) atomicAdd(&agg[seg].sum_has, dh);
+      atomicAdd(&agg[seg].sum_wants, dw);
+      if (with_count) atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)ds);
+    }
+    return;
+  }
+  unsigned long long rem = act;
+  while (rem) {
+    const int h = __builtin_ctzll(rem);
+    const int s0 = __builtin_amdgcn_readlane(seg, h);
+    const unsigned long long m = __ballot(active && seg == s0) & rem;
+    const bool in = (m >> lane) & 1;
+    AggR v{in ? ds : 0, in ? dh : 0.0, in ? dw : 0.0};
+    v = wave_reduce(v, OpR());
+    if (lane == h) {
+      if (with_has) atomicAdd(&agg[s0].sum_has, v.h);
+      atomicAdd(&agg[s0].sum_wants, v.w);
+      if (with_count) atomicAdd((unsigned long long*)&agg[s0].count, (unsigned long long)v.cnt);
+    }
+    rem &= ~m;
+  }
 }
 
 // Validation of one store-update call on the device (no O(n) host pass): rows in
@@ -1285,52 +1325,66 @@ __global__ void k_clear_rows(int64_t n, const int64_t* __restrict__ rows, int64_
 
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
-                         const int64_t* __restrict__ expiry, const int64_t* __restrict__ seg_off, int64_t R,
-                         double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg,
-                         const uint32_t* flags) {
+                         const int64_t* __restrict__ expiry, RowIndex ix, double* s_has, double* s_wants,
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || (*flags & kUpdReject)) return;
-  const int64_t r = rows[i];
-  const int seg = seg_of_row(seg_off, R, r);
-  const double dh = has[i] - s_has[r], dw = wants[i] - s_wants[r];
-  const long long ds = sub[i] - s_sub[r];
-  s_has[r] = has[i];
-  s_wants[r] = wants[i];
-  s_sub[r] = (int32_t)sub[i];  // in [0, 2^31) (k_check_rows)
-  s_exp[r] = expiry[i];
-  atomicAdd(&agg[seg].sum_has, dh);
-  atomicAdd(&agg[seg].sum_wants, dw);
-  atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)ds);
+  if (*flags & kUpdReject) return;  // uniform over the grid
+  const bool active = i < n;
+  int seg = 0;
+  double dh = 0.0, dw = 0.0;
+  long long ds = 0;
+  if (active) {
+    const int64_t r = rows[i];
+    seg = seg_of_row(ix, r);
+    dh = has[i] - s_has[r];
+    dw = wants[i] - s_wants[r];
+    ds = sub[i] - s_sub[r];
+    s_has[r] = has[i];
+    s_wants[r] = wants[i];
+    s_sub[r] = (int32_t)sub[i];  // in [0, 2^31) (k_check_rows)
+    s_exp[r] = expiry[i];
+  }
+  wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
 
-__global__ void k_release(int64_t n, const int64_t* __restrict__ rows, const int64_t* __restrict__ seg_off, int64_t R,
-                          double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg,
-                         const uint32_t* flags) {
+__global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex ix, double* s_has, double* s_wants,
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || (*flags & kUpdReject)) return;
-  const int64_t r = rows[i];
-  const int seg = seg_of_row(seg_off, R, r);
-  atomicAdd(&agg[seg].sum_has, -s_has[r]);
-  atomicAdd(&agg[seg].sum_wants, -s_wants[r]);
-  atomicAdd((unsigned long long*)&agg[seg].count, (unsigned long long)(-s_sub[r]));
-  s_has[r] = 0.0;
-  s_wants[r] = 0.0;
-  s_sub[r] = 0;
-  s_exp[r] = kReleased;
+  if (*flags & kUpdReject) return;  // uniform over the grid
+  const bool active = i < n;
+  int seg = 0;
+  double dh = 0.0, dw = 0.0;
+  long long ds = 0;
+  if (active) {
+    const int64_t r = rows[i];
+    seg = seg_of_row(ix, r);
+    dh = -s_has[r];
+    dw = -s_wants[r];
+    ds = -(long long)s_sub[r];
+    s_has[r] = 0.0;
+    s_wants[r] = 0.0;
+    s_sub[r] = 0;
+    s_exp[r] = kReleased;
+  }
+  wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
 
 // Narrow Assign for a refresh that only changes wants (store.go:157):
 // sumWants += new - old.  Rows are unique within one call.
 __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ wants,
-                               const int64_t* __restrict__ seg_off, int64_t R, double* s_wants, ResAgg* agg,
-                               const uint32_t* flags) {
+                               RowIndex ix, double* s_wants, ResAgg* agg, const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || (*flags & kUpdReject)) return;
-  const int64_t r = rows[i];
-  const int seg = seg_of_row(seg_off, R, r);
-  const double d = wants[i] - s_wants[r];
-  s_wants[r] = wants[i];
-  atomicAdd(&agg[seg].sum_wants, d);
+  if (*flags & kUpdReject) return;  // uniform over the grid
+  const bool active = i < n;
+  int seg = 0;
+  double d = 0.0;
+  if (active) {
+    const int64_t r = rows[i];
+    seg = seg_of_row(ix, r);
+    d = wants[i] - s_wants[r];
+    s_wants[r] = wants[i];
+  }
+  wave_seg_add(agg, active, seg, 0.0, d, 0, false, false);
 }
 
 // server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
@@ -1447,27 +1501,25 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 }
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
-                         const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
+                         const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, seg_off, R, s_has,
-                                                        s_wants, s_sub, s_exp, agg, flags);
+  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, ix, s_has, s_wants, s_sub,
+                                                        s_exp, agg, flags);
   return hipGetLastError();
 }
 
-hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
-                          double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
-                          hipStream_t st) {
+hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, seg_off, R, s_has, s_wants, s_sub, s_exp, agg,
-                                                         flags);
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, ix, s_has, s_wants, s_sub, s_exp, agg, flags);
   return hipGetLastError();
 }
 
-hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
+hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, seg_off, R, s_wants, agg, flags);
+  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, ix, s_wants, agg, flags);
   return hipGetLastError();
 }
 

@@ -24,16 +24,15 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
                           hipStream_t st);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
-                         const int64_t* expiry, const int64_t* seg_off, int64_t R, double* s_has, double* s_wants,
+                         const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
-hipError_t launch_release(int64_t n, const int64_t* rows, const int64_t* seg_off, int64_t R, double* s_has,
-                          double* s_wants, int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags,
-                          hipStream_t st);
+hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
                              const int64_t* sub, uint32_t* flags, hipStream_t st);
 hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st);
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
-hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const int64_t* seg_off, int64_t R,
+hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
@@ -103,6 +102,7 @@ struct dm_ctx {
   static constexpr int kAux = 3;
   hipStream_t aux[kAux] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kAux] = {};
+  hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
   std::string err;
 
   int64_t R = 0, N = 0;
@@ -112,6 +112,8 @@ struct dm_ctx {
 
   // lease table
   DBuf<int64_t> seg_off;
+  DBuf<int32_t> blk_seg;  // RowIndex coarse index
+  RowIndex row_index() const { return RowIndex{seg_off.p, blk_seg.p, R}; }
   DBuf<double> wants, has;
   DBuf<int32_t> sub;  // subclients, 4 B per lease on the device (the ABI carries int64)
   DBuf<int64_t> expiry;
@@ -187,7 +189,7 @@ struct dm_ctx {
     pending.clear();
   }
   void free_all() {
-    seg_off.release(); wants.release(); has.release(); sub.release(); expiry.release();
+    seg_off.release(); blk_seg.release(); wants.release(); has.release(); sub.release(); expiry.release();
     agg.release(); cfg.release();
     out_gets.release(); out_expiry.release(); res.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
@@ -393,6 +395,7 @@ int dm_create(int device, dm_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
     dm_destroy(c);
@@ -417,6 +420,8 @@ void dm_destroy(dm_ctx* c) {
     if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
   }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  for (auto ev : c->ev_stage)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -461,6 +466,18 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   c->h_seg_off.assign(s->seg_off, s->seg_off + R + 1);
   hipStream_t st = c->stream;
   DM_HIP(c, upload(c->seg_off, s->seg_off, (size_t)R + 1, st), "upload seg_off");
+  {  // RowIndex: resource of the first row of every 2^kRowBlkShift-row block
+    const int64_t nb = (N >> kRowBlkShift) + 2;
+    std::vector<int32_t> blk((size_t)nb, 0);
+    int64_t sg = 0;
+    for (int64_t b = 0; b < nb && R > 0; ++b) {
+      const int64_t row = std::min<int64_t>(b << kRowBlkShift, std::max<int64_t>(N - 1, 0));
+      while (sg + 1 < R && s->seg_off[sg + 1] <= row) ++sg;
+      blk[(size_t)b] = (int32_t)sg;
+    }
+    DM_HIP(c, upload(c->blk_seg, blk.data(), blk.size(), st), "upload row index");
+    DM_HIP(c, hipStreamSynchronize(st), "upload row index");  // blk leaves scope
+  }
   DM_HIP(c, upload(c->wants, s->wants, (size_t)N, st), "upload wants");
   DM_HIP(c, upload(c->has, s->has, (size_t)N, st), "upload has");
   {
@@ -725,11 +742,18 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
 
 // Rows of one upsert/release call: in range and unique (a bitmap over the table,
 // O(n + N/64)); the resource of each row is found on the device.
-// Stage one update call's rows and validate them on the device (k_check_rows):
-// no O(n) host pass, so host buffers go to the GPU by DMA only (pinned buffers from
-// dm_host_alloc at full PCIe rate).  Returns the flags via finish_update().
-static int begin_update(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants_dev,
-                        const int64_t* sub_dev) {
+// The call's columns cross PCIe in chunks on an auxiliary stream while the
+// context stream validates the chunks already there (k_check_rows: no O(n) host
+// pass, so pinned buffers from dm_host_alloc go at full DMA rate).  The apply
+// kernel then runs on the context stream; finish_update() maps the flags.
+struct StageCol {
+  void* dst;
+  const void* src;
+  size_t elem;
+};
+static constexpr int64_t kStageChunk = 1 << 22;  // rows per copy/validate step
+
+static int staged_check(dm_ctx* c, int64_t n, const StageCol* cols, int ncols, bool check_wants, bool check_sub) {
   if (!c->row_bits.p || c->row_bits.n < (size_t)(c->N / 32 + 1)) {
     DM_HIP(c, c->row_bits.ensure((size_t)(c->N / 32 + 1)), "row bitmap");
     DM_HIP(c, hipMemsetAsync(c->row_bits.p, 0, c->row_bits.n * sizeof(uint32_t), c->stream), "row bitmap");
@@ -739,9 +763,25 @@ static int begin_update(dm_ctx* c, int64_t n, const int64_t* rows, const double*
     DM_HIP(c, hipHostMalloc((void**)&c->h_flags, sizeof(uint32_t), hipHostMallocDefault), "update flags");
   }
   DM_HIP(c, hipMemsetAsync(c->upd_flags.p, 0, sizeof(uint32_t), c->stream), "update flags");
-  (void)rows;
-  DM_HIP(c, launch_check_rows(n, c->st_rows.p, c->N, c->row_bits.p, wants_dev, sub_dev, c->upd_flags.p, c->stream),
-         "check rows");
+  // the copy stream may overwrite staging only after earlier work on it is done
+  hipStream_t cp = c->aux[0];
+  DM_HIP(c, hipEventRecord(c->ev_fork, c->stream), "stage order");
+  DM_HIP(c, hipStreamWaitEvent(cp, c->ev_fork, 0), "stage order");
+  int k = 0;
+  for (int64_t off = 0; off < n; off += kStageChunk, ++k) {
+    const int64_t m = std::min(kStageChunk, n - off);
+    for (int j = 0; j < ncols; ++j)
+      DM_HIP(c,
+             hipMemcpyAsync((char*)cols[j].dst + off * cols[j].elem, (const char*)cols[j].src + off * cols[j].elem,
+                            (size_t)m * cols[j].elem, hipMemcpyHostToDevice, cp),
+             "stage update");
+    hipEvent_t ev = c->ev_stage[k & 1];
+    DM_HIP(c, hipEventRecord(ev, cp), "stage update");
+    DM_HIP(c, hipStreamWaitEvent(c->stream, ev, 0), "stage update");
+    DM_HIP(c, launch_check_rows(m, c->st_rows.p + off, c->N, c->row_bits.p, check_wants ? c->st_wants.p + off : nullptr,
+                                check_sub ? c->st_sub.p + off : nullptr, c->upd_flags.p, c->stream),
+           "check rows");
+  }
   return DM_OK;
 }
 
@@ -766,14 +806,16 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
-  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
-  DM_HIP(c, upload(c->st_has, has, (size_t)n, c->stream), "stage has");
-  DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
-  DM_HIP(c, upload(c->st_sub, sub, (size_t)n, c->stream), "stage sub");
-  DM_HIP(c, upload(c->st_exp, exp, (size_t)n, c->stream), "stage expiry");
-  int rc = begin_update(c, n, rows, c->st_wants.p, c->st_sub.p);
+  DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
+  DM_HIP(c, c->st_has.ensure((size_t)n), "stage has");
+  DM_HIP(c, c->st_wants.ensure((size_t)n), "stage wants");
+  DM_HIP(c, c->st_sub.ensure((size_t)n), "stage sub");
+  DM_HIP(c, c->st_exp.ensure((size_t)n), "stage expiry");
+  const StageCol cols[] = {{c->st_rows.p, rows, 8}, {c->st_wants.p, wants, 8}, {c->st_sub.p, sub, 8},
+                           {c->st_has.p, has, 8}, {c->st_exp.p, exp, 8}};
+  int rc = staged_check(c, n, cols, 5, true, true);
   if (rc) return rc;
-  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->seg_off.p, c->R,
+  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->row_index(),
                           c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->upd_flags.p, c->stream),
          "upsert");
   uint32_t f = 0;
@@ -791,11 +833,12 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
-  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
-  DM_HIP(c, upload(c->st_wants, wants, (size_t)n, c->stream), "stage wants");
-  int rc = begin_update(c, n, rows, c->st_wants.p, nullptr);
+  DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
+  DM_HIP(c, c->st_wants.ensure((size_t)n), "stage wants");
+  const StageCol cols[] = {{c->st_rows.p, rows, 8}, {c->st_wants.p, wants, 8}};
+  int rc = staged_check(c, n, cols, 2, true, false);
   if (rc) return rc;
-  DM_HIP(c, launch_update_wants(n, c->st_rows.p, c->st_wants.p, c->seg_off.p, c->R, c->wants.p, c->agg.p,
+  DM_HIP(c, launch_update_wants(n, c->st_rows.p, c->st_wants.p, c->row_index(), c->wants.p, c->agg.p,
                                 c->upd_flags.p, c->stream),
          "update wants");
   uint32_t f = 0;
@@ -811,10 +854,11 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
-  DM_HIP(c, upload(c->st_rows, rows, (size_t)n, c->stream), "stage rows");
-  int rc = begin_update(c, n, rows, nullptr, nullptr);
+  DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
+  const StageCol cols[] = {{c->st_rows.p, rows, 8}};
+  int rc = staged_check(c, n, cols, 1, false, false);
   if (rc) return rc;
-  DM_HIP(c, launch_release(n, c->st_rows.p, c->seg_off.p, c->R, c->has.p, c->wants.p, c->sub.p, c->expiry.p,
+  DM_HIP(c, launch_release(n, c->st_rows.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p,
                            c->agg.p, c->upd_flags.p, c->stream),
          "release");
   uint32_t f = 0;
