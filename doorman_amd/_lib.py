@@ -89,6 +89,24 @@ _SIGS = {
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_plan_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
+    "dm_read_leases_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    # round-oriented GetCapacity dispatch (dm_server.cpp)
+    "dm_server_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p),
+                                        ctypes.POINTER(ResourceCfg), ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "dm_server_destroy": (None, [ctypes.c_void_p]),
+    "dm_server_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "dm_server_get_capacity": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double,
+                                              ctypes.c_double, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "dm_server_release_capacity": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]),
+    "dm_server_tick": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "dm_server_lease": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                       ctypes.POINTER(ctypes.c_double)]),
+    "dm_server_resource": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_double)]),
+    "dm_server_ctx": (ctypes.c_void_p, [ctypes.c_void_p]),
 }
 
 

@@ -1387,6 +1387,16 @@ __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, cons
   wave_seg_add(agg, active, seg, 0.0, d, 0, false, false);
 }
 
+// gets / expiry of scattered rows (dm_read_leases_rows)
+__global__ void k_gather_leases(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ gets,
+                                const int64_t* __restrict__ expiry, double* out_gets, int64_t* out_exp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  out_gets[i] = gets[r];
+  out_exp[i] = expiry[r];
+}
+
 // server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
 __global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __restrict__ dst) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1520,6 +1530,13 @@ hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wan
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, ix, s_wants, agg, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_leases(int64_t n, const int64_t* rows, const double* gets, const int64_t* expiry,
+                               double* out_gets, int64_t* out_exp, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_gather_leases<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, gets, expiry, out_gets, out_exp);
   return hipGetLastError();
 }
 

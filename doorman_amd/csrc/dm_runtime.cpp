@@ -31,6 +31,8 @@ hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, do
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
                              const int64_t* sub, uint32_t* flags, hipStream_t st);
 hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st);
+hipError_t launch_gather_leases(int64_t n, const int64_t* rows, const double* gets, const int64_t* expiry,
+                               double* out_gets, int64_t* out_exp, hipStream_t st);
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
@@ -673,6 +675,26 @@ int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* exp
   const int64_t* e = c->last_writeback ? c->expiry.p : c->out_expiry.p;
   DM_HIP(c, download(gets, g, off, n, c->stream), "read gets");
   DM_HIP(c, download(expiry_ns, e, off, n, c->stream), "read expiry");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
+  return DM_OK;
+}
+
+int dm_read_leases_rows(dm_ctx* c, int64_t n, const int64_t* rows, double* gets, int64_t* expiry_ns) {
+  DM_CHECK_CTX(c);
+  if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
+  if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad rows");
+  if (n == 0) return DM_OK;
+  for (int64_t i = 0; i < n; ++i)
+    if (rows[i] < 0 || rows[i] >= c->N) return c->fail(DM_E_RANGE, "row out of range");
+  const double* g = c->last_writeback ? c->has.p : c->out_gets.p;
+  const int64_t* e = c->last_writeback ? c->expiry.p : c->out_expiry.p;
+  DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
+  DM_HIP(c, c->st_has.ensure((size_t)n), "stage gets");
+  DM_HIP(c, c->st_exp.ensure((size_t)n), "stage expiry");
+  DM_HIP(c, hipMemcpyAsync(c->st_rows.p, rows, (size_t)n * 8, hipMemcpyHostToDevice, c->stream), "stage rows");
+  DM_HIP(c, launch_gather_leases(n, c->st_rows.p, g, e, c->st_has.p, c->st_exp.p, c->stream), "gather leases");
+  DM_HIP(c, download(gets, (const double*)c->st_has.p, 0, n, c->stream), "read gets");
+  DM_HIP(c, download(expiry_ns, (const int64_t*)c->st_exp.p, 0, n, c->stream), "read expiry");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
   return DM_OK;
 }

@@ -138,6 +138,8 @@ int dm_apportion(dm_ctx* ctx, int64_t now_ns, uint32_t flags);
 /* lease outputs of the last dm_apportion: gets (Lease.Has), expiry in unix ns
  * (DM_RELEASED for released rows); any pointer may be NULL */
 int dm_read_leases(dm_ctx* ctx, int64_t off, int64_t n, double* gets, int64_t* expiry_ns);
+/* the same for n scattered rows (gathered on the device) */
+int dm_read_leases_rows(dm_ctx* ctx, int64_t n, const int64_t* rows, double* gets, int64_t* expiry_ns);
 /* proto form (server.go:787-791): capacity, expiry_time = Expiry.Unix(), refresh_interval seconds */
 int dm_read_leases_proto(dm_ctx* ctx, int64_t off, int64_t n, double* capacity, int64_t* expiry_time_s,
                          int64_t* refresh_interval_s);
@@ -175,6 +177,55 @@ int dm_reset_kernel_times(dm_ctx* ctx);
 /* plan summary of the loaded store: counts per dispatch bin (small packs, 64x1,
  * 256x1..256x16, large chunks) */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
+
+/* ---- round-oriented GetCapacity dispatch (dm_server.cpp) ----
+ *
+ * The request path of the reference server over a device-resident store:
+ *
+ *   Server.GetCapacity      go/server/doorman/server.go:730-796  -> dm_server_get_capacity + dm_server_tick
+ *   Server.getCapacity      go/server/doorman/server.go:798-817  -> dm_server_tick (one batch per round)
+ *   Server.ReleaseCapacity  go/server/doorman/server.go:668-714  -> dm_server_release_capacity
+ *   Resource.Decide         go/server/doorman/resource.go:100-113 -> Clean + Learn/Algorithm in the tick
+ *   LeaseStore (client-id)  go/server/doorman/store.go:68-167     -> client -> row map over the columnar store
+ *   SetSafeCapacity         go/server/doorman/resource.go:81-96   -> dm_server_lease(.safe_capacity)
+ *
+ * Requests queued during a round are decided together by dm_server_tick: the
+ * store first drops expired leases (Clean, store.go:169-181) and released
+ * clients (store.go:142-151), then holds every requesting client's row as its
+ * request (wants, subclients; has = the lease the server assigned, or the
+ * client-reported has in learning mode, algorithm.go:297-302), the tick decides
+ * the requesting clients against that one snapshot, and their leases are
+ * assigned (store.go:153-167).  Clients that did not ask keep their leases, which
+ * expire unless refreshed.  Resources are configured up front (the outcome of
+ * the reference's LoadConfig; config parsing and glob matching stay there);
+ * every resource's segment of the table grows when it runs out of free rows. */
+typedef struct dm_server dm_server;
+
+/* resource_ids: R NUL-terminated ids; cfg: their configuration (dm_config_load);
+ * slots: initial rows per resource (grown on demand) */
+int dm_server_create(int device, int64_t n_resources, const char* const* resource_ids, const dm_resource_cfg* cfg,
+                     int64_t slots, dm_server** out);
+void dm_server_destroy(dm_server* srv);
+const char* dm_server_last_error(dm_server* srv);
+/* queue one ResourceRequest of a GetCapacity (subclients = 1 there, >= 1 for a
+ * server band, server.go:863-866: DM_E_ARGUMENT otherwise); *ticket indexes the
+ * next dm_server_tick's leases; an unknown resource is DM_E_RANGE */
+int dm_server_get_capacity(dm_server* srv, const char* client, const char* resource, double has, double wants,
+                           int64_t subclients, int64_t* ticket);
+/* queue a ReleaseCapacity of one client's lease on one resource */
+int dm_server_release_capacity(dm_server* srv, const char* client, const char* resource);
+/* decide every queued request at time now_ns (one batch) */
+int dm_server_tick(dm_server* srv, int64_t now_ns);
+/* the lease of a ticket of the last tick, as GetCapacity returns it
+ * (server.go:783-796): capacity, expiry_time (unix s), refresh_interval (s),
+ * and the resource's safe capacity (resource.go:81-96) */
+int dm_server_lease(dm_server* srv, int64_t ticket, double* capacity, int64_t* expiry_time_s,
+                    int64_t* refresh_interval_s, double* safe_capacity);
+/* store state: number of clients holding a lease on a resource, and its running sums */
+int dm_server_resource(dm_server* srv, const char* resource, int64_t* clients, int64_t* count, double* sum_has,
+                       double* sum_wants);
+/* the underlying context (profiling, dm_read_*) */
+dm_ctx* dm_server_ctx(dm_server* srv);
 
 #ifdef __cplusplus
 }
