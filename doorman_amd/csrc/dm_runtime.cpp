@@ -785,10 +785,11 @@ static int staged_check(dm_ctx* c, int64_t n, const StageCol* cols, int ncols, b
     DM_HIP(c, hipHostMalloc((void**)&c->h_flags, sizeof(uint32_t), hipHostMallocDefault), "update flags");
   }
   DM_HIP(c, hipMemsetAsync(c->upd_flags.p, 0, sizeof(uint32_t), c->stream), "update flags");
-  // the copy stream may overwrite staging only after earlier work on it is done
+  // Every call that reads the staging buffers (updates, dm_read_leases_rows) waits
+  // for its kernels before it returns, so the copies need not wait for the context
+  // stream: they overlap whatever is still running there (e.g. an asynchronous
+  // tick), and each chunk's validation is ordered after that work and its copy.
   hipStream_t cp = c->aux[0];
-  DM_HIP(c, hipEventRecord(c->ev_fork, c->stream), "stage order");
-  DM_HIP(c, hipStreamWaitEvent(cp, c->ev_fork, 0), "stage order");
   int k = 0;
   for (int64_t off = 0; off < n; off += kStageChunk, ++k) {
     const int64_t m = std::min(kStageChunk, n - off);
