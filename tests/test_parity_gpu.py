@@ -254,6 +254,77 @@ def test_c2_zipf_full_size_sampled(eng):
     _sample_check(eng, snap, sample, "C2")
 
 
+def test_c3_full_size_sampled_and_checksum(eng):
+    """configs[3] size on one GPU: 100M leases (4.4 GB table, the HBM-streaming load
+    batching), FS/PS mixed with 1% expired rows.  Sampled resources against the
+    oracle, and over all 100k resources a size-independent property: after a
+    writeback tick each resource's sumHas equals the sum of its live leases' gets."""
+    snap = W.uniform(100_000, 1_000, kind="mixed", seed=33, expired_frac=0.01)
+    eng.load(snap)
+    eng.apportion(NOW)
+    rng = np.random.default_rng(7)
+    _sample_check(eng, snap, np.sort(rng.choice(100_000, 24, replace=False)), "C3")
+    eng.apportion(NOW, writeback=True)
+    gets, exp = eng.leases()
+    res = eng.resources(safe=False)
+    live = exp != W.RELEASED
+    per_res = np.add.reduceat(np.where(live, gets, 0.0), snap["seg_off"][:-1])
+    np.testing.assert_allclose(res["sum_has"], per_res, rtol=0, atol=1e-9 * 1000.0)
+    np.testing.assert_array_equal(res["count"], np.add.reduceat(live.astype(np.int64), snap["seg_off"][:-1]))
+    del snap, gets, exp
+
+
+def test_streaming_rounds_match_oracle(eng):
+    """configs[4]'s loop at small size: per 5 s round, 10% wants updates, 1% departures,
+    new clients into free rows, then a writeback tick (with Clean of leases that
+    expired).  A host copy of the store receives the same updates and the tick's
+    writeback; the oracle decides it each round from exact sums while the device
+    uses its running sums."""
+    rng = np.random.default_rng(44)
+    snap = W.uniform(3000, 500, kind="mixed", seed=44)
+    N = len(snap["wants"])
+    free = rng.random(N) < 0.05
+    snap["wants"][free] = 0.0
+    snap["has"][free] = 0.0
+    snap["subclients"] = np.where(free, 0, 1).astype(np.int64)
+    snap["expiry_ns"][free] = W.RELEASED
+    W.add_store_sums(snap)
+    eng.load(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    now = NOW
+    for rnd in range(6):
+        now += 5 * W.NS
+        alive = np.flatnonzero(host["expiry_ns"] != W.RELEASED)
+        upd = np.sort(rng.choice(alive, len(alive) // 10, replace=False))
+        w = rng.uniform(0.5, 1.5, len(upd)) * 2.0
+        eng.update_wants(upd, w)
+        host["wants"][upd] = w
+        rest = np.setdiff1d(alive, upd)
+        gone = np.sort(rng.choice(rest, len(alive) // 100, replace=False))
+        eng.release(gone)
+        for k, v in (("wants", 0.0), ("has", 0.0), ("subclients", 0), ("expiry_ns", W.RELEASED)):
+            host[k][gone] = v
+        pool = np.flatnonzero(host["expiry_ns"] == W.RELEASED)
+        new = np.sort(rng.choice(pool, min(len(pool), len(gone)), replace=False))
+        nw = rng.uniform(0.5, 1.5, len(new))
+        ne = np.full(len(new), now + 600 * W.NS)
+        eng.upsert(new, np.zeros(len(new)), nw, np.ones(len(new), np.int64), ne)
+        host["wants"][new], host["has"][new], host["subclients"][new], host["expiry_ns"][new] = nw, 0.0, 1, ne
+        W.add_store_sums(host)
+        eng.apportion(now, writeback=True)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now)
+        assert_leases_match(host, gets, exp, ref, f"round {rnd}")
+        live = ref["expiry_ns"] != W.RELEASED  # the tick's writeback, on the host copy
+        host["has"] = np.where(live, ref["gets"], 0.0)
+        host["wants"] = np.where(live, host["wants"], 0.0)
+        host["subclients"] = np.where(live, host["subclients"], 0)
+        host["expiry_ns"] = ref["expiry_ns"].copy()
+    store = eng.read_store()
+    np.testing.assert_array_equal(store["subclients"], host["subclients"])
+    np.testing.assert_array_equal(store["expiry_ns"], host["expiry_ns"])
+
+
 @pytest.mark.parametrize("case", [c for c in KATS["server"] if "error" not in c], ids=lambda c: c["name"])
 def test_server_kats_through_the_abi(eng, case):
     """server_test.go:339-553 (learning mode 20/90/100, learning persists across
