@@ -839,7 +839,7 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   r.valid = 0;
   r.live = 0;
   int64_t e[kLR];
-  // all loads in flight before the first is consumed (see group_segment)
+  // loads issued before any is consumed (see group_segment)
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
@@ -848,6 +848,9 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     r.h[k] = hb[u];
     r.s[k] = sb[u];
     e[k] = eb[u];
+    // two round trips of half the rows: with all 32 loads per lane in flight the
+    // vector-memory pipe backs up (64 % of wave time issue-stalled); C2 -3 %
+    if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
