@@ -154,9 +154,12 @@ class Engine:
         return out
 
     # -- the batch algorithm --
-    def apportion(self, now_ns: int, writeback: bool = False, recompute: bool = False, asynchronous: bool = False):
+    def apportion(self, now_ns: int, writeback: bool = False, recompute: bool = False, asynchronous: bool = False,
+                  wb_columns: str = "auto"):
+        """wb_columns: "auto", "inplace" or "alternate" (DM_WB_INPLACE / DM_WB_ALTERNATE)."""
         flags = ((_lib.DM_WRITEBACK if writeback else 0) | (_lib.DM_AGG_RECOMPUTE if recompute else 0)
-                 | (_lib.DM_ASYNC if asynchronous else 0))
+                 | (_lib.DM_ASYNC if asynchronous else 0)
+                 | {"auto": 0, "inplace": _lib.DM_WB_INPLACE, "alternate": _lib.DM_WB_ALTERNATE}[wb_columns])
         self._chk(self._L.dm_apportion(self._ctx, int(now_ns), flags))
 
     def leases(self, off: int = 0, n: int | None = None):

@@ -64,6 +64,11 @@ extern "C" {
                                running sums updated as the Assigns would (store.go:153-167) */
 #define DM_AGG_RECOMPUTE 2u /* ignore the store's running sums; recompute them from the rows */
 #define DM_ASYNC 4u         /* enqueue on the context stream and return without waiting */
+/* Where a writeback tick writes gets/expiry.  Default: in place for a store that
+   fits the Infinity Cache, else into a second pair of has/expiry columns that
+   becomes the store's after the tick (faster streaming; 16 B per lease of HBM). */
+#define DM_WB_INPLACE 8u    /* force in-place writeback */
+#define DM_WB_ALTERNATE 16u /* force the alternate columns */
 
 typedef struct dm_ctx dm_ctx;
 

@@ -127,15 +127,17 @@ def test_deterministic(eng):
     assert r1["sum_has"].tobytes() == r2["sum_has"].tobytes()
 
 
-def test_writeback_updates_store_like_assign(eng):
+@pytest.mark.parametrize("cols", ["auto", "inplace", "alternate"])
+def test_writeback_updates_store_like_assign(eng, cols):
     """DM_WRITEBACK: has := gets, expiry := now + lease, released rows zeroed and
     the running sums updated (store.go:142-167); a second tick on the written-back
-    store matches the oracle on that store."""
+    store matches the oracle on that store.  Both column modes (in place, and the
+    alternate has/expiry pair that becomes the store's)."""
     rng = np.random.default_rng(11)
     snap = snapshot_with_sizes(rng, binned_sizes(rng), expired_frac=0.1)
     ref = O.apportion(snap, NOW)
     eng.load(snap)
-    eng.apportion(NOW, writeback=True)
+    eng.apportion(NOW, writeback=True, wb_columns=cols)
     st = eng.read_store()
     live = ref["expiry_ns"] != W.RELEASED
     assert float_close(st["has"], np.where(live, ref["gets"], 0.0), np.repeat(snap["capacity"],
@@ -274,7 +276,8 @@ def test_c3_full_size_sampled_and_checksum(eng):
     del snap, gets, exp
 
 
-def test_streaming_rounds_match_oracle(eng):
+@pytest.mark.parametrize("cols", ["inplace", "alternate"])
+def test_streaming_rounds_match_oracle(eng, cols):
     """configs[4]'s loop at small size: per 5 s round, 10% wants updates, 1% departures,
     new clients into free rows, then a writeback tick (with Clean of leases that
     expired).  A host copy of the store receives the same updates and the tick's
@@ -311,7 +314,7 @@ def test_streaming_rounds_match_oracle(eng):
         eng.upsert(new, np.zeros(len(new)), nw, np.ones(len(new), np.int64), ne)
         host["wants"][new], host["has"][new], host["subclients"][new], host["expiry_ns"][new] = nw, 0.0, 1, ne
         W.add_store_sums(host)
-        eng.apportion(now, writeback=True)
+        eng.apportion(now, writeback=True, wb_columns=cols)
         gets, exp = eng.leases()
         ref = O.apportion(host, now)
         assert_leases_match(host, gets, exp, ref, f"round {rnd}")
