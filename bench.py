@@ -247,7 +247,8 @@ def main():
         if world > 1:
             dist.barrier()
 
-    step = lambda: eng.apportion(now, writeback=True, asynchronous=True)  # noqa: E731
+    # back-to-back ticks: a forked tick's class streams join lazily (DM_DEFER_JOIN)
+    step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
     root = None
     if args.workload == "c4":
         step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup)
@@ -299,6 +300,7 @@ def main():
     ev0.record(ext)
     for _ in range(args.steps):
         step()
+    eng.join()  # every class stream's work before the closing event
     ev1.record(ext)
     eng.sync()
     torch.cuda.synchronize()

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libdoorman_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "doorman_hip.h")
 
 DM_OK, DM_E_INVAL, DM_E_HIP, DM_E_STATE, DM_E_KIND, DM_E_RANGE, DM_E_ARGUMENT = 0, -1, -2, -3, -4, -5, -6
-DM_WRITEBACK, DM_AGG_RECOMPUTE, DM_ASYNC, DM_WB_INPLACE, DM_WB_ALTERNATE = 1, 2, 4, 8, 16
+DM_WRITEBACK, DM_AGG_RECOMPUTE, DM_ASYNC, DM_WB_INPLACE, DM_WB_ALTERNATE, DM_DEFER_JOIN = 1, 2, 4, 8, 16, 32
 
 
 class DmError(RuntimeError):
@@ -67,6 +67,7 @@ _SIGS = {
     "dm_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dm_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "dm_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "dm_join": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_store_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Snapshot)]),
     "dm_config_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ResourceCfg)]),
     "dm_store_upsert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5),
@@ -116,9 +117,13 @@ def header_symbols() -> list[str]:
     return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(dm_\w+)\s*\(", text, flags=re.M)))
 
 
-def _bind(path):
+def _bind(path, strict=True):
+    """strict: every entry point must exist (the in-tree build); an A/B variant built
+    from an older tree may lack newer ones."""
     L = ctypes.CDLL(path)  # RTLD_LOCAL: several builds can coexist in one process (A/B runs)
     for name, (res, args) in _SIGS.items():
+        if not strict and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -131,7 +136,7 @@ def lib(path: str | None = None):
     global _lib
     if path is not None and os.path.abspath(path) != LIB_PATH:
         if path not in _variants:
-            _variants[path] = _bind(path)
+            _variants[path] = _bind(path, strict=False)
         return _variants[path]
     if _lib is None:
         if not os.path.exists(LIB_PATH):

@@ -103,6 +103,7 @@ struct dm_ctx {
   // auxiliary streams: independent size bins of one tick run concurrently
   static constexpr int kAux = 3;
   hipStream_t aux[kAux] = {};
+  hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
   hipEvent_t ev_fork = nullptr, ev_join[kAux] = {};
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
   std::string err;
@@ -128,6 +129,24 @@ struct dm_ctx {
   DBuf<int64_t> out_expiry;
   DBuf<ResAgg> res;
   bool last_writeback = false, have_result = false;
+  // A forked tick's work classes run on the auxiliary streams.  Normally they are
+  // joined back into the context stream at the end of the tick; with DM_DEFER_JOIN
+  // the join waits for the next library call that needs it (each cross-queue hop
+  // costs ~20 us on the GPU, so back-to-back ticks keep every class streaming).
+  // aux_pending: class work not yet joined into the context stream.
+  // main_dirty: the context stream holds work the auxiliary streams have not
+  // waited for (the next fork must record an event).
+  bool aux_pending = false, main_dirty = true;
+  hipError_t join_aux() {
+    if (!aux_pending) return hipSuccess;
+    aux_pending = false;
+    for (int i = 0; i < kAux; ++i) {
+      hipError_t e = hipEventRecord(ev_join[i], aux[i]);
+      if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join[i], 0);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   // plan
   std::vector<Pack> h_packs;
   std::vector<WorkItem> h_bins[kNumBins];
@@ -219,6 +238,16 @@ struct dm_ctx {
       return DM_E_INVAL;                                    \
     }                                                       \
     DM_HIP(ctx, hipSetDevice((ctx)->device), "hipSetDevice"); \
+  } while (0)
+
+// Entry of every call that puts work on the context stream: join the auxiliary
+// streams' deferred tick work first (DM_DEFER_JOIN), and remember that the
+// context stream now holds work the next fork must order.
+#define DM_ENTER(ctx)                                         \
+  do {                                                        \
+    DM_CHECK_CTX(ctx);                                        \
+    DM_HIP(ctx, (ctx)->join_aux(), "join auxiliary streams"); \
+    (ctx)->main_dirty = true;                                 \
   } while (0)
 
 template <typename T>
@@ -396,6 +425,7 @@ int dm_create(int device, dm_ctx** out) {
     e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
   }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -421,6 +451,10 @@ void dm_destroy(dm_ctx* c) {
     }
     if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
   }
+  if (c->cpy) {
+    (void)hipStreamSynchronize(c->cpy);
+    (void)hipStreamDestroy(c->cpy);
+  }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
@@ -431,23 +465,29 @@ void dm_destroy(dm_ctx* c) {
 const char* dm_last_error(dm_ctx* c) { return c ? c->err.c_str() : g_last_error.c_str(); }
 
 int dm_set_stream(dm_ctx* c, void* s) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   c->stream = s ? (hipStream_t)s : c->own_stream;
+  c->main_dirty = true;
   return DM_OK;
 }
 
 void* dm_get_stream(dm_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+int dm_join(dm_ctx* c) {
+  DM_ENTER(c);
+  return DM_OK;
+}
+
 int dm_sync(dm_ctx* c) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   c->collect_profile();
   return DM_OK;
 }
 
 int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!s || s->n_resources < 0 || s->n_leases < 0 || !s->seg_off) return c->fail(DM_E_INVAL, "bad snapshot");
   const int64_t R = s->n_resources, N = s->n_leases;
   if (R > INT32_MAX - 1) return c->fail(DM_E_INVAL, "too many resources for one context (max 2^31-2)");
@@ -527,7 +567,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
 }
 
 int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!cfg || R < 0 || !cfg->kind || !cfg->capacity || !cfg->lease_length_s || !cfg->refresh_interval_s ||
       !cfg->learning_end_ns || !cfg->parent_expiry_ns || !cfg->safe_capacity)
     return c->fail(DM_E_INVAL, "bad config");
@@ -624,7 +664,11 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   const int nch = (int)c->h_chunks.size(), nls = (int)c->h_large.size();
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
-  if (c->maybe_general) DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
+  const bool general = c->maybe_general && c->n_nonsmall > 0;
+  if (c->maybe_general) {
+    DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
+    c->main_dirty = true;
+  }
   // Independent work classes: large resources (a 5-kernel chain), big groups,
   // small groups + packed.  With more than one class present they run on the
   // auxiliary streams concurrently, forked from and joined back to the main stream.
@@ -635,9 +679,13 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   const int classes = (nch > 0) + (big_bins > 0) + has_small;
   const bool fork = classes > 1;
   hipStream_t s_large = fork ? c->aux[0] : st, s_big = fork ? c->aux[1] : st, s_small = fork ? c->aux[2] : st;
-  if (fork) {
+  if (!fork) {  // everything on the context stream, after any deferred class work
+    DM_HIP(c, c->join_aux(), "join");
+    c->main_dirty = true;
+  } else if (c->main_dirty) {  // class streams wait for what the context stream holds
     DM_HIP(c, hipEventRecord(c->ev_fork, st), "fork");
     for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork");
+    c->main_dirty = false;
   }
   for (int ph = 0; ph < 5 && nch > 0; ++ph)
     DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
@@ -657,14 +705,15 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), s_small); }),
            "small kernel");
   if (fork) {
-    for (int i = 0; i < dm_ctx::kAux; ++i) {
-      DM_HIP(c, hipEventRecord(c->ev_join[i], c->aux[i]), "join");
-      DM_HIP(c, hipStreamWaitEvent(st, c->ev_join[i], 0), "join");
-    }
+    c->aux_pending = true;
+    // k_general consumes every class's worklist appends on the context stream
+    const bool defer = (flags & DM_ASYNC) && (flags & DM_DEFER_JOIN) && !general;
+    if (!defer) DM_HIP(c, c->join_aux(), "join");
   }
-  if (c->maybe_general && c->n_nonsmall > 0) {
+  if (general) {
     const int blocks = (int)std::min<int64_t>(c->n_nonsmall, 1024);
     DM_HIP(c, timed(KC_GENERAL, st, [&] { return launch_general(p, gl, gc, blocks, st); }), "general kernel");
+    c->main_dirty = true;
   }
   if (pingpong) {  // the written columns become the store's (stream order keeps later work correct)
     std::swap(c->has, c->out_gets);
@@ -685,7 +734,7 @@ static int check_range(dm_ctx* c, int64_t off, int64_t n, int64_t total) {
 }
 
 int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* expiry_ns) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
@@ -698,7 +747,7 @@ int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* exp
 }
 
 int dm_read_leases_rows(dm_ctx* c, int64_t n, const int64_t* rows, double* gets, int64_t* expiry_ns) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad rows");
   if (n == 0) return DM_OK;
@@ -748,7 +797,7 @@ int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, in
 
 int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* sum_has, double* sum_wants,
                       double* safe) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   int rc = check_range(c, r0, n, c->R);
   if (rc) return rc;
   if (safe && !c->have_result) return c->fail(DM_E_STATE, "safe capacity needs a dm_apportion result");
@@ -766,7 +815,7 @@ int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* 
 }
 
 int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants, int64_t* sub, int64_t* exp) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
@@ -807,7 +856,7 @@ static int staged_check(dm_ctx* c, int64_t n, const StageCol* cols, int ncols, b
   // for its kernels before it returns, so the copies need not wait for the context
   // stream: they overlap whatever is still running there (e.g. an asynchronous
   // tick), and each chunk's validation is ordered after that work and its copy.
-  hipStream_t cp = c->aux[0];
+  hipStream_t cp = c->cpy;
   int k = 0;
   for (int64_t off = 0; off < n; off += kStageChunk, ++k) {
     const int64_t m = std::min(kStageChunk, n - off);
@@ -843,7 +892,7 @@ static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
 
 int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has, const double* wants,
                     const int64_t* sub, const int64_t* exp) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
@@ -870,7 +919,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
 }
 
 int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
@@ -891,7 +940,7 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
 }
 
 int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
@@ -943,7 +992,7 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
 }
 
 int dm_publish_totals(dm_ctx* c, void* dst) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
   DM_HIP(c, launch_publish(c->R, c->agg.p, dst, c->stream), "publish");
@@ -958,7 +1007,7 @@ static bool root_layout_ok(dm_ctx* c, int G) {
 }
 
 int dm_hier_load_root(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns) {
-  DM_CHECK_CTX(root);
+  DM_ENTER(root);
   if (!root->store_loaded) return root->fail(DM_E_STATE, "root store not loaded");
   if (!gathered) return root->fail(DM_E_INVAL, "null gathered buffer");
   if (!root_layout_ok(root, n_servers))
@@ -974,8 +1023,10 @@ int dm_hier_load_root(dm_ctx* root, const void* gathered, int n_servers, int64_t
 }
 
 int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server) {
-  DM_CHECK_CTX(root);
+  DM_ENTER(root);
   if (!leaf) return root->fail(DM_E_INVAL, "null leaf context");
+  DM_HIP(root, leaf->join_aux(), "join leaf streams");
+  leaf->main_dirty = true;
   if (leaf->device != root->device) return root->fail(DM_E_INVAL, "root and leaf contexts must share a device");
   if (!root->have_result) return root->fail(DM_E_STATE, "no root dm_apportion result");
   const int G = (int)(root->R > 0 ? root->N / root->R : 0);
@@ -1005,7 +1056,7 @@ int dm_set_profiling(dm_ctx* c, int on) {
 }
 
 int dm_kernel_times(dm_ctx* c, dm_kernel_time* out, int max) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
   c->collect_profile();
   for (int i = 0; i < KC_COUNT && i < max; ++i) {
@@ -1017,7 +1068,7 @@ int dm_kernel_times(dm_ctx* c, dm_kernel_time* out, int max) {
 }
 
 int dm_reset_kernel_times(dm_ctx* c) {
-  DM_CHECK_CTX(c);
+  DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
   c->collect_profile();
   for (int i = 0; i < KC_COUNT; ++i) {

@@ -84,6 +84,10 @@ class Engine:
     def sync(self):
         self._chk(self._L.dm_sync(self._ctx))
 
+    def join(self):
+        """dm_join: order deferred ticks before later work on the context stream."""
+        self._chk(self._L.dm_join(self._ctx))
+
     # -- LeaseStore --
     def load(self, snap: dict):
         """NewLeaseStore + Assign of every row (store.go:114,153) and the resolved config."""
@@ -155,10 +159,11 @@ class Engine:
 
     # -- the batch algorithm --
     def apportion(self, now_ns: int, writeback: bool = False, recompute: bool = False, asynchronous: bool = False,
-                  wb_columns: str = "auto"):
-        """wb_columns: "auto", "inplace" or "alternate" (DM_WB_INPLACE / DM_WB_ALTERNATE)."""
+                  wb_columns: str = "auto", defer_join: bool = False):
+        """wb_columns: "auto", "inplace" or "alternate" (DM_WB_INPLACE / DM_WB_ALTERNATE);
+        defer_join (with asynchronous): DM_DEFER_JOIN."""
         flags = ((_lib.DM_WRITEBACK if writeback else 0) | (_lib.DM_AGG_RECOMPUTE if recompute else 0)
-                 | (_lib.DM_ASYNC if asynchronous else 0)
+                 | (_lib.DM_ASYNC if asynchronous else 0) | (_lib.DM_DEFER_JOIN if defer_join else 0)
                  | {"auto": 0, "inplace": _lib.DM_WB_INPLACE, "alternate": _lib.DM_WB_ALTERNATE}[wb_columns])
         self._chk(self._L.dm_apportion(self._ctx, int(now_ns), flags))
 

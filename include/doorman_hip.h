@@ -69,6 +69,13 @@ extern "C" {
    becomes the store's after the tick (faster streaming; 16 B per lease of HBM). */
 #define DM_WB_INPLACE 8u    /* force in-place writeback */
 #define DM_WB_ALTERNATE 16u /* force the alternate columns */
+#define DM_DEFER_JOIN 32u   /* with DM_ASYNC: a tick whose work classes run on the context's
+                               auxiliary streams need not join them back into the context
+                               stream at its end.  Every later library call on the context
+                               joins first; work the caller itself puts on the context
+                               stream is ordered after the tick only after dm_join or
+                               dm_sync.  Back-to-back ticks then skip two cross-queue hops
+                               each (C2: 240 -> 191 us per tick). */
 
 typedef struct dm_ctx dm_ctx;
 
@@ -113,6 +120,9 @@ const char* dm_last_error(dm_ctx* ctx);
 int dm_set_stream(dm_ctx* ctx, void* hip_stream);
 void* dm_get_stream(dm_ctx* ctx);
 int dm_sync(dm_ctx* ctx);
+/* Order every deferred tick (DM_DEFER_JOIN) before later work on the context stream,
+   without waiting on the host. */
+int dm_join(dm_ctx* ctx);
 
 /* ---- LeaseStore: device-resident columnar table ---- */
 int dm_store_load(dm_ctx* ctx, const dm_snapshot* snap);

@@ -471,3 +471,63 @@ def test_update_wants_narrow_assign(eng):
     eng.apportion(NOW)
     gets, exp = eng.leases()
     assert_leases_match(snap2, gets, exp, O.apportion(snap2, NOW), "after update_wants")
+
+
+@pytest.mark.parametrize("cols", ["inplace", "alternate"])
+def test_deferred_join_matches_joined_ticks(eng, cols):
+    """DM_DEFER_JOIN: back-to-back asynchronous writeback ticks whose work classes
+    stay on the auxiliary streams (no per-tick join) leave bit for bit the store,
+    running sums and leases of the same ticks run with a join per tick; then a
+    store update between deferred ticks (the call joins first) and two more ticks
+    agree too (to the ULP of the update's atomically accumulated running sums)."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(21)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng), expired_frac=0.05)
+    N = len(snap["wants"])
+    upd = np.sort(rng.choice(N, N // 8, replace=False))
+    new_w = rng.uniform(0.0, 50.0, len(upd))
+    cap = np.repeat(snap["capacity"], np.diff(snap["seg_off"]))
+    other = Engine(0)
+
+    def ticks(e, defer, t0, n):
+        for t in range(t0, t0 + n):
+            e.apportion(NOW + t * W.NS, writeback=True, asynchronous=True, wb_columns=cols, defer_join=defer)
+
+    def state(e):
+        gets, exp = e.leases()
+        return gets, exp, e.read_store(), e.resources(safe=False)
+
+    try:
+        outs = []
+        for e, defer in ((eng, True), (other, False)):
+            e.load(snap)
+            ticks(e, defer, 0, 6)
+            outs.append(state(e))
+        (g1, e1, s1, r1), (g2, e2, s2, r2) = outs
+        assert g1.tobytes() == g2.tobytes() and e1.tobytes() == e2.tobytes()
+        for k in ("has", "wants", "subclients", "expiry_ns"):
+            assert s1[k].tobytes() == s2[k].tobytes(), k
+        for k in ("count", "sum_has", "sum_wants"):
+            assert r1[k].tobytes() == r2[k].tobytes(), k
+        outs = []
+        for e, defer in ((eng, True), (other, False)):
+            ticks(e, defer, 6, 1)
+            e.update_wants(upd, new_w)
+            ticks(e, defer, 7, 2)
+            outs.append(state(e))
+        (g1, e1, s1, r1), (g2, e2, s2, r2) = outs
+        assert float_close(g1, g2, cap, 1e-12).all()
+        np.testing.assert_array_equal(e1, e2)
+        assert s1["wants"].tobytes() == s2["wants"].tobytes()
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        assert float_close(r1["sum_wants"], r2["sum_wants"], np.maximum(snap["capacity"], 1.0), 1e-12).all()
+        # and the deferred store agrees with the oracle on one more tick
+        ref_snap = dict(snap)
+        ref_snap.update(has=s1["has"], wants=s1["wants"], subclients=s1["subclients"], expiry_ns=s1["expiry_ns"],
+                        agg_count=r1["count"], agg_sum_has=r1["sum_has"], agg_sum_wants=r1["sum_wants"])
+        now = NOW + 10 * W.NS
+        eng.apportion(now, asynchronous=True, defer_join=True)
+        gets, exp = eng.leases()  # joins
+        assert_leases_match(ref_snap, gets, exp, O.apportion(ref_snap, now), "after deferred ticks")
+    finally:
+        other.close()
