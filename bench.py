@@ -96,7 +96,7 @@ def kernel_units(eng, snap):
 
 def streaming_step(eng, snap, rank, n_ticks):
     """configs[4]: one 5 s refresh tick of a device-resident store.  Per tick the
-    host sends 10% wants updates (dm_store_update_wants, narrow Assign), releases
+    host sends 10% wants updates (dm_store_update_wants_mask, narrow Assign), releases
     1% of the clients (departures, store.go:142-151), inserts 1% new clients into
     free slots (dm_store_upsert onto released rows), then the tick runs with
     writeback.  The update batches (what the RPCs would deliver) are generated
@@ -121,8 +121,10 @@ def streaming_step(eng, snap, rank, n_ticks):
         alive[new] = True
         now += 5 * W.NS
         k = len(new)
-        cols = (upd, rng.uniform(0.5, 1.5, len(upd)), gone, new, np.zeros(k), rng.uniform(0.5, 1.5, k),
-                np.ones(k, np.int64), np.full(k, now + 3600 * W.NS, np.int64))
+        # the wants refresh crosses PCIe as a row mask + packed values (1.25 B of mask
+        # per update at 10% instead of an 8-B row index: dm_store_update_wants_mask)
+        cols = (W.rows_to_mask(upd, N), rng.uniform(0.5, 1.5, len(upd)), gone, new, np.zeros(k),
+                rng.uniform(0.5, 1.5, k), np.ones(k, np.int64), np.full(k, now + 3600 * W.NS, np.int64))
         # the RPC layer would decode requests straight into page-locked buffers
         # (dm_host_alloc), which then cross PCIe by DMA
         pinned = []
@@ -134,8 +136,8 @@ def streaming_step(eng, snap, rank, n_ticks):
     it = iter(batches)
 
     def step():
-        upd, w, gone, new, nh, nw, ns, ne, t = next(it)
-        eng.update_wants(upd, w)
+        mask, w, gone, new, nh, nw, ns, ne, t = next(it)
+        eng.update_wants_mask(mask, w)
         eng.release(gone)
         eng.upsert(new, nh, nw, ns, ne)
         eng.apportion(t, writeback=True, asynchronous=True)

@@ -98,7 +98,8 @@ constexpr uint32_t kUpdDup = 2u;     // row twice in one call
 constexpr uint32_t kUpdSub = 4u;     // subclients outside [0, 2^31)
 constexpr uint32_t kUpdNaN = 8u;     // NaN wants (FairShare then needs k_general)
 constexpr uint32_t kUpdNotOne = 16u; // subclients != 1 (may make a resource heterogeneous)
-constexpr uint32_t kUpdReject = kUpdRange | kUpdDup | kUpdSub;
+constexpr uint32_t kUpdCount = 32u;  // packed values != set bits of the row mask
+constexpr uint32_t kUpdReject = kUpdRange | kUpdDup | kUpdSub | kUpdCount;
 
 // Per-resource configuration, AoS (one scalar burst per resource).
 struct ResCfg {

@@ -1427,6 +1427,114 @@ __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, cons
   wave_seg_add(agg, active, seg, 0.0, d, 0, false, false);
 }
 
+// ---- wants updates as a row mask + packed values (dm_store_update_wants_mask) ----
+// Bit j of word w is row first_row + 64 w + j; the set rows take the packed values
+// in ascending row order.  At 10% of the rows updated this moves 1.25 B of mask
+// per update over PCIe instead of an 8-B row index (C4: 116 instead of 200 MB).
+struct OpAddI64 {
+  __device__ long long operator()(long long a, long long b) const { return a + b; }
+};
+// Pass 1: popcount per 256-word block (+ rows past the store's end).
+__global__ __launch_bounds__(256) void k_mask_count(int64_t nwords, const uint64_t* __restrict__ mask,
+                                                    int64_t first_row, int64_t N, int64_t* block_sums,
+                                                    uint32_t* flags) {
+  __shared__ long long part[4];
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t m = w < nwords ? mask[w] : 0ull;
+  const int64_t row0 = first_row + 64 * w;
+  if (m && row0 + 63 >= N) {  // bits of rows >= N
+    const int64_t keep = N - row0;  // < 64
+    const uint64_t ok = keep <= 0 ? 0ull : ((1ull << keep) - 1ull);
+    if (m & ~ok) atomicOr(flags, kUpdRange);
+  }
+  long long c = __popcll(m);
+  c = wave_reduce(c, OpAddI64());
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// Pass 2 (one workgroup): exclusive scan of the block sums in place; the total
+// must equal the number of packed values.
+__global__ __launch_bounds__(1024) void k_mask_scan(int64_t nblocks, int64_t* block_sums, int64_t n_values,
+                                                    uint32_t* flags) {
+  __shared__ int64_t tot[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nblocks + 1023) / 1024;
+  const int64_t b0 = t * per < nblocks ? t * per : nblocks;
+  const int64_t b1 = b0 + per < nblocks ? b0 + per : nblocks;
+  int64_t s = 0;
+  for (int64_t b = b0; b < b1; ++b) s += block_sums[b];
+  tot[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the 1024 partials
+    const int64_t v = t >= o ? tot[t - o] : 0;
+    __syncthreads();
+    tot[t] += v;
+    __syncthreads();
+  }
+  int64_t run = tot[t] - s;
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t v = block_sums[b];
+    block_sums[b] = run;
+    run += v;
+  }
+  if (t == 1023 && tot[1023] != n_values) atomicOr(flags, kUpdCount);
+}
+
+// Pass 3: each lane applies its word's rows (narrow Assign, store.go:157).
+// Deltas of a lane's run within one resource are summed first; the lane's last
+// run goes through the wave aggregation, earlier ones (resource boundaries inside
+// the 64 rows) add directly.
+__global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64_t* __restrict__ mask,
+                                                    int64_t first_row, const int64_t* __restrict__ block_offs,
+                                                    const double* __restrict__ wants, RowIndex ix, double* s_wants,
+                                                    ResAgg* agg, uint32_t* flags) {
+  __shared__ int wsum[4];
+  if (*flags & kUpdReject) return;  // uniform over the grid
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t m = w < nwords ? mask[w] : 0ull;
+  // offset of this word's first value: the block's offset + a scan within the block
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = __popcll(m);
+  int incl = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int64_t off = block_offs[blockIdx.x] + incl - c;
+  for (int i = 0; i < wave; ++i) off += wsum[i];
+  int seg = 0;
+  double acc = 0.0;
+  bool nan = false;
+  if (m) {
+    const int64_t row0 = first_row + 64 * w;
+    seg = seg_of_row(ix, row0 + __builtin_ctzll(m));
+    int64_t seg_end = ix.seg_off[seg + 1];
+    while (m) {
+      const int j = __builtin_ctzll(m);
+      m &= m - 1;
+      const int64_t r = row0 + j;
+      if (r >= seg_end) {  // the previous resource's run ends inside this word
+        atomicAdd(&agg[seg].sum_wants, acc);
+        acc = 0.0;
+        do {
+          ++seg;
+          seg_end = ix.seg_off[seg + 1];
+        } while (r >= seg_end);
+      }
+      const double v = wants[off++];
+      nan |= __builtin_isnan(v);
+      acc += v - s_wants[r];
+      s_wants[r] = v;
+    }
+  }
+  wave_seg_add(agg, c > 0, seg, 0.0, acc, 0, false, false);
+  if (__ballot(nan) && lane == 0) atomicOr(flags, kUpdNaN);
+}
+
 // gets / expiry of scattered rows (dm_read_leases_rows)
 __global__ void k_gather_leases(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ gets,
                                 const int64_t* __restrict__ expiry, double* out_gets, int64_t* out_exp) {
@@ -1596,6 +1704,17 @@ hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st) {
   if (R <= 0) return hipSuccess;
   k_publish<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, agg, (double2*)dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
+                                    int64_t n_values, const double* wants, int64_t* block_sums, const RowIndex& ix,
+                                    double* s_wants, ResAgg* agg, uint32_t* flags, hipStream_t st) {
+  if (nwords <= 0) return hipSuccess;
+  const int64_t nb = (nwords + 255) / 256;
+  k_mask_count<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, N, block_sums, flags);
+  k_mask_scan<<<1, 1024, 0, st>>>(nb, block_sums, n_values, flags);
+  k_mask_apply<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, block_sums, wants, ix, s_wants, agg, flags);
   return hipGetLastError();
 }
 

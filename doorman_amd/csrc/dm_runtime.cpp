@@ -36,6 +36,9 @@ hipError_t launch_gather_leases(int64_t n, const int64_t* rows, const double* ge
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
+hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
+                                    int64_t n_values, const double* wants, int64_t* block_sums, const RowIndex& ix,
+                                    double* s_wants, ResAgg* agg, uint32_t* flags, hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
@@ -169,6 +172,8 @@ struct dm_ctx {
   // staging for upsert / release
   DBuf<int64_t> st_rows, st_sub, st_exp;
   DBuf<double> st_has, st_wants;
+  DBuf<uint64_t> st_mask;  // dm_store_update_wants_mask
+  DBuf<int64_t> st_blk;
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
@@ -219,6 +224,7 @@ struct dm_ctx {
     pa_nan.release(); pa_live.release(); p_tot.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
+    st_mask.release(); st_blk.release();
     row_bits.release(); upd_flags.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
@@ -934,6 +940,46 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
   if (rc) return rc;
+  if (f & kUpdNaN) c->maybe_general = true;
+  c->have_result = false;
+  return DM_OK;
+}
+
+// The same narrow Assign with the rows as a bit mask (one bit per row of
+// [first_row, first_row + 64 nwords)) and the values packed in row order: at
+// more than ~3% of the rows updated the mask is smaller than 8-B row indices.
+int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, const uint64_t* mask, int64_t n,
+                               const double* wants) {
+  DM_ENTER(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (first_row < 0 || (first_row & 63) || nwords < 0 || n < 0 || (nwords > 0 && !mask) || (n > 0 && !wants))
+    return c->fail(DM_E_INVAL, "bad masked update (first_row must be a multiple of 64)");
+  if (nwords == 0) return n == 0 ? DM_OK : c->fail(DM_E_INVAL, "packed values without a mask");
+  if (first_row + 64 * (nwords - 1) >= c->N) return c->fail(DM_E_RANGE, "mask words past the store's end");
+  const int64_t nb = (nwords + 255) / 256;
+  DM_HIP(c, c->st_mask.ensure((size_t)nwords), "stage mask");
+  DM_HIP(c, c->st_wants.ensure((size_t)std::max<int64_t>(n, 1)), "stage wants");
+  DM_HIP(c, c->st_blk.ensure((size_t)nb), "stage block sums");
+  if (!c->upd_flags.p) {
+    DM_HIP(c, c->upd_flags.ensure(1), "update flags");
+    DM_HIP(c, hipHostMalloc((void**)&c->h_flags, sizeof(uint32_t), hipHostMallocDefault), "update flags");
+  }
+  DM_HIP(c, hipMemsetAsync(c->upd_flags.p, 0, sizeof(uint32_t), c->stream), "update flags");
+  // the copies overlap whatever still runs on the context's streams (staged_check)
+  DM_HIP(c, hipMemcpyAsync(c->st_mask.p, mask, (size_t)nwords * 8, hipMemcpyHostToDevice, c->cpy), "stage mask");
+  if (n > 0)
+    DM_HIP(c, hipMemcpyAsync(c->st_wants.p, wants, (size_t)n * 8, hipMemcpyHostToDevice, c->cpy), "stage wants");
+  DM_HIP(c, hipEventRecord(c->ev_stage[0], c->cpy), "stage update");
+  DM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_stage[0], 0), "stage update");
+  DM_HIP(c, launch_update_wants_mask(nwords, c->st_mask.p, first_row, c->N, n, c->st_wants.p, c->st_blk.p,
+                                     c->row_index(), c->wants.p, c->agg.p, c->upd_flags.p, c->stream),
+         "masked update");
+  DM_HIP(c, hipMemcpyAsync(c->h_flags, c->upd_flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream),
+         "update flags");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "update");
+  const uint32_t f = *c->h_flags;
+  if (f & kUpdRange) return c->fail(DM_E_RANGE, "mask bit past the store's end");
+  if (f & kUpdCount) return c->fail(DM_E_INVAL, "packed values must match the mask's set bits");
   if (f & kUpdNaN) c->maybe_general = true;
   c->have_result = false;
   return DM_OK;

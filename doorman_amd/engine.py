@@ -144,6 +144,13 @@ class Engine:
         rows, wants = _c(rows, np.int64), _c(wants, np.float64)
         self._chk(self._L.dm_store_update_wants(self._ctx, len(rows), _ptr(rows), _ptr(wants)))
 
+    def update_wants_mask(self, mask, wants, first_row: int = 0):
+        """update_wants with the rows as a bit mask (uint64 words; bit j of word w is row
+        first_row + 64 w + j) and the values packed in ascending row order."""
+        mask, wants = _c(mask, np.uint64), _c(wants, np.float64)
+        self._chk(self._L.dm_store_update_wants_mask(self._ctx, int(first_row), len(mask), _ptr(mask), len(wants),
+                                                     _ptr(wants)))
+
     def release(self, rows):
         """Release (store.go:142-151)."""
         rows = _c(rows, np.int64)

@@ -202,3 +202,11 @@ def random_snapshot(rng, n_resources, max_clients, kinds=(0, 1, 2, 3), hetero=Fa
     lease = rng.integers(1, 600, R)
     refresh = rng.integers(1, 60, R)
     return make_snapshot(sizes, wants, has, sub, exp, kind, capacity, lease, refresh, learning, parent, safe)
+
+
+def rows_to_mask(rows, n_rows: int, first_row: int = 0) -> np.ndarray:
+    """Row mask of dm_store_update_wants_mask: bit j of word w is row first_row + 64 w + j."""
+    nwords = (n_rows + 63) // 64
+    bits = np.zeros(nwords * 64, np.uint8)
+    bits[np.asarray(rows, np.int64) - first_row] = 1
+    return np.packbits(bits, bitorder="little").view(np.uint64)

@@ -133,6 +133,14 @@ int dm_store_upsert(dm_ctx* ctx, int64_t n, const int64_t* rows, const double* h
 /* Assign of a refresh that only changes wants (store.go:153-167 with has, subclients and
  * expiry unchanged): sumWants += new - old.  12 bytes per update over PCIe. */
 int dm_store_update_wants(dm_ctx* ctx, int64_t n, const int64_t* rows, const double* wants);
+/* The same narrow Assign with the rows given as a bit mask: bit j of mask[w] is row
+   first_row + 64*w + j (first_row a multiple of 64); the n set rows take wants[0..n)
+   in ascending row order.  Smaller than row indices above ~3% of the rows (C4's 10%
+   wants refresh: 116 instead of 200 MB over PCIe).  DM_E_RANGE for a bit past the
+   store's end, DM_E_INVAL when n differs from the mask's popcount; a rejected call
+   leaves the store untouched. */
+int dm_store_update_wants_mask(dm_ctx* ctx, int64_t first_row, int64_t nwords, const uint64_t* mask, int64_t n,
+                               const double* wants);
 /* Release (store.go:142-151): sums -= row; row zeroed and marked DM_RELEASED.  A released
  * row is a free slot: dm_store_upsert onto it is Assign of a new client. */
 int dm_store_release(dm_ctx* ctx, int64_t n, const int64_t* rows);

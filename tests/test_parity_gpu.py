@@ -531,3 +531,70 @@ def test_deferred_join_matches_joined_ticks(eng, cols):
         assert_leases_match(ref_snap, gets, exp, O.apportion(ref_snap, now), "after deferred ticks")
     finally:
         other.close()
+
+
+def test_update_wants_mask_matches_row_form(eng):
+    """dm_store_update_wants_mask (rows as a bit mask, values packed in row order)
+    leaves the store and running sums of dm_store_update_wants on the same rows,
+    across resource boundaries inside a 64-row word and for a window that starts
+    at a 64-row boundary; the next tick matches the oracle."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(31)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng), expired_frac=0.0)
+    N = len(snap["wants"])
+    cap = np.maximum(snap["capacity"], 1.0)
+    other = Engine(0)
+    try:
+        eng.load(snap)
+        other.load(snap)
+        rows = np.sort(rng.choice(N, N // 7, replace=False))
+        w = rng.uniform(0.0, 40.0, len(rows))
+        eng.update_wants_mask(W.rows_to_mask(rows, N), w)
+        other.update_wants(rows, w)
+        lo = 64 * (N // 128)
+        sub = np.sort(rng.choice(np.arange(lo, N), (N - lo) // 3, replace=False))
+        w2 = rng.uniform(0.0, 40.0, len(sub))
+        eng.update_wants_mask(W.rows_to_mask(sub, N - lo, first_row=lo), w2, first_row=lo)
+        other.update_wants(sub, w2)
+        s1, s2 = eng.read_store(), other.read_store()
+        assert s1["wants"].tobytes() == s2["wants"].tobytes()
+        r1, r2 = eng.resources(safe=False), other.resources(safe=False)
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        assert float_close(r1["sum_wants"], r2["sum_wants"], cap, 1e-12).all()
+        exact = snap["agg_sum_wants"].copy()
+        np.add.at(exact, np.repeat(np.arange(len(cap)), np.diff(snap["seg_off"])), s1["wants"] - snap["wants"])
+        assert float_close(r1["sum_wants"], exact, cap, 1e-12).all()
+        ref_snap = dict(snap)
+        ref_snap.update(wants=s1["wants"], agg_sum_wants=r1["sum_wants"])
+        eng.apportion(NOW)
+        gets, exp = eng.leases()
+        assert_leases_match(ref_snap, gets, exp, O.apportion(ref_snap, NOW), "after masked update")
+    finally:
+        other.close()
+
+
+def test_update_wants_mask_rejects_bad_input(eng):
+    """Count mismatch (DM_E_INVAL), a bit past the store's end (DM_E_RANGE), a window
+    not on a 64-row boundary (DM_E_INVAL): the store is left untouched."""
+    from doorman_amd._lib import DM_E_INVAL, DM_E_RANGE, DmError
+    rng = np.random.default_rng(32)
+    snap = snapshot_with_sizes(rng, np.array([5, 70, 300]), expired_frac=0.0)
+    N = len(snap["wants"])
+    assert N % 64 != 0
+    eng.load(snap)
+    before, res0 = eng.read_store(), eng.resources(safe=False)
+    mask = W.rows_to_mask([1, 5, 9], N)
+    with pytest.raises(DmError) as e:
+        eng.update_wants_mask(mask, [1.0, 2.0])
+    assert e.value.code == DM_E_INVAL
+    bad = mask.copy()
+    bad[-1] |= np.uint64(1) << np.uint64(63)
+    with pytest.raises(DmError) as e:
+        eng.update_wants_mask(bad, [1.0, 2.0, 3.0, 4.0])
+    assert e.value.code == DM_E_RANGE
+    with pytest.raises(DmError) as e:
+        eng.update_wants_mask(mask, [1.0, 2.0, 3.0], first_row=3)
+    assert e.value.code == DM_E_INVAL
+    after, res1 = eng.read_store(), eng.resources(safe=False)
+    assert after["wants"].tobytes() == before["wants"].tobytes()
+    assert res1["sum_wants"].tobytes() == res0["sum_wants"].tobytes()

@@ -93,3 +93,13 @@ def test_hierarchy_exchange_gloo_world2():
     # every server asked for more than its share: FairShare splits the capacity by subclients
     tot = res[0][0] + res[1][0]
     assert np.all(tot <= 1000.0 + 1e-9)
+
+
+def test_rows_to_mask_round_trip():
+    """Bit j of word w is row first_row + 64 w + j (dm_store_update_wants_mask)."""
+    rng = np.random.default_rng(3)
+    rows = np.sort(rng.choice(1000, 137, replace=False)) + 128
+    mask = W.rows_to_mask(rows, 1000, first_row=128)
+    assert mask.dtype == np.uint64 and len(mask) == (1000 + 63) // 64
+    got = [128 + 64 * w + j for w in range(len(mask)) for j in range(64) if (int(mask[w]) >> j) & 1]
+    np.testing.assert_array_equal(got, rows)
