@@ -446,6 +446,11 @@ int dm_create(int device, dm_ctx** out) {
 void dm_destroy(dm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  // deferred tick work (DM_DEFER_JOIN) and update copies may still run on the
+  // auxiliary streams: drain every stream before any buffer is freed
+  for (int i = 0; i < dm_ctx::kAux; ++i)
+    if (c->aux[i]) (void)hipStreamSynchronize(c->aux[i]);
+  if (c->cpy) (void)hipStreamSynchronize(c->cpy);
   (void)hipStreamSynchronize(c->stream);
   c->collect_profile();
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
