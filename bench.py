@@ -201,7 +201,26 @@ def cpu_baseline(snap, now_ns, budget_s=12.0):
             "cores": threads,
             "sample": f"whole snapshot x{reps}: oracle/ closed form (SURVEY.md §8a), OpenMP over resources",
         },
+        "host": host_info(),
     }
+
+
+def host_info():
+    """CPU model and core counts of the box the baseline ran on (SURVEY.md §8d asks
+    for them next to the Go reference's GOMAXPROCS, which has no counterpart here)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cores": usable}
 
 
 def main():
