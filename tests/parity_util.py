@@ -61,9 +61,9 @@ def binned_sizes(rng, per_bin=3, large=True):
     sizes = []
     for lo, hi in edges:
         sizes += list(rng.integers(lo, hi + 1, per_bin))
-    sizes += [8, 9, 16, 17, 32, 33, 64, 65, 256, 257, 4096]
-    if large:
-        sizes += [4097, 8192]
+    sizes += [8, 9, 16, 17, 32, 33, 64, 65, 128, 129, 256, 257, 512, 513, 1024, 1025, 2048, 2049, 4096]
+    if large:  # chunk edges of the large path (kChunkRows = 2048): 1-row tail, exact multiples
+        sizes += [4097, 6144, 8192, 10241]
     rng.shuffle(sizes)
     return np.asarray(sizes, dtype=np.int64)
 
