@@ -1434,11 +1434,13 @@ __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, cons
 struct OpAddI64 {
   __device__ long long operator()(long long a, long long b) const { return a + b; }
 };
-// Pass 1: popcount per 256-word block (+ rows past the store's end).
+// Pass 1: popcount per 256-word block (+ rows past the store's end), and every
+// word's exclusive offset within its block.
 __global__ __launch_bounds__(256) void k_mask_count(int64_t nwords, const uint64_t* __restrict__ mask,
                                                     int64_t first_row, int64_t N, int64_t* block_sums,
-                                                    uint32_t* flags) {
-  __shared__ long long part[4];
+                                                    int32_t* word_pre, uint32_t* flags) {
+  __shared__ int part[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t m = w < nwords ? mask[w] : 0ull;
   const int64_t row0 = first_row + 64 * w;
@@ -1447,11 +1449,18 @@ __global__ __launch_bounds__(256) void k_mask_count(int64_t nwords, const uint64
     const uint64_t ok = keep <= 0 ? 0ull : ((1ull << keep) - 1ull);
     if (m & ~ok) atomicOr(flags, kUpdRange);
   }
-  long long c = __popcll(m);
-  c = wave_reduce(c, OpAddI64());
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  const int c = __popcll(m);
+  int incl = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) part[wave] = incl;
   __syncthreads();
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+  int pre = incl - c;
+  for (int i = 0; i < wave; ++i) pre += part[i];
+  if (w < nwords) word_pre[w] = pre;
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = (int64_t)part[0] + part[1] + part[2] + part[3];
 }
 
 // Pass 2 (one workgroup): exclusive scan of the block sums in place; the total
@@ -1482,56 +1491,92 @@ __global__ __launch_bounds__(1024) void k_mask_scan(int64_t nblocks, int64_t* bl
   if (t == 1023 && tot[1023] != n_values) atomicOr(flags, kUpdCount);
 }
 
-// Pass 3: each lane applies its word's rows (narrow Assign, store.go:157).
-// Deltas of a lane's run within one resource are summed first; the lane's last
-// run goes through the wave aggregation, earlier ones (resource boundaries inside
-// the 64 rows) add directly.
+// Pass 3: one lane per row; a wave takes kMaskWords consecutive mask words (64
+// rows each).  Lane q first fetches word q, its first value's offset and the
+// resource of its first row (all words in parallel); then every row's loads of
+// every word are issued before any is consumed (coalesced: per word the wave reads
+// its packed values and 512 B of the wants column).  A resource's deltas stay in
+// per-lane registers while consecutive words lie inside it and leave with one
+// reduction + atomic when the resource changes; a word that spans resources adds
+// its runs directly (wave_seg_add).
+constexpr int kMaskWords = 16;
 __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64_t* __restrict__ mask,
                                                     int64_t first_row, const int64_t* __restrict__ block_offs,
+                                                    const int32_t* __restrict__ word_pre,
                                                     const double* __restrict__ wants, RowIndex ix, double* s_wants,
                                                     ResAgg* agg, uint32_t* flags) {
-  __shared__ int wsum[4];
   if (*flags & kUpdReject) return;  // uniform over the grid
-  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  uint64_t m = w < nwords ? mask[w] : 0ull;
-  // offset of this word's first value: the block's offset + a scan within the block
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = __popcll(m);
-  int incl = c;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kMaskWords;
+  if (w0 >= nwords) return;  // whole waves
+  const int nw = nwords - w0 < kMaskWords ? (int)(nwords - w0) : kMaskWords;
+  uint64_t my_m = 0ull;
+  int64_t my_off = 0, my_end = 0;
+  int my_seg = 0;
+  if (lane < nw) {
+    const int64_t w = w0 + lane;
+    my_m = mask[w];
+    my_off = block_offs[w >> 8] + word_pre[w];
+    my_seg = seg_of_row(ix, first_row + 64 * w);
+    my_end = ix.seg_off[my_seg + 1];  // the word lies in one resource iff its last row < my_end
   }
-  if (lane == 63) wsum[wave] = incl;
-  __syncthreads();
-  int64_t off = block_offs[blockIdx.x] + incl - c;
-  for (int i = 0; i < wave; ++i) off += wsum[i];
-  int seg = 0;
-  double acc = 0.0;
-  bool nan = false;
-  if (m) {
-    const int64_t row0 = first_row + 64 * w;
-    seg = seg_of_row(ix, row0 + __builtin_ctzll(m));
-    int64_t seg_end = ix.seg_off[seg + 1];
-    while (m) {
-      const int j = __builtin_ctzll(m);
-      m &= m - 1;
-      const int64_t r = row0 + j;
-      if (r >= seg_end) {  // the previous resource's run ends inside this word
-        atomicAdd(&agg[seg].sum_wants, acc);
-        acc = 0.0;
-        do {
-          ++seg;
-          seg_end = ix.seg_off[seg + 1];
-        } while (r >= seg_end);
+  const uint64_t below = (1ull << lane) - 1ull;
+  double v[kMaskWords], old[kMaskWords];
+#pragma unroll
+  for (int q = 0; q < kMaskWords; ++q) {  // every load in flight before the first use
+    v[q] = 0.0;
+    old[q] = 0.0;
+    if (q < nw) {
+      const uint64_t m = readlane_any(my_m, q);
+      if ((m >> lane) & 1ull) {
+        v[q] = wants[readlane_any(my_off, q) + __popcll(m & below)];
+        old[q] = s_wants[first_row + 64 * (w0 + q) + lane];
       }
-      const double v = wants[off++];
-      nan |= __builtin_isnan(v);
-      acc += v - s_wants[r];
-      s_wants[r] = v;
     }
   }
-  wave_seg_add(agg, c > 0, seg, 0.0, acc, 0, false, false);
+  int cur = -1;      // resource whose deltas `acc` holds (uniform)
+  double acc = 0.0;  // this lane's share of them
+  bool nan = false;
+#pragma unroll
+  for (int q = 0; q < kMaskWords; ++q) {
+    const uint64_t m = q < nw ? readlane_any(my_m, q) : 0ull;
+    if (m != 0ull) {  // uniform
+      const int64_t row0 = first_row + 64 * (w0 + q);
+      const bool act = (m >> lane) & 1ull;
+      const int s0 = __builtin_amdgcn_readlane(my_seg, q);
+      const bool single = readlane_any(my_end, q) > row0 + 63 - __builtin_clzll(m);
+      double d = 0.0;
+      int seg = s0;
+      if (act) {
+        const int64_t r = row0 + lane;
+        nan |= __builtin_isnan(v[q]);
+        if (!single)
+          while (ix.seg_off[seg + 1] <= r) ++seg;
+        d = v[q] - old[q];
+        s_wants[r] = v[q];
+      }
+      if (single && s0 == cur) {
+        acc += d;
+      } else {
+        if (cur >= 0) {  // flush the previous resource
+          const double t = wave_reduce(acc, [](double a, double b) { return a + b; });
+          if (lane == 0) atomicAdd(&agg[cur].sum_wants, t);
+        }
+        if (single) {
+          cur = s0;
+          acc = d;
+        } else {
+          cur = -1;
+          acc = 0.0;
+          wave_seg_add(agg, act, seg, 0.0, d, 0, false, false);
+        }
+      }
+    }
+  }
+  if (cur >= 0) {
+    const double t = wave_reduce(acc, [](double a, double b) { return a + b; });
+    if (lane == 0) atomicAdd(&agg[cur].sum_wants, t);
+  }
   if (__ballot(nan) && lane == 0) atomicOr(flags, kUpdNaN);
 }
 
@@ -1708,13 +1753,16 @@ hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t s
 }
 
 hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
-                                    int64_t n_values, const double* wants, int64_t* block_sums, const RowIndex& ix,
-                                    double* s_wants, ResAgg* agg, uint32_t* flags, hipStream_t st) {
+                                    int64_t n_values, const double* wants, int64_t* block_sums, int32_t* word_pre,
+                                    const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
+                                    hipStream_t st) {
   if (nwords <= 0) return hipSuccess;
   const int64_t nb = (nwords + 255) / 256;
-  k_mask_count<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, N, block_sums, flags);
+  k_mask_count<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, N, block_sums, word_pre, flags);
   k_mask_scan<<<1, 1024, 0, st>>>(nb, block_sums, n_values, flags);
-  k_mask_apply<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, block_sums, wants, ix, s_wants, agg, flags);
+  const int64_t waves = (nwords + kMaskWords - 1) / kMaskWords;
+  k_mask_apply<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(nwords, mask, first_row, block_sums, word_pre, wants, ix,
+                                                            s_wants, agg, flags);
   return hipGetLastError();
 }
 

@@ -37,8 +37,9 @@ hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t s
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
-                                    int64_t n_values, const double* wants, int64_t* block_sums, const RowIndex& ix,
-                                    double* s_wants, ResAgg* agg, uint32_t* flags, hipStream_t st);
+                                    int64_t n_values, const double* wants, int64_t* block_sums, int32_t* word_pre,
+                                    const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
+                                    hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
@@ -174,6 +175,7 @@ struct dm_ctx {
   DBuf<double> st_has, st_wants;
   DBuf<uint64_t> st_mask;  // dm_store_update_wants_mask
   DBuf<int64_t> st_blk;
+  DBuf<int32_t> st_wpre;
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
@@ -224,7 +226,7 @@ struct dm_ctx {
     pa_nan.release(); pa_live.release(); p_tot.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
-    st_mask.release(); st_blk.release();
+    st_mask.release(); st_blk.release(); st_wpre.release();
     row_bits.release(); upd_flags.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
@@ -965,6 +967,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
   DM_HIP(c, c->st_mask.ensure((size_t)nwords), "stage mask");
   DM_HIP(c, c->st_wants.ensure((size_t)std::max<int64_t>(n, 1)), "stage wants");
   DM_HIP(c, c->st_blk.ensure((size_t)nb), "stage block sums");
+  DM_HIP(c, c->st_wpre.ensure((size_t)nwords), "stage word offsets");
   if (!c->upd_flags.p) {
     DM_HIP(c, c->upd_flags.ensure(1), "update flags");
     DM_HIP(c, hipHostMalloc((void**)&c->h_flags, sizeof(uint32_t), hipHostMallocDefault), "update flags");
@@ -977,7 +980,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
   DM_HIP(c, hipEventRecord(c->ev_stage[0], c->cpy), "stage update");
   DM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_stage[0], 0), "stage update");
   DM_HIP(c, launch_update_wants_mask(nwords, c->st_mask.p, first_row, c->N, n, c->st_wants.p, c->st_blk.p,
-                                     c->row_index(), c->wants.p, c->agg.p, c->upd_flags.p, c->stream),
+                                     c->st_wpre.p, c->row_index(), c->wants.p, c->agg.p, c->upd_flags.p, c->stream),
          "masked update");
   DM_HIP(c, hipMemcpyAsync(c->h_flags, c->upd_flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream),
          "update flags");

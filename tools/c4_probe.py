@@ -30,9 +30,9 @@ def main():
     # reach into the pre-generated batches through the closure
     it = step.__closure__[step.__code__.co_freevars.index("it")].cell_contents
     for k in range(args.steps + 2):
-        upd, w, gone, new, nh, nw, ns, ne, t = next(it)
+        mask, w, gone, new, nh, nw, ns, ne, t = next(it)
         ts = [time.perf_counter()]
-        eng.update_wants(upd, w)
+        eng.update_wants_mask(mask, w)
         eng.sync()
         ts.append(time.perf_counter())
         eng.release(gone)
@@ -44,8 +44,8 @@ def main():
         eng.apportion(t, writeback=True)
         ts.append(time.perf_counter())
         d = np.diff(ts) * 1e3
-        mb = (upd.nbytes + w.nbytes) / 1e6
-        print(f"step {k}: update_wants {d[0]:.2f} ms ({len(upd)} rows, {mb:.0f} MB -> {mb / d[0]:.1f} GB/s) "
+        mb = (mask.nbytes + w.nbytes) / 1e6
+        print(f"step {k}: update_wants_mask {d[0]:.2f} ms ({len(w)} rows, {mb:.0f} MB -> {mb / d[0]:.1f} GB/s) "
               f"release {d[1]:.2f} ms ({len(gone)}) upsert {d[2]:.2f} ms ({len(new)}) tick {d[3]:.2f} ms", flush=True)
     n = 200 * 2 ** 20 // 8
     big = torch.empty(n, dtype=torch.float64).pin_memory()
