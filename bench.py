@@ -96,10 +96,10 @@ def kernel_units(eng, snap):
 
 def streaming_step(eng, snap, rank, n_ticks):
     """configs[4]: one 5 s refresh tick of a device-resident store.  Per tick the
-    host sends 10% wants updates (dm_store_update_wants_mask, narrow Assign), releases
+    host sends 10% wants updates (row mask + packed values, narrow Assign), releases
     1% of the clients (departures, store.go:142-151), inserts 1% new clients into
-    free slots (dm_store_upsert onto released rows), then the tick runs with
-    writeback.  The update batches (what the RPCs would deliver) are generated
+    free slots (upsert onto released rows) -- all three in one dm_store_apply call --
+    then the tick runs with writeback.  The update batches (what the RPCs would deliver) are generated
     before the timed region."""
     from doorman_amd import workloads as W
     rng = np.random.default_rng(400 + rank)
@@ -137,9 +137,7 @@ def streaming_step(eng, snap, rank, n_ticks):
 
     def step():
         mask, w, gone, new, nh, nw, ns, ne, t = next(it)
-        eng.update_wants_mask(mask, w)
-        eng.release(gone)
-        eng.upsert(new, nh, nw, ns, ne)
+        eng.apply(mask, w, gone, (new, nh, nw, ns, ne))  # the round's three update kinds, one call
         eng.apportion(t, writeback=True, asynchronous=True)
 
     return step

@@ -39,6 +39,18 @@ class Snapshot(ctypes.Structure):
     ]
 
 
+class StoreBatch(ctypes.Structure):
+    """dm_store_batch: one round's refresh (row mask + packed wants), departures, arrivals."""
+    _fields_ = [
+        ("wants_first_row", ctypes.c_int64), ("wants_nwords", ctypes.c_int64), ("wants_mask", ctypes.c_void_p),
+        ("wants_n", ctypes.c_int64), ("wants", ctypes.c_void_p),
+        ("release_n", ctypes.c_int64), ("release_rows", ctypes.c_void_p),
+        ("upsert_n", ctypes.c_int64), ("upsert_rows", ctypes.c_void_p), ("upsert_has", ctypes.c_void_p),
+        ("upsert_wants", ctypes.c_void_p), ("upsert_subclients", ctypes.c_void_p),
+        ("upsert_expiry_ns", ctypes.c_void_p),
+    ]
+
+
 class ResourceCfg(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_void_p),
@@ -74,6 +86,7 @@ _SIGS = {
     "dm_config_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ResourceCfg)]),
     "dm_store_upsert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5),
     "dm_store_release": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "dm_store_apply": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dm_host_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     "dm_host_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dm_store_update_wants": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),

@@ -1580,6 +1580,9 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
   if (__ballot(nan) && lane == 0) atomicOr(flags, kUpdNaN);
 }
 
+// dm_store_apply: a part is applied only if no earlier part was rejected.
+__global__ void k_carry_reject(const uint32_t* __restrict__ from, uint32_t* to) { *to |= *from & kUpdReject; }
+
 // gets / expiry of scattered rows (dm_read_leases_rows)
 __global__ void k_gather_leases(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ gets,
                                 const int64_t* __restrict__ expiry, double* out_gets, int64_t* out_exp) {
@@ -1763,6 +1766,11 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
   const int64_t waves = (nwords + kMaskWords - 1) / kMaskWords;
   k_mask_apply<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(nwords, mask, first_row, block_sums, word_pre, wants, ix,
                                                             s_wants, agg, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st) {
+  k_carry_reject<<<1, 1, 0, st>>>(from, to);
   return hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     int64_t n_values, const double* wants, int64_t* block_sums, int32_t* word_pre,
                                     const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
                                     hipStream_t st);
+hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
@@ -176,6 +177,11 @@ struct dm_ctx {
   DBuf<uint64_t> st_mask;  // dm_store_update_wants_mask
   DBuf<int64_t> st_blk;
   DBuf<int32_t> st_wpre;
+  DBuf<double> st_mwants;   // dm_store_apply: the refresh part's values
+  DBuf<int64_t> st_rel;     // dm_store_apply: the departures' rows
+  DBuf<uint32_t> bat_flags; // dm_store_apply: one flags word per part
+  uint32_t* h_bat_flags = nullptr;
+  hipEvent_t ev_bat[3] = {};
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
@@ -226,7 +232,10 @@ struct dm_ctx {
     pa_nan.release(); pa_live.release(); p_tot.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
-    st_mask.release(); st_blk.release(); st_wpre.release();
+    st_mask.release(); st_blk.release(); st_wpre.release(); st_mwants.release(); st_rel.release();
+    bat_flags.release();
+    if (h_bat_flags) (void)hipHostFree(h_bat_flags);
+    h_bat_flags = nullptr;
     row_bits.release(); upd_flags.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
@@ -436,6 +445,7 @@ int dm_create(int device, dm_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
+  for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
     dm_destroy(c);
@@ -470,6 +480,8 @@ void dm_destroy(dm_ctx* c) {
   }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   for (auto ev : c->ev_stage)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : c->ev_bat)
     if (ev) (void)hipEventDestroy(ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -1009,6 +1021,121 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   rc = finish_update(c, n, &f);
   if (rc) return rc;
   c->have_result = false;
+  return DM_OK;
+}
+
+// One round of updates: every part's columns cross PCIe back to back on the copy
+// stream; each part is validated and applied on the context stream as soon as its
+// columns have landed (overlapping the later parts' copies), in the order refresh,
+// departures, arrivals.  A part whose validation fails is not applied, nor is any
+// later part (k_carry_reject); earlier parts stay applied.
+int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
+  DM_ENTER(c);
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (!b) return c->fail(DM_E_INVAL, "null batch");
+  const int64_t nw = b->wants_nwords, nm = b->wants_n, nr = b->release_n, nu = b->upsert_n;
+  if (nw < 0 || nm < 0 || nr < 0 || nu < 0) return c->fail(DM_E_INVAL, "negative batch sizes");
+  if (nw == 0 && nm > 0) return c->fail(DM_E_INVAL, "packed values without a mask");
+  if (nw > 0) {
+    const int64_t fr = b->wants_first_row;
+    if (fr < 0 || (fr & 63) || !b->wants_mask || (nm > 0 && !b->wants))
+      return c->fail(DM_E_INVAL, "bad masked update (first_row must be a multiple of 64)");
+    if (fr + 64 * (nw - 1) >= c->N) return c->fail(DM_E_RANGE, "mask words past the store's end");
+  }
+  if (nr > 0 && !b->release_rows) return c->fail(DM_E_INVAL, "bad release");
+  if (nu > 0 && (!b->upsert_rows || !b->upsert_has || !b->upsert_wants || !b->upsert_subclients ||
+                 !b->upsert_expiry_ns))
+    return c->fail(DM_E_INVAL, "bad upsert");
+  if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
+  hipStream_t st = c->stream, cp = c->cpy;
+  if (!c->bat_flags.p) {
+    DM_HIP(c, c->bat_flags.ensure(3), "batch flags");
+    DM_HIP(c, hipHostMalloc((void**)&c->h_bat_flags, 3 * sizeof(uint32_t), hipHostMallocDefault), "batch flags");
+  }
+  if (!c->row_bits.p || c->row_bits.n < (size_t)(c->N / 32 + 1)) {
+    DM_HIP(c, c->row_bits.ensure((size_t)(c->N / 32 + 1)), "row bitmap");
+    DM_HIP(c, hipMemsetAsync(c->row_bits.p, 0, c->row_bits.n * sizeof(uint32_t), st), "row bitmap");
+  }
+  DM_HIP(c, hipMemsetAsync(c->bat_flags.p, 0, 3 * sizeof(uint32_t), st), "batch flags");
+  uint32_t* F = c->bat_flags.p;
+  // copies, back to back
+  if (nw > 0) {
+    DM_HIP(c, c->st_mask.ensure((size_t)nw), "stage mask");
+    DM_HIP(c, c->st_mwants.ensure((size_t)std::max<int64_t>(nm, 1)), "stage wants");
+    DM_HIP(c, c->st_blk.ensure((size_t)((nw + 255) / 256)), "stage block sums");
+    DM_HIP(c, c->st_wpre.ensure((size_t)nw), "stage word offsets");
+    DM_HIP(c, hipMemcpyAsync(c->st_mask.p, b->wants_mask, (size_t)nw * 8, hipMemcpyHostToDevice, cp), "stage mask");
+    if (nm > 0)
+      DM_HIP(c, hipMemcpyAsync(c->st_mwants.p, b->wants, (size_t)nm * 8, hipMemcpyHostToDevice, cp), "stage wants");
+    DM_HIP(c, hipEventRecord(c->ev_bat[0], cp), "stage");
+  }
+  if (nr > 0) {
+    DM_HIP(c, c->st_rel.ensure((size_t)nr), "stage release rows");
+    DM_HIP(c, hipMemcpyAsync(c->st_rel.p, b->release_rows, (size_t)nr * 8, hipMemcpyHostToDevice, cp), "stage rows");
+    DM_HIP(c, hipEventRecord(c->ev_bat[1], cp), "stage");
+  }
+  if (nu > 0) {
+    DM_HIP(c, c->st_rows.ensure((size_t)nu), "stage rows");
+    DM_HIP(c, c->st_has.ensure((size_t)nu), "stage has");
+    DM_HIP(c, c->st_wants.ensure((size_t)nu), "stage wants");
+    DM_HIP(c, c->st_sub.ensure((size_t)nu), "stage sub");
+    DM_HIP(c, c->st_exp.ensure((size_t)nu), "stage expiry");
+    const StageCol cols[] = {{c->st_rows.p, b->upsert_rows, 8}, {c->st_wants.p, b->upsert_wants, 8},
+                             {c->st_sub.p, b->upsert_subclients, 8}, {c->st_has.p, b->upsert_has, 8},
+                             {c->st_exp.p, b->upsert_expiry_ns, 8}};
+    for (const auto& col : cols)
+      DM_HIP(c, hipMemcpyAsync(col.dst, col.src, (size_t)nu * col.elem, hipMemcpyHostToDevice, cp), "stage upsert");
+    DM_HIP(c, hipEventRecord(c->ev_bat[2], cp), "stage");
+  }
+  // part 1: wants refresh (validated by its count/scan passes before the apply)
+  if (nw > 0) {
+    DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[0], 0), "stage");
+    DM_HIP(c, launch_update_wants_mask(nw, c->st_mask.p, b->wants_first_row, c->N, nm, c->st_mwants.p, c->st_blk.p,
+                                       c->st_wpre.p, c->row_index(), c->wants.p, c->agg.p, F + 0, st),
+           "masked update");
+  }
+  // part 2: departures
+  if (nr > 0) {
+    DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[1], 0), "stage");
+    DM_HIP(c, launch_check_rows(nr, c->st_rel.p, c->N, c->row_bits.p, nullptr, nullptr, F + 1, st), "check rows");
+    DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
+    DM_HIP(c, launch_release(nr, c->st_rel.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
+                             F + 1, st),
+           "release");
+    DM_HIP(c, launch_clear_rows(nr, c->st_rel.p, c->N, c->row_bits.p, st), "clear rows");
+  } else {
+    DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
+  }
+  // part 3: arrivals / full refreshes
+  if (nu > 0) {
+    DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[2], 0), "stage");
+    DM_HIP(c, launch_check_rows(nu, c->st_rows.p, c->N, c->row_bits.p, c->st_wants.p, c->st_sub.p, F + 2, st),
+           "check rows");
+    DM_HIP(c, launch_carry_reject(F + 1, F + 2, st), "carry");
+    DM_HIP(c, launch_upsert(nu, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->row_index(),
+                            c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, F + 2, st),
+           "upsert");
+    DM_HIP(c, launch_clear_rows(nu, c->st_rows.p, c->N, c->row_bits.p, st), "clear rows");
+  }
+  DM_HIP(c, hipMemcpyAsync(c->h_bat_flags, F, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "batch flags");
+  DM_HIP(c, hipStreamSynchronize(st), "batch");
+  c->have_result = false;
+  const uint32_t f0 = c->h_bat_flags[0], f1 = c->h_bat_flags[1], f2 = c->h_bat_flags[2];
+  auto reject = [&](uint32_t f, const char* part) -> int {
+    const std::string p(part);
+    if (f & kUpdRange) return c->fail(DM_E_RANGE, p + ": row out of range");
+    if (f & kUpdCount) return c->fail(DM_E_INVAL, p + ": packed values must match the mask's set bits");
+    if (f & kUpdDup) return c->fail(DM_E_INVAL, p + ": rows must be unique within one part");
+    return c->fail(DM_E_INVAL, p + ": subclients must be in [0, 2^31-1]");
+  };
+  if (f0 & kUpdReject) return reject(f0, "wants refresh");
+  if (f0 & kUpdNaN) c->maybe_general = true;
+  if (f1 & kUpdReject) return reject(f1, "release");
+  if (f2 & kUpdReject) return reject(f2, "upsert");
+  if (nu > 0) {
+    if ((f2 & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one) c->maybe_general = true;
+    if (f2 & kUpdNotOne) c->all_sub_one = false;
+  }
   return DM_OK;
 }
 

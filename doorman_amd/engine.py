@@ -151,6 +151,32 @@ class Engine:
         self._chk(self._L.dm_store_update_wants_mask(self._ctx, int(first_row), len(mask), _ptr(mask), len(wants),
                                                      _ptr(wants)))
 
+    def apply(self, wants_mask=None, wants=None, release_rows=None, upsert=None, wants_first_row: int = 0):
+        """dm_store_apply: one round's refresh (row mask + packed wants), departures and
+        arrivals (upsert = (rows, has, wants, subclients, expiry_ns)) in one call."""
+        keep = []
+
+        def col(a, dt):
+            a = _c(a, dt)
+            keep.append(a)
+            return a
+
+        b = _lib.StoreBatch()
+        if wants_mask is not None:
+            m, w = col(wants_mask, np.uint64), col(wants if wants is not None else [], np.float64)
+            b.wants_first_row, b.wants_nwords, b.wants_mask = int(wants_first_row), len(m), _ptr(m)
+            b.wants_n, b.wants = len(w), _ptr(w)
+        if release_rows is not None:
+            r = col(release_rows, np.int64)
+            b.release_n, b.release_rows = len(r), _ptr(r)
+        if upsert is not None:
+            rows, has, wv, sub, exp = upsert
+            rows = col(rows, np.int64)
+            b.upsert_n, b.upsert_rows = len(rows), _ptr(rows)
+            b.upsert_has, b.upsert_wants = _ptr(col(has, np.float64)), _ptr(col(wv, np.float64))
+            b.upsert_subclients, b.upsert_expiry_ns = _ptr(col(sub, np.int64)), _ptr(col(exp, np.int64))
+        self._chk(self._L.dm_store_apply(self._ctx, ctypes.byref(b)))
+
     def release(self, rows):
         """Release (store.go:142-151)."""
         rows = _c(rows, np.int64)

@@ -104,6 +104,28 @@ typedef struct {
   const double* safe_capacity;      /* ResourceTemplate.safe_capacity; NaN = unset */
 } dm_resource_cfg;
 
+/* One round of store updates (dm_store_apply): the parts are applied in this order,
+   each exactly as the single call named beside it; a part with n == 0 (or
+   wants_nwords == 0) is skipped.  All parts' columns cross PCIe back to back on the
+   copy stream, so a part's validation and apply overlap the later parts' copies. */
+typedef struct {
+  /* refresh of existing clients' wants (dm_store_update_wants_mask) */
+  int64_t wants_first_row, wants_nwords;
+  const uint64_t* wants_mask;
+  int64_t wants_n;
+  const double* wants;
+  /* departures (dm_store_release) */
+  int64_t release_n;
+  const int64_t* release_rows;
+  /* arrivals and full refreshes (dm_store_upsert) */
+  int64_t upsert_n;
+  const int64_t* upsert_rows;
+  const double* upsert_has;
+  const double* upsert_wants;
+  const int64_t* upsert_subclients;
+  const int64_t* upsert_expiry_ns;
+} dm_store_batch;
+
 typedef struct {
   const char* name;
   int64_t launches;
@@ -144,6 +166,10 @@ int dm_store_update_wants_mask(dm_ctx* ctx, int64_t first_row, int64_t nwords, c
 /* Release (store.go:142-151): sums -= row; row zeroed and marked DM_RELEASED.  A released
  * row is a free slot: dm_store_upsert onto it is Assign of a new client. */
 int dm_store_release(dm_ctx* ctx, int64_t n, const int64_t* rows);
+/* The three update kinds of one round in one call (see dm_store_batch).  Parts run
+   in order; the first rejected part returns its error, earlier parts stay applied
+   and later ones are not applied.  Synchronous on return, like the single calls. */
+int dm_store_apply(dm_ctx* ctx, const dm_store_batch* batch);
 /* The three update calls validate on the device (rows in [0, N), unique within the
  * call, subclients in [0, 2^31)); a rejected call (DM_E_RANGE / DM_E_INVAL) leaves the
  * store untouched.  They return after the update is applied, so the caller may reuse

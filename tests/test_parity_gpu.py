@@ -598,3 +598,77 @@ def test_update_wants_mask_rejects_bad_input(eng):
     after, res1 = eng.read_store(), eng.resources(safe=False)
     assert after["wants"].tobytes() == before["wants"].tobytes()
     assert res1["sum_wants"].tobytes() == res0["sum_wants"].tobytes()
+
+
+def _round_parts(rng, snap):
+    N = len(snap["wants"])
+    alive = np.flatnonzero(snap["expiry_ns"] != W.RELEASED)
+    upd = np.sort(rng.choice(alive, len(alive) // 9, replace=False))
+    rest = np.setdiff1d(alive, upd)
+    gone = np.sort(rng.choice(rest, len(alive) // 50, replace=False))
+    new = np.sort(rng.choice(np.setdiff1d(np.arange(N), np.concatenate([upd, gone])), len(gone), replace=False))
+    k = len(new)
+    ups = (new, rng.uniform(0, 2, k), rng.uniform(0.5, 1.5, k), np.ones(k, np.int64), np.full(k, NOW + 900 * W.NS))
+    return upd, rng.uniform(0.5, 1.5, len(upd)), gone, ups
+
+
+def test_store_apply_matches_sequential_calls(eng):
+    """dm_store_apply (refresh mask + departures + arrivals in one call, copies back
+    to back) leaves the store of the three single calls; the next tick matches the
+    oracle."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(41)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng), expired_frac=0.0)
+    N = len(snap["wants"])
+    cap = np.maximum(snap["capacity"], 1.0)
+    upd, w, gone, ups = _round_parts(rng, snap)
+    other = Engine(0)
+    try:
+        eng.load(snap)
+        other.load(snap)
+        eng.apply(W.rows_to_mask(upd, N), w, gone, ups)
+        other.update_wants(upd, w)
+        other.release(gone)
+        other.upsert(*ups)
+        s1, s2 = eng.read_store(), other.read_store()
+        for k in ("has", "wants", "subclients", "expiry_ns"):
+            assert s1[k].tobytes() == s2[k].tobytes(), k
+        r1, r2 = eng.resources(safe=False), other.resources(safe=False)
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        for k in ("sum_has", "sum_wants"):
+            assert float_close(r1[k], r2[k], cap, 1e-12).all(), k
+        ref_snap = dict(snap)
+        ref_snap.update(has=s1["has"], wants=s1["wants"], subclients=s1["subclients"], expiry_ns=s1["expiry_ns"],
+                        agg_count=r1["count"], agg_sum_has=r1["sum_has"], agg_sum_wants=r1["sum_wants"])
+        eng.apportion(NOW)
+        gets, exp = eng.leases()
+        assert_leases_match(ref_snap, gets, exp, O.apportion(ref_snap, NOW), "after dm_store_apply")
+    finally:
+        other.close()
+
+
+def test_store_apply_stops_at_the_first_rejected_part(eng):
+    """A rejected part (duplicate departure rows) returns its error; the refresh before
+    it stays applied, the arrivals after it are not; a bad mask rejects everything."""
+    from doorman_amd._lib import DM_E_INVAL, DmError
+    rng = np.random.default_rng(42)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=False), expired_frac=0.0)
+    N = len(snap["wants"])
+    upd, w, gone, ups = _round_parts(rng, snap)
+    eng.load(snap)
+    before = eng.read_store()
+    with pytest.raises(DmError) as e:
+        eng.apply(W.rows_to_mask(upd, N), w, np.concatenate([gone, gone[:1]]), ups)
+    assert e.value.code == DM_E_INVAL and "release" in str(e.value)
+    st = eng.read_store()
+    exp_w = before["wants"].copy()
+    exp_w[upd] = w
+    assert st["wants"].tobytes() == exp_w.tobytes()  # refresh applied, arrivals' wants not
+    assert st["expiry_ns"].tobytes() == before["expiry_ns"].tobytes()  # no departure, no arrival
+    eng.load(snap)
+    with pytest.raises(DmError) as e:
+        eng.apply(W.rows_to_mask(upd, N), w[:-1], gone, ups)
+    assert e.value.code == DM_E_INVAL
+    st = eng.read_store()
+    for k in ("has", "wants", "subclients", "expiry_ns"):
+        assert st[k].tobytes() == before[k].tobytes(), k
