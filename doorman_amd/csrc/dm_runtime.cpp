@@ -690,7 +690,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
   const bool general = c->maybe_general && c->n_nonsmall > 0;
-  if (c->maybe_general) {
+  if (general) {  // only non-small resources are ever appended to the worklist
     DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
     c->main_dirty = true;
   }

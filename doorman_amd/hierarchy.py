@@ -76,16 +76,21 @@ class HierarchicalTick:
         dev = torch.device("cuda", torch.cuda.current_device())
         self.totals = torch.empty((self.R, 2), dtype=torch.float64, device=dev)
         self.gathered = torch.empty((self.G * self.R, 2), dtype=torch.float64, device=dev)
-        stream = torch.cuda.current_stream().cuda_stream
-        # the library's kernels and torch's collectives share one stream: ordered
-        leaf.set_stream(stream)
-        root.set_stream(stream)
+        # The library's kernels and torch's collective share ONE stream, so publish ->
+        # all-gather -> root -> grants -> leaf tick are ordered without host syncs.  It
+        # is a stream of its own: torch's default stream is the HIP null stream, which
+        # dm_set_stream cannot select (NULL restores the context's own stream) and
+        # which does not order the library's non-blocking streams.
+        self.stream = torch.cuda.Stream(device=dev)
+        leaf.set_stream(self.stream.cuda_stream)
+        root.set_stream(self.stream.cuda_stream)
 
     def exchange(self, now_ns: int):
         """publish -> all-gather -> root apportionment -> take this server's grants."""
         from . import _lib
         self.leaf.publish_totals(self.totals.data_ptr())
-        self.gather(self.totals, self.gathered)
+        with self.torch.cuda.stream(self.stream):  # the collective orders with our stream
+            self.gather(self.totals, self.gathered)
         L = self.root._L
         _lib.check(L.dm_hier_load_root(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns)),
                    self.root._ctx, L)

@@ -138,7 +138,9 @@ int dm_device_count(int* out);
 int dm_create(int device, dm_ctx** out);
 void dm_destroy(dm_ctx* ctx);
 const char* dm_last_error(dm_ctx* ctx);
-/* use an existing hipStream_t (e.g. the caller's current stream); NULL = the context's own */
+/* use an existing hipStream_t (e.g. the caller's current stream); NULL = the context's own.
+   The HIP null stream therefore cannot be selected: a caller whose current stream is the
+   null stream (torch's default) must create a stream to share (doorman_amd/hierarchy.py). */
 int dm_set_stream(dm_ctx* ctx, void* hip_stream);
 void* dm_get_stream(dm_ctx* ctx);
 int dm_sync(dm_ctx* ctx);

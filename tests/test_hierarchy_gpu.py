@@ -71,3 +71,40 @@ def test_hierarchy_round(G):
         assert_leases_match(leaf, gets2, exp2, O.apportion(leaf, later), f"leaf {g} after parent expiry")
     for e in leaves + [root]:
         e.close()
+
+
+def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
+    """HierarchicalTick orders publish -> gather -> root -> grants -> leaf tick on one
+    stream (not torch's null stream, which dm_set_stream cannot select): three
+    asynchronous steps leave the same leaf leases as the same steps run with a sync
+    after every stage."""
+    import torch
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    R = 300
+    snap = W.uniform(R, 200, kind=W.FAIR_SHARE, seed=77, capacity=1000.0)
+
+    def gather(src, dst):
+        dst.copy_(src)
+
+    outs = []
+    for sync_each in (False, True):
+        leaf, root = Engine(0), Engine(0)
+        leaf.load(snap)
+        root.load(H.root_snapshot(R, 1, W.FAIR_SHARE, np.asarray(snap["capacity"]), lease_length_s=20))
+        ht = H.HierarchicalTick(torch, leaf, root, R, 1, 0, gather)
+        assert leaf.stream == root.stream == ht.stream.cuda_stream != 0
+        for t in range(3):
+            if sync_each:
+                ht.exchange(NOW + t * W.NS)
+                leaf.sync()
+                root.sync()
+                leaf.apportion(NOW + t * W.NS, writeback=True)
+            else:
+                ht.tick(NOW + t * W.NS, asynchronous=True)
+        leaf.sync()
+        outs.append(leaf.leases())
+        leaf.close()
+        root.close()
+    (g1, e1), (g2, e2) = outs
+    assert g1.tobytes() == g2.tobytes() and e1.tobytes() == e2.tobytes()
