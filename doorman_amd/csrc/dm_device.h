@@ -140,4 +140,13 @@ struct DevParams {
   int32_t pad;
 };
 
+// dm_hier_root_tick: the fused root-store tick of the hierarchy (k_small_t<true>)
+struct HierArgs {
+  const double2* gathered;  // [G][R] {SumWants, Count as bits} (k_publish records)
+  ResCfg* leaf_cfg;         // this server's leaf template
+  int64_t R;
+  int G;
+  int server;
+};
+
 }  // namespace dm

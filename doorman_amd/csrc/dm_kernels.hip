@@ -573,7 +573,14 @@ __global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __rest
 __device__ __forceinline__ int shfl_i(int v, int lane) { return __shfl(v, lane, 64); }
 __device__ __forceinline__ double shfl_d(double v, int lane) { return shfl_any(v, lane); }
 
-__global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restrict__ packs, int npacks) {
+// HIER: the root store of the intermediate-server hierarchy (R resources x G server
+// rows, row = r*G + g), fused with what dm_hier_load_root and dm_hier_take_grants do
+// around it: every row's request comes from the gathered totals (k_hier_root's rule)
+// and is stored, and this server's grants go straight into the leaf's config
+// (k_hier_grants' rule).  One launch instead of three per hierarchy exchange.
+template <bool HIER>
+__global__ __launch_bounds__(256) void k_small_t(DevParams p, const Pack* __restrict__ packs, int npacks,
+                                                 HierArgs ha) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wv >= npacks) return;
   const int lane = threadIdx.x & 63;
@@ -588,10 +595,34 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   int64_t e = 0;
   if (nrows > 0) {
     const int64_t row = row0 + (valid ? lane : nrows - 1);
-    w = p.wants[row];
-    h = p.has[row];
-    s = p.sub[row];
-    e = p.expiry[row];
+    if constexpr (HIER) {
+      const int64_t r = row / ha.G;
+      const int g = (int)(row - r * ha.G);
+      const double2 v = ha.gathered[(int64_t)g * ha.R + r];
+      const long long count = __double_as_longlong(v.y);
+      const int64_t e_old = p.expiry[row];
+      h = p.has[row];
+      if (v.x > 0.0 && count >= 1) {  // a request (server.go:241, :863-866)
+        w = v.x;
+        s = (int)(count < INT32_MAX ? count : INT32_MAX);
+        if (e_old == kReleased) h = 0.0;  // a new lease has nothing yet
+        e = p.now;                        // refreshing now: live for this tick's Clean
+      } else {
+        w = 0.0;
+        h = 0.0;
+        s = 0;
+        e = kReleased;
+      }
+      if (valid) {  // the root store keeps the requests (dm_hier_load_root)
+        p.out_wants[row] = w;
+        p.out_sub[row] = s;
+      }
+    } else {
+      w = p.wants[row];
+      h = p.has[row];
+      s = p.sub[row];
+      e = p.expiry[row];
+    }
   }
   // resource of this row: last k < nseg with rel[k] <= lane (offsets relative to row0)
   const int offk = lane <= nseg ? (int)pkr.rel[lane] : INT32_MAX;
@@ -708,6 +739,15 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
       }
     }
     if (need2) g = fs_stage2(w, h, s, C, sh, eq, x, wi, T, c);
+  }
+  if constexpr (HIER) {  // this server's grant -> the leaf's template (server.go:284-296)
+    if (valid && lv && (int)((row0 + lane) % ha.G) == ha.server) {
+      const int64_t r = (row0 + lane) / ha.G;
+      const int64_t ex = rs.exp_out;
+      const int64_t sec = ex >= 0 ? ex / kNs : -((-ex + kNs - 1) / kNs);  // time.Unix(sec, 0)
+      ha.leaf_cfg[r].capacity = g;
+      ha.leaf_cfg[r].parent_expiry_ns = sec * kNs;
+    }
   }
   if (valid) {
     if (lv) {
@@ -1650,7 +1690,7 @@ __global__ void k_hier_grants(int64_t R, int G, int g, const double* __restrict_
 // --------------------------------------------------------------------------
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_small<<<(n + 3) / 4, 256, 0, st>>>(p, packs, n);
+  k_small_t<false><<<(n + 3) / 4, 256, 0, st>>>(p, packs, n, HierArgs{});
   return hipGetLastError();
 }
 
@@ -1771,6 +1811,12 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
 
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st) {
   k_carry_reject<<<1, 1, 0, st>>>(from, to);
+  return hipGetLastError();
+}
+
+hipError_t launch_small_hier(const DevParams& p, const Pack* packs, int n, const HierArgs& ha, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_small_t<true><<<(n + 3) / 4, 256, 0, st>>>(p, packs, n, ha);
   return hipGetLastError();
 }
 

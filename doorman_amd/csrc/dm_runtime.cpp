@@ -41,6 +41,7 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
+hipError_t launch_small_hier(const DevParams& p, const Pack* packs, int n, const HierArgs& ha, hipStream_t st);
 hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
                             int64_t* r_exp, int64_t now, hipStream_t st);
 hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
@@ -1227,6 +1228,62 @@ int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server) {
     DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
     DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
   }
+  return DM_OK;
+}
+
+// dm_hier_load_root + dm_apportion(WRITEBACK | AGG_RECOMPUTE) + dm_hier_take_grants in
+// one launch when every root resource is small (G <= kSmallMax servers: the
+// wave-packed path evaluates each server row literally): k_small_t<true> reads the
+// requests straight from the gathered records and writes this server's grants into
+// the leaf's config.  Otherwise the three calls run in turn.
+int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns, dm_ctx* leaf, int server) {
+  DM_ENTER(root);
+  if (!root->store_loaded || !root->cfg_loaded) return root->fail(DM_E_STATE, "root store / config not loaded");
+  if (!gathered || !leaf) return root->fail(DM_E_INVAL, "null gathered buffer or leaf context");
+  if (!root_layout_ok(root, n_servers))
+    return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows");
+  if (server < 0 || server >= n_servers) return root->fail(DM_E_RANGE, "server index out of range");
+  if (leaf->device != root->device) return root->fail(DM_E_INVAL, "root and leaf contexts must share a device");
+  if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
+  bool fused = n_servers <= kSmallMax && root->h_chunks.empty();
+  for (int b = 0; b < kNumBins; ++b) fused = fused && root->h_bins[b].empty();
+  if (!fused) {
+    int rc = dm_hier_load_root(root, gathered, n_servers, now_ns);
+    if (!rc) rc = dm_apportion(root, now_ns, DM_WRITEBACK | DM_AGG_RECOMPUTE | DM_ASYNC);
+    if (!rc) rc = dm_hier_take_grants(root, leaf, server);
+    return rc;
+  }
+  DM_HIP(root, leaf->join_aux(), "join leaf streams");
+  leaf->main_dirty = true;
+  const bool same = root->stream == leaf->stream;
+  if (!same) {  // root after the leaf's prior work (its config is written)
+    DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
+    DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
+  }
+  DevParams p{};
+  p.seg_off = root->seg_off.p;
+  p.wants = root->wants.p;
+  p.has = root->has.p;
+  p.sub = root->sub.p;
+  p.expiry = root->expiry.p;
+  p.cfg = root->cfg.p;
+  p.agg = root->agg.p;
+  p.out_gets = root->has.p;  // writeback in place (a root store is small)
+  p.out_expiry = root->expiry.p;
+  p.out_wants = root->wants.p;
+  p.out_sub = root->sub.p;
+  p.res = root->agg.p;
+  p.now = now_ns;
+  p.recompute = 1;
+  const HierArgs ha{(const double2*)gathered, leaf->cfg.p, root->R, n_servers, server};
+  DM_HIP(root, launch_small_hier(p, root->packs.p, (int)root->h_packs.size(), ha, root->stream), "hier root tick");
+  if (!same) {  // the leaf's next tick after its new template
+    DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
+    DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
+  }
+  root->maybe_general = true;  // rows carry heterogeneous subclient counts
+  root->last_writeback = true;
+  root->have_result = true;
   return DM_OK;
 }
 

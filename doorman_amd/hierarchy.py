@@ -92,10 +92,9 @@ class HierarchicalTick:
         with self.torch.cuda.stream(self.stream):  # the collective orders with our stream
             self.gather(self.totals, self.gathered)
         L = self.root._L
-        _lib.check(L.dm_hier_load_root(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns)),
-                   self.root._ctx, L)
-        self.root.apportion(now_ns, writeback=True, recompute=True, asynchronous=True)
-        _lib.check(L.dm_hier_take_grants(self.root._ctx, self.leaf._ctx, self.g), self.root._ctx, L)
+        # load_root + root apportionment + take_grants (one launch for G <= 8)
+        _lib.check(L.dm_hier_root_tick(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns),
+                                       self.leaf._ctx, self.g), self.root._ctx, L)
 
     def tick(self, now_ns: int, asynchronous: bool = False):
         self.exchange(now_ns)

@@ -219,6 +219,11 @@ int dm_hier_load_root(dm_ctx* root, const void* dev_gathered, int n_servers, int
  * capacity and the grant's expiry (Unix seconds) as parent expiry; resources it did not
  * request keep their template.  Both contexts must be on the same device. */
 int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server);
+/* One hierarchy exchange's root work: dm_hier_load_root, dm_apportion(root, WRITEBACK |
+   AGG_RECOMPUTE | ASYNC) and dm_hier_take_grants(root, leaf, server) -- fused into one
+   kernel launch when n_servers <= 8, else those three calls in turn.  Stream-ordered. */
+int dm_hier_root_tick(dm_ctx* root, const void* dev_gathered, int n_servers, int64_t now_ns, dm_ctx* leaf,
+                      int server);
 
 /* ---- profiling ---- */
 int dm_set_profiling(dm_ctx* ctx, int on);

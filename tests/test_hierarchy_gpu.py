@@ -108,3 +108,48 @@ def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
         root.close()
     (g1, e1), (g2, e2) = outs
     assert g1.tobytes() == g2.tobytes() and e1.tobytes() == e2.tobytes()
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 8, 20])
+def test_hier_root_tick_matches_separate_calls(G):
+    """dm_hier_root_tick (one fused launch for G <= 8, the three calls above) leaves
+    the root store, its running sums and the leaf's template exactly as
+    dm_hier_load_root + dm_apportion(WRITEBACK | AGG_RECOMPUTE) + dm_hier_take_grants;
+    two rounds, so the second sees the first's root leases."""
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    R = 257
+    rng = np.random.default_rng(100 + G)
+    snap = W.uniform(R, 40, kind=W.FAIR_SHARE, seed=5 + G, capacity=1000.0)
+    rec = np.empty((G * R, 2))
+    rec[:, 0] = rng.uniform(0.0, 600.0, G * R) * (rng.random(G * R) > 0.1)
+    rec[:, 1] = rng.integers(0, 50, G * R).astype(np.int64).view(np.float64)
+    gathered = torch.from_numpy(rec).to("cuda")
+    L = _lib.lib()
+    outs = []
+    for fused in (True, False):
+        leaf, root = Engine(0), Engine(0)
+        leaf.load(snap)
+        root.load(H.root_snapshot(R, G, W.FAIR_SHARE, np.asarray(snap["capacity"]) * G, lease_length_s=20))
+        for t in range(2):
+            now = NOW + t * W.NS
+            server = (t + G - 1) % G
+            if fused:
+                _lib.check(L.dm_hier_root_tick(root._ctx, gathered.data_ptr(), G, now, leaf._ctx, server), root._ctx)
+            else:
+                _lib.check(L.dm_hier_load_root(root._ctx, gathered.data_ptr(), G, now), root._ctx)
+                root.apportion(now, writeback=True, recompute=True)
+                _lib.check(L.dm_hier_take_grants(root._ctx, leaf._ctx, server), root._ctx)
+        root.sync()
+        leaf.apportion(NOW + W.NS, writeback=False)
+        outs.append((root.read_store(), root.resources(safe=False), leaf.leases()))
+        leaf.close()
+        root.close()
+    (s1, r1, l1), (s2, r2, l2) = outs
+    for k in ("has", "wants", "subclients", "expiry_ns"):
+        assert s1[k].tobytes() == s2[k].tobytes(), k
+    for k in ("count", "sum_has", "sum_wants"):
+        assert r1[k].tobytes() == r2[k].tobytes(), k
+    assert l1[0].tobytes() == l2[0].tobytes() and l1[1].tobytes() == l2[1].tobytes()
