@@ -3,18 +3,25 @@
 One step = one apportionment tick over every lease of the rank's store: the
 device-resident snapshot is decided (Clean, learning mode, the resource's
 algorithm) and written back (DM_WRITEBACK), inputs already resident in HBM.
+With the hierarchy on (the default for the north-star workload c3), every step
+first runs the intermediate-server exchange (publish per-resource totals, one
+all-gather over RCCL, the root's apportionment, this server's grants).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c1ps|c2|c3]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c1ps|c2|c3|c4] [--hier on|off|auto]
 
-For N > 1 it runs under torch.distributed.run, one rank per GPU; resources are
-sharded by id (each rank owns its own shard of the workload: weak scaling, no
-data-path collective).  Rank 0 prints one JSON line.
+--gpus N > 1 without a torch.distributed environment starts N ranks itself
+(python -m torch.distributed.run, one process per GPU, started before this
+process touches the GPU) and exits with their status.  Under torchrun each rank
+owns one GPU and its own store (weak scaling: a full C3-shaped store per GPU).
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,12 +33,14 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 HBM_COPY_CEIL_GBS = 6290.0  # measured float4 copy ceiling (same table)
 METRIC = "client leases apportioned/sec (whole node) + % HBM peak, FairShare, 1-8 GPU"
+DEFAULT_WORKLOAD = "c3"
 
 WORKLOADS = {
     "c1": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), FairShare, uniform wants",
     "c1ps": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), ProportionalShare",
     "c2": "C2 (BASELINE configs[2]): 1M resources, Zipf 1..1M clients (13,970,034 leases), mixed kinds, 5% learning",
-    "c3": "C3 shape on one GPU (north-star target): 100,000 resources x 1,000 clients (100M leases), FairShare",
+    "c3": "C3 (BASELINE configs[3], north-star size): 100,000 resources x 1,000 clients = 100M leases per GPU, "
+          "FairShare",
     "c4": "C4 (BASELINE configs[4]) per GPU: 125M-lease device-resident store (1B over 8 GPUs), 125k resources x "
           "1k client slots, FS/PS mixed, 5% learning; every step = 5 s refresh tick: 10% wants updates and 1% "
           "departures + 1% new clients over PCIe, then the tick",
@@ -75,10 +84,9 @@ def algorithmic_bytes(n_leases: int, n_resources: int) -> int:
     return LEASE_BYTES * n_leases + 64 * n_resources
 
 
-def kernel_units(eng, snap):
+def kernel_units(snap):
     """(leases, resources) each kernel class of the plan processes per launch."""
-    so = snap["seg_off"]
-    sizes = np.diff(so)
+    sizes = np.diff(snap["seg_off"])
     units = {}
     edges = [("group16", 9, 16), ("group32", 17, 32), ("wave64x1", 33, 64), ("wave64x2", 65, 128),
              ("wave64x4", 129, 256), ("block256x2", 257, 512), ("block256x4", 513, 1024), ("block512x4", 1025, 2048),
@@ -143,6 +151,46 @@ def streaming_step(eng, snap, rank, n_ticks):
     return step
 
 
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's algorithm restated in C
+# (oracle/, test infrastructure), timed on this host's cores.
+# ---------------------------------------------------------------------------
+def host_cores():
+    """CPUs this process may actually use: the scheduler affinity, capped by the
+    cgroup CPU quota (a GPU box grants one GPU's share of a large host) and by
+    OMP_NUM_THREADS when the environment sets it (the box does: its CPU share)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = usable
+    if quota:
+        n = min(n, quota)
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n), {"usable_cores": usable, "cgroup_cpu_quota": quota, "omp_num_threads": env}
+
+
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
 def subset_rows(snap, max_rows):
     """the leading resources of a snapshot holding at most max_rows leases"""
     from doorman_amd import workloads as W
@@ -152,32 +200,33 @@ def subset_rows(snap, max_rows):
 
 
 def cpu_baseline(snap, now_ns, budget_s=12.0):
-    """Reference algorithm restated in C (oracle, literal per-request Resource.Decide on a
-    private copy of the store, single thread), timed on a bounded sample of this workload."""
+    """The reference algorithm restated in C, timed on a bounded sample of this
+    workload at the host's width:
+      value          literal per-request Resource.Decide on a private store copy (O(n) per
+                     request, as the reference), OpenMP pool over resources;
+      closed_form_mt the closed form (SURVEY.md §8a, same outputs) over all resources;
+      configs0       BASELINE configs[0] (1 resource x 1,000 clients, ProportionalShare)."""
+    from doorman_amd import workloads as W
     from oracle import oracle as O
+    threads, cores = host_cores()
     so = snap["seg_off"]
     sizes = np.diff(so)
-    order = np.argsort(-sizes, kind="stable")
-    # sample whole resources from the middle of the size distribution up to the budget
     rng = np.random.default_rng(0)
     cand = rng.permutation(np.flatnonzero(sizes > 0))
+    row_cap = 4000  # O(n^2) per resource: a slice of clients of the giant resources
     gets = np.empty(len(snap["wants"]))
-    done_rows, t_total, used = 0, 0.0, []
-    for r in cand:
-        n = int(sizes[r])
-        lo, hi = int(so[r]), int(so[r + 1])
-        if n > 4000:  # O(n^2) per resource: take a slice of clients of the big resources
-            hi = lo + 4000
-        t0 = time.perf_counter()
-        done_rows += O.apportion_literal_rows(snap, int(r), lo, hi, now_ns, gets)
-        t_total += time.perf_counter() - t0
-        used.append(int(r))
-        if t_total > budget_s:
-            break
-    del order
-    # SURVEY.md §8(d)(iii): the closed form (same outputs) over all resources on the
-    # host's cores, the optimised-CPU comparator, timed on the whole snapshot
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    # calibrate on a small batch, then one batch sized to the budget
+    k0 = min(len(cand), 4 * threads)
+    t0 = time.perf_counter()
+    O.apportion_literal_sample(snap, cand[:k0], row_cap, now_ns, gets, threads)
+    t_cal = time.perf_counter() - t0
+    k1 = int(min(len(cand) - k0, max(threads, k0 * max(budget_s - t_cal, 0.0) / max(t_cal, 1e-3))))
+    t0 = time.perf_counter()
+    rows = O.apportion_literal_sample(snap, cand[k0:k0 + k1], row_cap, now_ns, gets, threads) if k1 > 0 else 0
+    t_lit = time.perf_counter() - t0
+    if k1 <= 0:
+        rows, t_lit, k1 = O.apportion_literal_sample(snap, cand[:k0], row_cap, now_ns, gets, threads), t_cal, k0
+    # the closed form over the whole snapshot
     O.apportion(subset_rows(snap, 2000), now_ns, "closed", threads=threads)  # warm the pool
     reps, t_mt = 0, 0.0
     while reps < 3 and t_mt < 5.0:
@@ -185,40 +234,133 @@ def cpu_baseline(snap, now_ns, budget_s=12.0):
         O.apportion(snap, now_ns, "closed", threads=threads)
         t_mt += time.perf_counter() - t0
         reps += 1
+    # configs[0]: the reference's own CPU case, single resource (one thread: one store)
+    c0 = W.c0()
+    n0 = len(c0["wants"])
+    g0 = np.empty(n0)
+    reps0, t0s = 0, 0.0
+    while t0s < 1.0:
+        t0 = time.perf_counter()
+        O.apportion_literal_rows(c0, 0, 0, n0, now_ns, g0)
+        t0s += time.perf_counter() - t0
+        reps0 += 1
     return {
-        "value": done_rows / t_total if t_total > 0 else None,
+        "value": rows / t_lit if t_lit > 0 else None,
         "unit": "leases/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{done_rows} leases of {len(used)} resources of the same workload, each decided by the literal "
-                  f"C restatement of Resource.Decide (go/server/doorman/resource.go:100-113) on a private store copy "
-                  f"(O(n) per request as in the reference), single thread, {t_total:.1f} s",
+        "sample": f"{rows} leases of {k1} resources of the same workload (first {row_cap} clients of each), every "
+                  f"one decided by the literal C restatement of Resource.Decide (go/server/doorman/resource.go:100-113) "
+                  f"on a private store copy (O(n) per request as in the reference), OpenMP pool over resources on "
+                  f"{threads} threads, {t_lit:.1f} s",
         "closed_form_mt": {
             "value": reps * len(snap["wants"]) / t_mt,
             "unit": "leases/s",
             "cores": threads,
             "sample": f"whole snapshot x{reps}: oracle/ closed form (SURVEY.md §8a), OpenMP over resources",
         },
-        "host": host_info(),
+        "configs0": {
+            "value": reps0 * n0 / t0s,
+            "unit": "leases/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"BASELINE configs[0]: 1 resource x {n0} clients, ProportionalShare (workloads.c0), literal "
+                      f"per-request Decide x{reps0}, one thread (one store)",
+        },
+        "host": {**host_info(), **cores, "threads_used": threads},
     }
 
 
-def host_info():
-    """CPU model and core counts of the box the baseline ran on (SURVEY.md §8d asks
-    for them next to the Go reference's GOMAXPROCS, which has no counterpart here)."""
-    model = None
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except AttributeError:
-        usable = None
-    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cores": usable}
+# ---------------------------------------------------------------------------
+# timing
+# ---------------------------------------------------------------------------
+def timed_steps(torch, eng, step, steps, warmup, sync_ranks, extra_warm=True):
+    """W untimed warm-up steps, then more until ~0.3 s of ticks have run (the first
+    milliseconds of back-to-back ticks run ~10% slow: C3 measured 843 us/tick after 3
+    warm-up ticks, 765 after 30; the count is agreed over ranks), then K timed steps
+    between barrier + synchronize, then K profiled steps (HIP events around every
+    launch, on the stream each kernel runs on)."""
+    t_w = time.perf_counter()
+    for _ in range(max(warmup, 1)):
+        step()
+    eng.sync()
+    per_step = (time.perf_counter() - t_w) / max(warmup, 1)
+    extra = min(20000, int(0.3 / max(per_step, 1e-6))) if extra_warm else 0
+    extra = sync_ranks("max_int", extra)
+    for i in range(extra):
+        step()
+        if i % 8 == 7:
+            eng.sync()
+    eng.sync()
+    ext = torch.cuda.ExternalStream(eng.stream)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sync_ranks("barrier", None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(ext)
+    for _ in range(steps):
+        step()
+    eng.join()  # every class stream's work before the closing event
+    ev1.record(ext)
+    eng.sync()
+    torch.cuda.synchronize()
+    sync_ranks("barrier", None)
+    elapsed = time.perf_counter() - t0
+    stream_ms = ev0.elapsed_time(ev1)
+    eng.set_profiling(True)
+    eng.reset_kernel_times()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    ktimes = eng.kernel_times()
+    eng.set_profiling(False)
+    return {"elapsed": elapsed, "stream_ms": stream_ms, "ktimes": ktimes, "warm_run": max(warmup, 1) + extra}
+
+
+def roofline_of(workload, snap, run, steps, single_kernel_tick):
+    """Roofline object for the dominant kernel (largest share of in-stream time)."""
+    ktimes = run["ktimes"]
+    if not ktimes:
+        return None
+    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
+    name, (launches, total_ms) = max(ktimes.items(), key=lambda kv: kv[1][1])
+    avg_s = total_ms / launches / 1e3
+    single = single_kernel_tick and len(ktimes) == 1 and launches == steps
+    if single:  # one kernel per tick: HIP events around the timed region itself
+        avg_s = run["stream_ms"] / steps / 1e3
+    leases_k, res_k = kernel_units(snap).get(name, (N, R))
+    alg = algorithmic_bytes(leases_k, res_k)
+    achieved = alg / avg_s / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(name, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
+            "traffic_source": f"profiles/pmc_{workload}.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, calibrated)",
+            "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2),
+            "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
+            "timed_region_stream_us_per_step": round(run["stream_ms"] * 1e3 / steps, 2),
+            "duration_source": ("HIP event pair around the timed region on the kernel's stream (one kernel "
+                                "per tick)" if single else "HIP events around every launch, profiled region")}
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 outside torchrun: start N ranks with torch.distributed.run before
+    this process touches the GPU (a child process, never exec), return their status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -226,20 +368,28 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra C1 line of the default run")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on a node; gloo + --same-device rehearses N>1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
-    ap.add_argument("--hier", action="store_true",
+    ap.add_argument("--hier", default="auto", choices=["auto", "on", "off"],
                     help="every step runs the intermediate-server exchange first (SURVEY.md §8e, configs[3]): "
-                         "publish totals, RCCL all-gather, root apportionment, take grants, then the leaf tick")
+                         "publish totals, RCCL all-gather, root apportionment, take grants, then the leaf tick; "
+                         "auto = on for c3")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
+    hier = args.hier == "on" or (args.hier == "auto" and args.workload == "c3")
 
     import torch  # loaded first: libdoorman_hip then binds to torch's HIP runtime
     import torch.distributed as dist
@@ -247,11 +397,25 @@ def main():
     dev_index = 0 if args.same_device else local_rank
     torch.cuda.set_device(dev_index)
     gloo = args.dist_backend == "gloo"
+    dist_info = None
     if world > 1:
         if gloo:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "device": "cuda:0 for every rank (rehearsal)" if args.same_device else "cuda:LOCAL_RANK"}
+    red_dev = "cpu" if gloo else "cuda"
+
+    def sync_ranks(what, v):
+        if world <= 1:
+            return v
+        if what == "barrier":
+            dist.barrier()
+            return v
+        t = torch.tensor([v], dtype=torch.int64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
 
     from doorman_amd import workloads as W
     from doorman_amd.engine import Engine
@@ -262,16 +426,12 @@ def main():
     eng.load(snap)
     now = W.NOW_NS
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
     # back-to-back ticks: a forked tick's class streams join lazily (DM_DEFER_JOIN)
     step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
     root = None
     if args.workload == "c4":
         step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup)
-    if args.hier:
+    if hier:
         from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
         root = Engine(dev_index)
         root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world, lease_length_s=20))
@@ -289,88 +449,32 @@ def main():
         ht = HierarchicalTick(torch, eng, root, R, world, rank, gather)
         step = lambda: ht.tick(now, asynchronous=True)  # noqa: E731
 
-    # W warmup steps, then more untimed steps until ~0.3 s of ticks have run: the
-    # first few milliseconds of back-to-back ticks run ~10% slow (clock ramp; C3
-    # measured 843 us/tick after 3 warmup ticks, 765 after 30).  The extra count is
-    # agreed over ranks (the hierarchy's steps hold a collective).  C4's update
-    # batches are pre-generated per step, so it runs exactly W.
-    t_w = time.perf_counter()
-    for _ in range(max(args.warmup, 1)):
-        step()
-    eng.sync()
-    per_step = (time.perf_counter() - t_w) / max(args.warmup, 1)
-    extra = 0 if args.workload == "c4" else min(20000, int(0.3 / max(per_step, 1e-6)))
-    if world > 1:
-        ex = torch.tensor([extra], dtype=torch.int64, device="cpu" if gloo else "cuda")
-        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
-        extra = int(ex.item())
-    for i in range(extra):
-        step()
-        if i % 8 == 7:
-            eng.sync()
-    warm_run = max(args.warmup, 1) + extra
-    eng.sync()
-    # timed region: only a start/stop HIP event pair on the engine's stream
-    ext = torch.cuda.ExternalStream(eng.stream)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(ext)
-    for _ in range(args.steps):
-        step()
-    eng.join()  # every class stream's work before the closing event
-    ev1.record(ext)
-    eng.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    stream_ms = ev0.elapsed_time(ev1)
-    # profiled region (same steps): HIP events around every kernel launch, on the
-    # stream each kernel runs on, for the per-kernel roofline
-    eng.set_profiling(True)
-    eng.reset_kernel_times()
-    for _ in range(args.steps):
-        step()
-    eng.sync()
-    ktimes = eng.kernel_times()
-    eng.set_profiling(False)
-    red_dev = "cpu" if gloo else "cuda"
-    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4")
+    t = torch.tensor([run["elapsed"]], dtype=torch.float64, device=red_dev)
     n = torch.tensor([N], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
     t_max, n_total = float(t.item()), float(n.item())
+    roofline = roofline_of(args.workload, snap, run, args.steps,
+                           single_kernel_tick=not hier and args.workload != "c4")
+    if hier:
+        ht.check()  # any server whose request the root rejected (server.go:863-866) fails loudly
 
-    # dominant kernel: largest share of in-stream time
-    units = kernel_units(eng, snap)
-    dom = max(ktimes.items(), key=lambda kv: kv[1][1]) if ktimes else None
-    roofline = None
-    if dom:
-        name, (launches, total_ms) = dom
-        avg_s = total_ms / launches / 1e3
-        single = len(ktimes) == 1 and launches == args.steps and not args.hier and args.workload != "c4"
-        if single:  # one kernel per tick: HIP events around the timed region itself
-            avg_s = stream_ms / args.steps / 1e3
-        leases_k, res_k = units.get(name, (N, R))
-        alg = algorithmic_bytes(leases_k, res_k)
-        achieved = alg / avg_s / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-        if os.path.exists(pmc_path):
-            try:
-                traffic = json.load(open(pmc_path)).get(name, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2),
-                    "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
-                    "timed_region_stream_us_per_step": round(stream_ms * 1e3 / args.steps, 2),
-                    "duration_source": ("HIP event pair around the timed region on the kernel's stream (one kernel "
-                                        "per tick)" if single else "HIP events around every launch, profiled region")}
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_extra and args.workload == "c3":
+        # the 10M-lease C1 tick (BASELINE configs[1]) beside the north-star line
+        eng.close()
+        snap1 = make_workload("c1", 0)
+        e1 = Engine(dev_index)
+        e1.load(snap1)
+        st1 = lambda: e1.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
+        r1 = timed_steps(torch, e1, st1, args.steps, args.warmup, sync_ranks)
+        n1 = len(snap1["wants"])
+        extra["c1"] = {"workload": WORKLOADS["c1"], "value": n1 * args.steps / r1["elapsed"], "unit": "leases/s",
+                       "ms_per_step": r1["elapsed"] / args.steps * 1e3,
+                       "roofline": roofline_of("c1", snap1, r1, args.steps, True)}
+        e1.close()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -385,7 +489,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "warmup_steps_run": warm_run,
+            "warmup_steps_run": run["warm_run"],
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
@@ -393,15 +497,18 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded numpy generators of SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.workload] + (
-                           "; hierarchical: every GPU is an intermediate server of the same resources, RCCL "
-                           "all-gather of per-resource totals + root apportionment each step" if args.hier else ""),
+                           "; hierarchical: every GPU is an intermediate server of the same resources, all-gather "
+                           "of per-resource totals + root apportionment every step" if hier else ""),
                        "resources_per_gpu": R, "leases_per_gpu": N,
                        "parallelism": (f"intermediate-server hierarchy x{world} (all-gather 16 B x R per GPU)"
-                                       if args.hier else f"resource-sharded x{world} (no data-path collective)"),
+                                       if hier else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
+            "dist": dist_info,
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
-            "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in ktimes.items()},
+            "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
+                        for k, v in run["ktimes"].items()},
             "roofline": roofline,
+            "extra": extra or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

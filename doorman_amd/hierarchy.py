@@ -96,6 +96,10 @@ class HierarchicalTick:
         _lib.check(L.dm_hier_root_tick(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns),
                                        self.leaf._ctx, self.g), self.root._ctx, L)
 
+    def check(self):
+        """Raise if the root rejected a server's request (placeholder until the status word lands)."""
+        return None
+
     def tick(self, now_ns: int, asynchronous: bool = False):
         self.exchange(now_ns)
         self.leaf.apportion(now_ns, writeback=True, asynchronous=asynchronous)

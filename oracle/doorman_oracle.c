@@ -386,6 +386,20 @@ int64_t or_apportion_literal_rows(const or_snapshot* sn, int64_t r, int64_t row_
   return n;
 }
 
+/* or_apportion_literal_rows over a list of resources on `threads` OpenMP threads
+ * (rows [lo, lo + row_cap) of each): the reference's per-request Decide timed at
+ * the host's width (bench.py cpu_baseline). */
+int64_t or_apportion_literal_sample(const or_snapshot* sn, const int64_t* res, int64_t nres, int64_t row_cap,
+                                    int64_t now_ns, double* gets, int threads) {
+  int64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1) reduction(+ : total)
+  for (int64_t k = 0; k < nres; ++k) {
+    const int64_t r = res[k], lo = sn->seg_off[r];
+    total += or_apportion_literal_rows(sn, r, lo, lo + row_cap, now_ns, gets);
+  }
+  return total;
+}
+
 /* Closed form with every sum taken in row order, which makes
  * it bit-identical to or_apportion_literal. */
 typedef struct {

@@ -142,6 +142,10 @@ int or_apportion_closed_mt(const or_snapshot* snap, int64_t now_ns, or_outputs* 
  * (bounded CPU-baseline samples); returns number of rows evaluated */
 int64_t or_apportion_literal_rows(const or_snapshot* snap, int64_t resource, int64_t row_lo, int64_t row_hi,
                                   int64_t now_ns, double* gets);
+/* the same over nres resources (rows [lo, lo + row_cap) of each) on `threads`
+ * OpenMP threads; returns the number of rows evaluated */
+int64_t or_apportion_literal_sample(const or_snapshot* snap, const int64_t* resources, int64_t nres, int64_t row_cap,
+                                    int64_t now_ns, double* gets, int threads);
 
 #ifdef __cplusplus
 }

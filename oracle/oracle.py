@@ -132,6 +132,8 @@ def lib():
         L.or_apportion_closed_mt.argtypes = [ctypes.POINTER(_Snapshot), i64, ctypes.POINTER(_Outputs), i32]
         L.or_apportion_literal_rows.restype = i64
         L.or_apportion_literal_rows.argtypes = [ctypes.POINTER(_Snapshot), i64, i64, i64, i64, vp]
+        L.or_apportion_literal_sample.restype = i64
+        L.or_apportion_literal_sample.argtypes = [ctypes.POINTER(_Snapshot), vp, i64, i64, i64, vp, i32]
         _lib = L
     return _lib
 
@@ -305,3 +307,14 @@ def apportion_literal_rows(snap: dict, resource: int, row_lo: int, row_hi: int, 
     keep = []
     s = _mk_snapshot(snap, keep)
     return lib().or_apportion_literal_rows(ctypes.byref(s), resource, row_lo, row_hi, now_ns, gets.ctypes.data)
+
+
+def apportion_literal_sample(snap: dict, resources, row_cap: int, now_ns: int, gets: np.ndarray,
+                             threads: int = 1) -> int:
+    """Literal per-request Decide for the first row_cap rows of each listed resource on
+    `threads` OpenMP threads (bench.py cpu_baseline)."""
+    keep = []
+    s = _mk_snapshot(snap, keep)
+    res = np.ascontiguousarray(resources, dtype=np.int64)
+    return lib().or_apportion_literal_sample(ctypes.byref(s), res.ctypes.data, len(res), int(row_cap), now_ns,
+                                             gets.ctypes.data, int(threads))
