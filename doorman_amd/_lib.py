@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "libdoorman_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "doorman_hip.h")
 
 DM_OK, DM_E_INVAL, DM_E_HIP, DM_E_STATE, DM_E_KIND, DM_E_RANGE, DM_E_ARGUMENT = 0, -1, -2, -3, -4, -5, -6
+DM_HIER_INVALID, DM_HIER_COUNT_RANGE = 1, 2
 DM_WRITEBACK, DM_AGG_RECOMPUTE, DM_ASYNC, DM_WB_INPLACE, DM_WB_ALTERNATE, DM_DEFER_JOIN = 1, 2, 4, 8, 16, 32
 
 
@@ -101,8 +102,8 @@ _SIGS = {
     "dm_aggregate_bands": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "dm_publish_totals": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
-    "dm_hier_load_root": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
-    "dm_hier_take_grants": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "dm_read_config": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 7),
+    "dm_hier_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),

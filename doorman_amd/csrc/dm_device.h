@@ -109,7 +109,7 @@ struct ResCfg {
   int64_t learning_end_ns;  // learningModeEndTime
   int64_t parent_expiry_ns; // Resource.expiryTime (INT64_MAX = nil)
   int32_t kind;             // pb.Algorithm.Kind
-  int32_t pad;
+  int32_t refresh_s;        // Algorithm.refresh_interval (seconds; < 2^31, checked at load)
 };
 
 // The store's running sums (store.go:105-111) and the tick's SetSafeCapacity value.
@@ -140,9 +140,13 @@ struct DevParams {
   int32_t pad;
 };
 
-// dm_hier_root_tick: the fused root-store tick of the hierarchy (k_small_t<true>)
+// dm_hier_root_tick: one exchange round of the hierarchy's root (k_hier_tick)
+constexpr int kHierMaxServers = 64;     // one lane per server row, whole resources per wave
+constexpr uint32_t kHierInvalid = 1u;    // a band with num_clients < 1: InvalidArgument (server.go:863-866)
+constexpr uint32_t kHierCountRange = 2u; // Count >= 2^31: beyond the root's 32-bit subclients column
 struct HierArgs {
   const double2* gathered;  // [G][R] {SumWants, Count as bits} (k_publish records)
+  const uint32_t* status;   // [G] k_hier_validate flags; a flagged server requests nothing
   ResCfg* leaf_cfg;         // this server's leaf template
   int64_t R;
   int G;

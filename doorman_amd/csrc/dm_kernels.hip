@@ -573,14 +573,7 @@ __global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __rest
 __device__ __forceinline__ int shfl_i(int v, int lane) { return __shfl(v, lane, 64); }
 __device__ __forceinline__ double shfl_d(double v, int lane) { return shfl_any(v, lane); }
 
-// HIER: the root store of the intermediate-server hierarchy (R resources x G server
-// rows, row = r*G + g), fused with what dm_hier_load_root and dm_hier_take_grants do
-// around it: every row's request comes from the gathered totals (k_hier_root's rule)
-// and is stored, and this server's grants go straight into the leaf's config
-// (k_hier_grants' rule).  One launch instead of three per hierarchy exchange.
-template <bool HIER>
-__global__ __launch_bounds__(256) void k_small_t(DevParams p, const Pack* __restrict__ packs, int npacks,
-                                                 HierArgs ha) {
+__global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restrict__ packs, int npacks) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wv >= npacks) return;
   const int lane = threadIdx.x & 63;
@@ -595,34 +588,10 @@ __global__ __launch_bounds__(256) void k_small_t(DevParams p, const Pack* __rest
   int64_t e = 0;
   if (nrows > 0) {
     const int64_t row = row0 + (valid ? lane : nrows - 1);
-    if constexpr (HIER) {
-      const int64_t r = row / ha.G;
-      const int g = (int)(row - r * ha.G);
-      const double2 v = ha.gathered[(int64_t)g * ha.R + r];
-      const long long count = __double_as_longlong(v.y);
-      const int64_t e_old = p.expiry[row];
-      h = p.has[row];
-      if (v.x > 0.0 && count >= 1) {  // a request (server.go:241, :863-866)
-        w = v.x;
-        s = (int)(count < INT32_MAX ? count : INT32_MAX);
-        if (e_old == kReleased) h = 0.0;  // a new lease has nothing yet
-        e = p.now;                        // refreshing now: live for this tick's Clean
-      } else {
-        w = 0.0;
-        h = 0.0;
-        s = 0;
-        e = kReleased;
-      }
-      if (valid) {  // the root store keeps the requests (dm_hier_load_root)
-        p.out_wants[row] = w;
-        p.out_sub[row] = s;
-      }
-    } else {
-      w = p.wants[row];
-      h = p.has[row];
-      s = p.sub[row];
-      e = p.expiry[row];
-    }
+    w = p.wants[row];
+    h = p.has[row];
+    s = p.sub[row];
+    e = p.expiry[row];
   }
   // resource of this row: last k < nseg with rel[k] <= lane (offsets relative to row0)
   const int offk = lane <= nseg ? (int)pkr.rel[lane] : INT32_MAX;
@@ -739,15 +708,6 @@ __global__ __launch_bounds__(256) void k_small_t(DevParams p, const Pack* __rest
       }
     }
     if (need2) g = fs_stage2(w, h, s, C, sh, eq, x, wi, T, c);
-  }
-  if constexpr (HIER) {  // this server's grant -> the leaf's template (server.go:284-296)
-    if (valid && lv && (int)((row0 + lane) % ha.G) == ha.server) {
-      const int64_t r = (row0 + lane) / ha.G;
-      const int64_t ex = rs.exp_out;
-      const int64_t sec = ex >= 0 ? ex / kNs : -((-ex + kNs - 1) / kNs);  // time.Unix(sec, 0)
-      ha.leaf_cfg[r].capacity = g;
-      ha.leaf_cfg[r].parent_expiry_ns = sec * kNs;
-    }
   }
   if (valid) {
     if (lv) {
@@ -1643,46 +1603,242 @@ __global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __
   dst[r] = v;
 }
 
-// Intermediate-server hierarchy (server.go:227-323 -> :822-901).  The root store
-// holds R resources x G server rows (resource r owns rows [r*G, r*G+G)); gathered
-// is the all-gather of every server's k_publish records, [G][R] x 16 B.  A server
-// requests a resource only when its SumWants > 0 (server.go:241) and its band
-// must have num_clients >= 1 (server.go:863-866); other rows are released.
-__global__ void k_hier_root(int64_t R, int G, const double2* __restrict__ gathered, double* r_wants, double* r_has,
-                            int32_t* r_sub, int64_t* r_exp, int64_t now) {
+// Intermediate-server hierarchy (server.go:227-323 on each intermediate ->
+// :822-901 on the root).  The root store holds R resources x G server rows
+// (resource r owns rows [r*G, r*G+G), server g = client g); `gathered` is the
+// all-gather of every server's k_publish records, [G][R] x 16 B.
+//
+// k_hier_validate: a server's GetServerCapacity carries one band per resource
+// whose SumWants > 0 (server.go:241-253); a band with num_clients < 1 makes the
+// root reject the whole RPC with InvalidArgument (server.go:863-866), so that
+// server requests nothing this round and keeps its configuration
+// (performRequests returns before LoadConfig, server.go:268-272).  A Count that
+// does not fit the root's 32-bit subclients column is rejected the same way
+// (kHierCountRange) instead of being clamped.
+__global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ gathered, uint32_t* status) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R * G) return;
-  const int64_t r = i / G;
-  const int g = (int)(i - r * G);
-  const double2 v = gathered[(int64_t)g * R + r];
-  const double sum_wants = v.x;
+  const double2 v = gathered[i];
+  if (!(v.x > 0.0)) return;  // not requested (server.go:241)
   const long long count = __double_as_longlong(v.y);
-  if (sum_wants > 0.0 && count >= 1) {
-    r_wants[i] = sum_wants;  // GetServerCapacity: wantsTotal, subclientsTotal (:850-879)
-    r_sub[i] = (int32_t)(count < INT32_MAX ? count : INT32_MAX);  // rows hold subclients < 2^31
-    if (r_exp[i] == kReleased) r_has[i] = 0.0;  // a new lease has nothing yet
-    r_exp[i] = now;  // refreshing now: live for this tick's Clean
-  } else {
-    r_wants[i] = 0.0;
-    r_has[i] = 0.0;
-    r_sub[i] = 0;
-    r_exp[i] = kReleased;
-  }
+  uint32_t f = 0;
+  if (count < 1) f |= kHierInvalid;
+  if (count > 2147483647LL) f |= kHierCountRange;
+  if (f) atomicOr(&status[i / R], f);
 }
 
-// server.go:284-296: the intermediate's template for resource r takes the root's
-// grant as capacity and its expiry (Unix seconds) as the parent-lease expiry.
-// Resources the server did not request keep their previous template.
-__global__ void k_hier_grants(int64_t R, int G, int g, const double* __restrict__ gets,
-                              const int64_t* __restrict__ expiry, ResCfg* leaf_cfg) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const int64_t i = r * G + g;
-  const int64_t e = expiry[i];
-  if (e == kReleased) return;
-  leaf_cfg[r].capacity = gets[i];
-  const int64_t sec = e >= 0 ? e / kNs : -((-e + kNs - 1) / kNs);  // time.Unix(sec, 0)
-  leaf_cfg[r].parent_expiry_ns = sec * kNs;
+// One exchange round of the root, decided literally: every requesting server's
+// request {has 0 (the intermediate never fills Has, server.go:244,873), wants
+// SumWants_g, subclients Count_g} is decided by Resource.Decide against the root
+// store as it was before the round (resource.go:100-113: Clean, then Learn or
+// the algorithm, algorithm.go:95-302 with the request's own values), then all of
+// the round's leases are assigned (store.go:153-167).  Servers that do not
+// request keep their root lease until Clean expires it.  The running sums follow
+// the reference's own update sequence -- Clean's releases in row order, then one
+// Assign per request in server order -- so they equal a sequential replay of the
+// round bit for bit.
+//
+// G <= 64 servers: a wave holds 64/G whole resources, one lane per server row;
+// every lane loops over its resource's rows by shuffles (O(G) per request).
+// The lane of `ha.server` then loads that server's template for each resource
+// exactly as performRequests + LoadConfig do (server.go:279-313,
+// resource.go:117-125): a requested resource takes the root's grant as capacity,
+// its expiry (Unix seconds) as the parent expiry, and the root's algorithm
+// (kind, lease length, refresh) and configured safe capacity (0 when unset,
+// server.go:894); a resource it did not request drops to the "*" default
+// template (server.go:53-63: capacity 0, safe 0, FAIR_SHARE, lease 20 s, refresh
+// 1 s, no parent expiry).  learningModeEndTime is kept (set once, resource.go:163).
+__global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
+  const int G = ha.G;
+  const int per = 64 / G;  // resources per wave
+  const int lane = threadIdx.x & 63;
+  const int rl = lane / G, g = lane - rl * G;
+  const int64_t r = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * per + rl;
+  if (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * per >= ha.R) return;  // whole waves only
+  const bool valid = rl < per && r < ha.R;
+  const int64_t rr = valid ? r : 0;
+  const int64_t row = rr * G + (valid ? g : 0);
+  double w = 0.0, h = 0.0, rw = 0.0;
+  int s = 0, rs = 0;
+  int64_t e = kReleased;
+  bool req = false;
+  if (valid) {
+    w = p.wants[row];
+    h = p.has[row];
+    s = p.sub[row];
+    e = p.expiry[row];
+    const double2 v = ha.gathered[(int64_t)g * ha.R + rr];
+    req = ha.status[g] == 0u && v.x > 0.0;  // count in [1, 2^31) when status is clear
+    rw = v.x;
+    rs = req ? (int)__double_as_longlong(v.y) : 0;
+  }
+  const Res rs_cfg = load_res(p, (int)rr);
+  const bool released = e == kReleased;
+  const bool live = valid && !released && !(p.now > e);     // present after Clean (store.go:174)
+  const bool expired = valid && !released && (p.now > e);   // released by this round's Clean
+  const int base = rl * G;                                  // first lane of this resource
+  const int sl = live ? s : ~s;                             // subclients + live bit (s >= 0)
+  auto src = [&](int q) { const int j = base + q; return j < 64 ? j : 63; };
+
+  // Clean on the running sums, in row order (store.go:169-181 -> :142-151)
+  long long count = rs_cfg.agg_count;
+  double sh = rs_cfg.agg_has, sw = rs_cfg.agg_wants;
+  const int xp = expired ? 1 : 0;
+  if (__any(xp)) {
+    for (int q = 0; q < G; ++q) {
+      const double hj = shfl_d(h, src(q)), wj = shfl_d(w, src(q));
+      const int sj = shfl_i(s, src(q)), xj = shfl_i(xp, src(q));
+      if (xj) {
+        sw -= wj;
+        sh -= hj;
+        count -= sj;
+      }
+    }
+  }
+
+  // Decide (algorithm.go) for this lane's request against the cleaned store
+  const double C = rs_cfg.C;
+  const double old_h = live ? h : 0.0;  // store.Get: the zero Lease when absent
+  const int old_s = live ? s : 0;
+  const bool ps = !rs_cfg.learning && rs_cfg.kind == 2;
+  double gets = 0.0;
+  double eq = 0.0, ds = 0.0, avail = 0.0;
+  bool loop1 = false;
+  if (req) {
+    if (rs_cfg.learning) {
+      gets = 0.0;  // Learn: the request's Has (never filled by an intermediate)
+    } else if (rs_cfg.kind == 0) {
+      gets = rw;
+    } else if (rs_cfg.kind == 1) {
+      gets = minF(C, rw);
+    } else if (ps) {
+      const long long cnt = count + (live ? 0 : rs);  // :217-225
+      eq = C / (double)cnt;                            // :229
+      ds = eq * (double)rs;                            // :233 equalSharePerClient
+      avail = C - sh + old_h;                          // :239 unusedCapacity
+      if (sw <= C || rw <= ds) gets = minF(rw, avail);  // :245
+      else loop1 = true;
+    } else {
+      const long long cnt = count - old_s + rs;  // :115
+      avail = C - sh + old_h;                    // :120
+      eq = C / (double)cnt;                      // :123
+      ds = eq * (double)rs;                      // :126
+      if (rw <= ds) gets = minF(rw, avail);      // :131
+      else loop1 = true;
+    }
+  }
+  double x = 0.0, y = 0.0;
+  long long wx = rs;  // FairShare wantExtra starts at the request's subclients (:148)
+  if (__any(loop1)) {
+    for (int q = 0; q < G; ++q) {
+      const double wj = shfl_d(w, src(q));
+      const int sj = shfl_i(sl, src(q));
+      if (!loop1 || sj < 0) continue;  // absent rows are not in the store's Map
+      if (ps) {  // store.Map with this client's own request values (:259-279)
+        const double wv = (q == g) ? rw : wj;
+        const int sv = (q == g) ? rs : sj;
+        const double esp = eq * (double)sv;  // :273
+        if (wv < esp)
+          x += esp - wv;  // :275
+        else
+          y += wv - esp;  // :277
+      } else if (q != g) {  // FairShare round 1, this client skipped (:156-171)
+        const double d = (double)sj * eq;  // :160
+        if (wj < d)
+          x += d - wj;  // :164
+        else if (wj > d)
+          wx += sj;  // :168
+      }
+    }
+  }
+  bool loop2 = false;
+  double dE = 0.0, T = 0.0;
+  if (loop1) {
+    if (ps) {
+      gets = minF(ds + (rw - ds) * (x / y), avail);  // :283,290
+    } else {
+      dE = (x / (double)wx) * (double)rs;  // :175
+      if (rw < ds + dE) gets = minF(rw, avail);  // :179
+      else {
+        T = dE + ds;  // :197 deservedExtra + deservedShare
+        loop2 = true;
+      }
+    }
+  }
+  if (__any(loop2)) {
+    double ee = 0.0;
+    long long wee = rs;  // :189
+    for (int q = 0; q < G; ++q) {
+      const double wj = shfl_d(w, src(q));
+      const int sj = shfl_i(sl, src(q));
+      if (!loop2 || sj < 0 || q == g) continue;
+      if (!(wj > (double)sj * eq)) continue;  // wantExtraClients (:165-169)
+      if (wj < T)
+        ee += T - wj;  // :197-198
+      else if (wj > T)
+        wee += sj;  // :199-200
+    }
+    if (loop2) gets = minF(ds + dE + (ee / (double)wee) * (double)rs, avail);  // :203-204
+  }
+
+  // Assign the round's leases (store.go:153-167) and the running sums, in server order
+  const int64_t exp_new = rs_cfg.exp_out;
+  if (valid) {
+    if (req) {  // the root store is written in place (out_* alias its columns)
+      p.out_gets[row] = gets;
+      p.out_wants[row] = rw;
+      p.out_sub[row] = rs;
+      p.out_expiry[row] = exp_new;
+    } else if (expired) {
+      p.out_gets[row] = 0.0;
+      p.out_wants[row] = 0.0;
+      p.out_sub[row] = 0;
+      p.out_expiry[row] = kReleased;
+    }
+  }
+  const int rq = req ? 1 : 0;
+  for (int q = 0; q < G; ++q) {
+    const int rj = shfl_i(rq, src(q));
+    const double gj = shfl_d(gets, src(q)), rwj = shfl_d(rw, src(q));
+    const int rsj = shfl_i(rs, src(q));
+    const double ohj = shfl_d(old_h, src(q)), owj = shfl_d(live ? w : 0.0, src(q));
+    const int osj = shfl_i(old_s, src(q));
+    if (rj) {
+      sh += gj - ohj;
+      sw += rwj - owj;
+      count += rsj - osj;
+    }
+  }
+  if (valid && g == 0) {
+    ResAgg a;
+    a.count = count;
+    a.sum_has = sh;
+    a.sum_wants = sw;
+    a.safe = __builtin_isnan(rs_cfg.safe) ? rs_cfg.cap_cfg / (double)count : rs_cfg.safe;  // resource.go:91-95
+    p.res[rr] = a;
+  }
+
+  // this server's new template for the resource (server.go:279-313)
+  if (valid && g == ha.server && ha.status[g] == 0u) {
+    ResCfg* c = ha.leaf_cfg + rr;
+    if (req) {
+      const ResCfg rc = p.cfg[rr];
+      const int64_t sec = exp_new >= 0 ? exp_new / kNs : -((-exp_new + kNs - 1) / kNs);  // time.Unix(sec, 0)
+      c->capacity = gets;                                                  // :293
+      c->safe_capacity = __builtin_isnan(rc.safe_capacity) ? 0.0 : rc.safe_capacity;  // :294, :894
+      c->lease_len_ns = rc.lease_len_ns;                                   // :295 Algorithm
+      c->refresh_s = rc.refresh_s;
+      c->kind = rc.kind;
+      c->parent_expiry_ns = sec * kNs;                                     // :287-288
+    } else {  // the "*" default template (server.go:53-63, :305)
+      c->capacity = 0.0;
+      c->safe_capacity = 0.0;
+      c->lease_len_ns = 20 * kNs;
+      c->refresh_s = 1;
+      c->kind = 3;
+      c->parent_expiry_ns = INT64_MAX;  // expiryTimes has no entry: nil
+    }
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -1690,7 +1846,7 @@ __global__ void k_hier_grants(int64_t R, int G, int g, const double* __restrict_
 // --------------------------------------------------------------------------
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_small_t<false><<<(n + 3) / 4, 256, 0, st>>>(p, packs, n, HierArgs{});
+  k_small<<<(n + 3) / 4, 256, 0, st>>>(p, packs, n);
   return hipGetLastError();
 }
 
@@ -1814,24 +1970,17 @@ hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t launch_small_hier(const DevParams& p, const Pack* packs, int n, const HierArgs& ha, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  k_small_t<true><<<(n + 3) / 4, 256, 0, st>>>(p, packs, n, ha);
-  return hipGetLastError();
-}
-
-hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
-                            int64_t* r_exp, int64_t now, hipStream_t st) {
+hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, hipStream_t st) {
   if (R * G <= 0) return hipSuccess;
-  k_hier_root<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, r_wants, r_has, r_sub,
-                                                               r_exp, now);
+  k_hier_validate<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, status);
   return hipGetLastError();
 }
 
-hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
-                              hipStream_t st) {
-  if (R <= 0) return hipSuccess;
-  k_hier_grants<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, G, g, gets, expiry, leaf_cfg);
+hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st) {
+  if (ha.R <= 0) return hipSuccess;
+  const int64_t per = 64 / ha.G;
+  const int64_t waves = (ha.R + per - 1) / per;
+  k_hier_tick<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(p, ha);
   return hipGetLastError();
 }
 

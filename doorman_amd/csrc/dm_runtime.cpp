@@ -41,11 +41,8 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
-hipError_t launch_small_hier(const DevParams& p, const Pack* packs, int n, const HierArgs& ha, hipStream_t st);
-hipError_t launch_hier_root(int64_t R, int G, const void* gathered, double* r_wants, double* r_has, int32_t* r_sub,
-                            int64_t* r_exp, int64_t now, hipStream_t st);
-hipError_t launch_hier_grants(int64_t R, int G, int g, const double* gets, const int64_t* expiry, ResCfg* leaf_cfg,
-                              hipStream_t st);
+hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, hipStream_t st);
+hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st);
 }  // namespace dm
 
 using namespace dm;
@@ -185,6 +182,8 @@ struct dm_ctx {
   hipEvent_t ev_bat[3] = {};
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
+  DBuf<uint32_t> hier_status;  // dm_hier_root_tick: per-server rejection flags of the last round
+  int hier_servers = 0;
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
   bool profiling = false;
@@ -237,7 +236,7 @@ struct dm_ctx {
     bat_flags.release();
     if (h_bat_flags) (void)hipHostFree(h_bat_flags);
     h_bat_flags = nullptr;
-    row_bits.release(); upd_flags.release();
+    row_bits.release(); upd_flags.release(); hier_status.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
   }
@@ -397,7 +396,7 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
 // ---------------------------------------------------------------------------
 extern "C" {
 
-const char* dm_version(void) { return "doorman-hip 0.1 (gfx950, abi 1)"; }
+const char* dm_version(void) { return "doorman-hip 0.2 (gfx950, abi 2)"; }
 
 int dm_device_count(int* out) {
   if (!out) return DM_E_INVAL;
@@ -600,6 +599,8 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   for (int64_t r = 0; r < R; ++r) {
     if (cfg->lease_length_s[r] < 0 || cfg->refresh_interval_s[r] < 0)
       return c->fail(DM_E_INVAL, "lease_length and refresh_interval must be >= 0 (server.go:384-434)");
+    if (cfg->refresh_interval_s[r] > INT32_MAX || cfg->lease_length_s[r] > INT64_MAX / kNs)
+      return c->fail(DM_E_INVAL, "refresh_interval must be < 2^31 s and lease_length < 2^63 ns");
   }
   for (int64_t r = 0; r < R; ++r)
     if (cfg->kind[r] < DM_NO_ALGORITHM || cfg->kind[r] > DM_FAIR_SHARE) {
@@ -612,7 +613,7 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   std::vector<ResCfg> rc(R);
   for (int64_t r = 0; r < R; ++r)
     rc[r] = ResCfg{cfg->capacity[r], cfg->safe_capacity[r], cfg->lease_length_s[r] * kNs, cfg->learning_end_ns[r],
-                   cfg->parent_expiry_ns[r], cfg->kind[r], 0};
+                   cfg->parent_expiry_ns[r], cfg->kind[r], (int32_t)cfg->refresh_interval_s[r]};
   DM_HIP(c, upload(c->cfg, rc.data(), (size_t)R, st), "upload config");
   c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
   DM_HIP(c, hipStreamSynchronize(st), "config load");
@@ -809,13 +810,19 @@ int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, in
       if (v % kNs != 0 && v < 0) --q;
       expiry_time_s[i] = q;
     }
-  if (refresh_interval_s) {
+  if (refresh_interval_s && n > 0) {
+    // the device config: a hierarchy exchange rewrites a leaf's algorithm (dm_hier_root_tick)
     const auto& so = c->h_seg_off;
-    int64_t r = std::upper_bound(so.begin(), so.end(), off) - so.begin() - 1;
+    const int64_t r0 = std::upper_bound(so.begin(), so.end(), off) - so.begin() - 1;
+    const int64_t r1 = std::upper_bound(so.begin(), so.end(), off + n - 1) - so.begin() - 1;
+    std::vector<ResCfg> cf((size_t)(r1 - r0 + 1));
+    DM_HIP(c, download(cf.data(), (const ResCfg*)c->cfg.p, r0, r1 - r0 + 1, c->stream), "read config");
+    DM_HIP(c, hipStreamSynchronize(c->stream), "read config");
+    int64_t r = r0;
     for (int64_t i = 0; i < n; ++i) {
       const int64_t row = off + i;
       while (r + 1 < (int64_t)so.size() && so[r + 1] <= row) ++r;
-      refresh_interval_s[i] = e[i] == DM_RELEASED ? 0 : c->h_refresh_s[r];
+      refresh_interval_s[i] = e[i] == DM_RELEASED ? 0 : cf[(size_t)(r - r0)].refresh_s;
     }
   }
   return DM_OK;
@@ -836,6 +843,28 @@ int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* 
     if (sum_has) sum_has[i] = v[i].sum_has;
     if (sum_wants) sum_wants[i] = v[i].sum_wants;
     if (safe) safe[i] = v[i].safe;
+  }
+  return DM_OK;
+}
+
+int dm_read_config(dm_ctx* c, int64_t r0, int64_t n, int32_t* kind, double* capacity, int64_t* lease_length_s,
+                   int64_t* refresh_interval_s, int64_t* learning_end_ns, int64_t* parent_expiry_ns,
+                   double* safe_capacity) {
+  DM_ENTER(c);
+  if (!c->cfg_loaded) return c->fail(DM_E_STATE, "no configuration loaded");
+  int rc = check_range(c, r0, n, c->R);
+  if (rc) return rc;
+  std::vector<ResCfg> v(n > 0 ? (size_t)n : 0);
+  DM_HIP(c, download(v.data(), (const ResCfg*)c->cfg.p, r0, n, c->stream), "read config");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "read config");
+  for (int64_t i = 0; i < n; ++i) {
+    if (kind) kind[i] = v[i].kind;
+    if (capacity) capacity[i] = v[i].capacity;
+    if (lease_length_s) lease_length_s[i] = v[i].lease_len_ns / kNs;
+    if (refresh_interval_s) refresh_interval_s[i] = v[i].refresh_s;
+    if (learning_end_ns) learning_end_ns[i] = v[i].learning_end_ns;
+    if (parent_expiry_ns) parent_expiry_ns[i] = v[i].parent_expiry_ns;
+    if (safe_capacity) safe_capacity[i] = v[i].safe_capacity;
   }
   return DM_OK;
 }
@@ -1182,84 +1211,40 @@ int dm_publish_totals(dm_ctx* c, void* dst) {
 }
 
 static bool root_layout_ok(dm_ctx* c, int G) {
-  if (G <= 0 || c->R <= 0 || c->N != c->R * (int64_t)G) return false;
+  if (G <= 0 || G > kHierMaxServers || c->R <= 0 || c->N != c->R * (int64_t)G) return false;
   for (int64_t r = 0; r <= c->R; ++r)
     if (c->h_seg_off[r] != r * (int64_t)G) return false;
   return true;
 }
 
-int dm_hier_load_root(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns) {
-  DM_ENTER(root);
-  if (!root->store_loaded) return root->fail(DM_E_STATE, "root store not loaded");
-  if (!gathered) return root->fail(DM_E_INVAL, "null gathered buffer");
-  if (!root_layout_ok(root, n_servers))
-    return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows");
-  // stream-ordered (no host sync): the all-gather that produced `gathered` must be
-  // ordered before this call on the same stream (dm_set_stream)
-  DM_HIP(root, launch_hier_root(root->R, n_servers, gathered, root->wants.p, root->has.p, root->sub.p,
-                                root->expiry.p, now_ns, root->stream),
-         "hier root update");
-  root->maybe_general = true;  // rows now carry heterogeneous subclient counts
-  root->have_result = false;
-  return DM_OK;
-}
-
-int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server) {
-  DM_ENTER(root);
-  if (!leaf) return root->fail(DM_E_INVAL, "null leaf context");
-  DM_HIP(root, leaf->join_aux(), "join leaf streams");
-  leaf->main_dirty = true;
-  if (leaf->device != root->device) return root->fail(DM_E_INVAL, "root and leaf contexts must share a device");
-  if (!root->have_result) return root->fail(DM_E_STATE, "no root dm_apportion result");
-  const int G = (int)(root->R > 0 ? root->N / root->R : 0);
-  if (!root_layout_ok(root, G)) return root->fail(DM_E_STATE, "root store layout");
-  if (server < 0 || server >= G) return root->fail(DM_E_RANGE, "server index out of range");
-  if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
-  const double* gets = root->last_writeback ? root->has.p : root->out_gets.p;
-  const int64_t* exp = root->last_writeback ? root->expiry.p : root->out_expiry.p;
-  // stream-ordered hand-off: root stream after leaf's prior work, leaf after the update
-  const bool same = root->stream == leaf->stream;
-  if (!same) {
-    DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
-    DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
-  }
-  DM_HIP(root, launch_hier_grants(root->R, G, server, gets, exp, leaf->cfg.p, root->stream), "hier grants");
-  if (!same) {
-    DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
-    DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
-  }
-  return DM_OK;
-}
-
-// dm_hier_load_root + dm_apportion(WRITEBACK | AGG_RECOMPUTE) + dm_hier_take_grants in
-// one launch when every root resource is small (G <= kSmallMax servers: the
-// wave-packed path evaluates each server row literally): k_small_t<true> reads the
-// requests straight from the gathered records and writes this server's grants into
-// the leaf's config.  Otherwise the three calls run in turn.
+// One exchange round of the hierarchy (server.go:227-323 -> :822-901): validate
+// every server's request (k_hier_validate), decide the round on the root store
+// and load this server's template into the leaf (k_hier_tick).  Stream-ordered:
+// the all-gather that produced `gathered` must precede it on the root's stream.
 int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns, dm_ctx* leaf, int server) {
   DM_ENTER(root);
   if (!root->store_loaded || !root->cfg_loaded) return root->fail(DM_E_STATE, "root store / config not loaded");
   if (!gathered || !leaf) return root->fail(DM_E_INVAL, "null gathered buffer or leaf context");
+  if (n_servers <= 0 || n_servers > kHierMaxServers)
+    return root->fail(DM_E_INVAL, "1..64 intermediate servers per root store");
   if (!root_layout_ok(root, n_servers))
-    return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows");
+    return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows (resource r: rows r*G..r*G+G-1)");
   if (server < 0 || server >= n_servers) return root->fail(DM_E_RANGE, "server index out of range");
   if (leaf->device != root->device) return root->fail(DM_E_INVAL, "root and leaf contexts must share a device");
   if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
-  bool fused = n_servers <= kSmallMax && root->h_chunks.empty();
-  for (int b = 0; b < kNumBins; ++b) fused = fused && root->h_bins[b].empty();
-  if (!fused) {
-    int rc = dm_hier_load_root(root, gathered, n_servers, now_ns);
-    if (!rc) rc = dm_apportion(root, now_ns, DM_WRITEBACK | DM_AGG_RECOMPUTE | DM_ASYNC);
-    if (!rc) rc = dm_hier_take_grants(root, leaf, server);
-    return rc;
-  }
   DM_HIP(root, leaf->join_aux(), "join leaf streams");
   leaf->main_dirty = true;
+  DM_HIP(root, root->hier_status.ensure((size_t)n_servers), "hierarchy status");
+  root->hier_servers = n_servers;
   const bool same = root->stream == leaf->stream;
-  if (!same) {  // root after the leaf's prior work (its config is written)
+  if (!same) {  // root after the leaf's prior work (its config is rewritten)
     DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
     DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
   }
+  DM_HIP(root, hipMemsetAsync(root->hier_status.p, 0, (size_t)n_servers * sizeof(uint32_t), root->stream),
+         "hierarchy status");
+  DM_HIP(root, launch_hier_validate(root->R, n_servers, gathered, root->hier_status.p, root->stream),
+         "hierarchy validate");
   DevParams p{};
   p.seg_off = root->seg_off.p;
   p.wants = root->wants.p;
@@ -1268,23 +1253,36 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   p.expiry = root->expiry.p;
   p.cfg = root->cfg.p;
   p.agg = root->agg.p;
-  p.out_gets = root->has.p;  // writeback in place (a root store is small)
+  p.out_gets = root->has.p;
   p.out_expiry = root->expiry.p;
   p.out_wants = root->wants.p;
   p.out_sub = root->sub.p;
   p.res = root->agg.p;
   p.now = now_ns;
-  p.recompute = 1;
-  const HierArgs ha{(const double2*)gathered, leaf->cfg.p, root->R, n_servers, server};
-  DM_HIP(root, launch_small_hier(p, root->packs.p, (int)root->h_packs.size(), ha, root->stream), "hier root tick");
+  p.recompute = 0;  // the root's running sums, updated as the reference's Clean + Assigns
+  const HierArgs ha{(const double2*)gathered, root->hier_status.p, leaf->cfg.p, root->R, n_servers, server};
+  DM_HIP(root, launch_hier_tick(p, ha, root->stream), "hierarchy root tick");
   if (!same) {  // the leaf's next tick after its new template
     DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
     DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
   }
   root->maybe_general = true;  // rows carry heterogeneous subclient counts
+  root->all_sub_one = false;
   root->last_writeback = true;
   root->have_result = true;
   return DM_OK;
+}
+
+int dm_hier_status(dm_ctx* root, uint32_t* status, int n) {
+  DM_ENTER(root);
+  if (!status || n < 0) return root->fail(DM_E_INVAL, "bad status buffer");
+  if (root->hier_servers == 0) return root->fail(DM_E_STATE, "no dm_hier_root_tick yet");
+  if (n != root->hier_servers) return root->fail(DM_E_INVAL, "status buffer must hold one word per server");
+  DM_HIP(root, download(status, (const uint32_t*)root->hier_status.p, 0, n, root->stream), "hierarchy status");
+  DM_HIP(root, hipStreamSynchronize(root->stream), "hierarchy status");
+  int bad = 0;
+  for (int g = 0; g < n; ++g) bad += status[g] != 0;
+  return bad;
 }
 
 int dm_set_profiling(dm_ctx* c, int on) {

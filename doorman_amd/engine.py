@@ -37,6 +37,7 @@ class Engine:
         self.device = device
         self.n_resources = 0
         self.n_leases = 0
+        self.seg_off = np.zeros(1, np.int64)
         self._pinned = []
 
     # -- lifetime --
@@ -118,6 +119,7 @@ class Engine:
             s.agg_sum_wants = _ptr(keep["agg_sum_wants"])
         self._chk(self._L.dm_store_load(self._ctx, ctypes.byref(s)))
         self.n_resources, self.n_leases = s.n_resources, s.n_leases
+        self.seg_off = keep["seg_off"].copy()  # the table layout (host copy)
 
     def load_config(self, snap: dict):
         R = len(snap["kind"])
@@ -219,6 +221,15 @@ class Engine:
             out["safe_capacity"] = np.empty(n)
         self._chk(self._L.dm_read_resources(self._ctx, r0, n, _ptr(out["count"]), _ptr(out["sum_has"]),
                                           _ptr(out["sum_wants"]), _ptr(out.get("safe_capacity"))))
+        return out
+
+    def config(self, r0: int = 0, n: int | None = None) -> dict:
+        """dm_read_config: the per-resource configuration the device holds (CFG_FIELDS columns)."""
+        n = self.n_resources - r0 if n is None else n
+        out = {"kind": np.empty(n, np.int32), "capacity": np.empty(n), "lease_length_s": np.empty(n, np.int64),
+               "refresh_interval_s": np.empty(n, np.int64), "learning_end_ns": np.empty(n, np.int64),
+               "parent_expiry_ns": np.empty(n, np.int64), "safe_capacity": np.empty(n)}
+        self._chk(self._L.dm_read_config(self._ctx, r0, n, *[_ptr(out[k]) for k in CFG_FIELDS]))
         return out
 
     def publish_totals(self, dev_ptr: int):

@@ -9,9 +9,10 @@
   GPU is one intermediate server holding its own clients of the same R
   resources.  Per tick each server publishes {SumWants, Count} per resource
   (dm_publish_totals), one RCCL all-gather over xGMI shares them, every rank
-  evaluates the root's apportionment of the G server rows redundantly
-  (dm_hier_load_root + dm_apportion on a root store of R x G rows), takes its
-  own grant as leaf capacity (dm_hier_take_grants) and runs its leaf tick.
+  evaluates the root's round of the G server requests redundantly on its own
+  copy of the root store (R x G rows), loads its own new templates (grant,
+  root algorithm, or the "*" default) into its leaf (dm_hier_root_tick) and runs
+  its leaf tick.
 
 torch is plumbing here (device buffers and torch.distributed); import it before
 doorman_amd so the HIP library binds to torch's HIP runtime.
@@ -52,7 +53,7 @@ def shard(snap: dict, world: int, rank: int) -> dict:
 
 def root_snapshot(n_resources: int, n_servers: int, kind, capacity, lease_length_s=20, refresh_interval_s=5) -> dict:
     """The root server's store for the hierarchy: R resources x G server rows,
-    all released until the first dm_hier_load_root."""
+    all released until the first exchange (dm_hier_root_tick)."""
     G = n_servers
     N = n_resources * G
     return W.make_snapshot(np.full(n_resources, G), np.zeros(N), np.zeros(N), np.zeros(N, np.int64),
@@ -86,19 +87,32 @@ class HierarchicalTick:
         root.set_stream(self.stream.cuda_stream)
 
     def exchange(self, now_ns: int):
-        """publish -> all-gather -> root apportionment -> take this server's grants."""
+        """publish -> all-gather -> the root's round -> this server's new templates."""
         from . import _lib
         self.leaf.publish_totals(self.totals.data_ptr())
         with self.torch.cuda.stream(self.stream):  # the collective orders with our stream
             self.gather(self.totals, self.gathered)
         L = self.root._L
-        # load_root + root apportionment + take_grants (one launch for G <= 8)
         _lib.check(L.dm_hier_root_tick(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns),
                                        self.leaf._ctx, self.g), self.root._ctx, L)
 
+    def status(self) -> np.ndarray:
+        """dm_hier_status: per-server flags of the last exchange (0 = request accepted)."""
+        from . import _lib
+        st = np.zeros(self.G, np.uint32)
+        _lib.check(self.root._L.dm_hier_status(self.root._ctx, st.ctypes.data, self.G), self.root._ctx, self.root._L)
+        return st
+
     def check(self):
-        """Raise if the root rejected a server's request (placeholder until the status word lands)."""
-        return None
+        """Raise DmError(DM_E_ARGUMENT) if the root rejected some server's request in the
+        last exchange (a band with num_clients < 1, server.go:863-866, or a Count beyond
+        2^31): the reference fails that server's GetServerCapacity RPC."""
+        from . import _lib
+        st = self.status()
+        bad = np.flatnonzero(st)
+        if len(bad):
+            raise _lib.DmError(_lib.DM_E_ARGUMENT, f"root rejected the requests of servers {bad.tolist()} "
+                                                   f"(flags {st[bad].tolist()}: 1 = num_clients < 1, 2 = Count >= 2^31)")
 
     def tick(self, now_ns: int, asynchronous: bool = False):
         self.exchange(now_ns)

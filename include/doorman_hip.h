@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DM_ABI_VERSION 1
+#define DM_ABI_VERSION 2
 
 /* return codes */
 #define DM_OK 0
@@ -183,6 +183,13 @@ int dm_host_free(dm_ctx* ctx, void* ptr);
 int dm_read_store(dm_ctx* ctx, int64_t off, int64_t n, double* has, double* wants, int64_t* subclients,
                   int64_t* expiry_ns);
 
+/* the resolved configuration the device holds for resources [r0, r0+n) (the
+ * dm_resource_cfg columns; Resource.config / Status, resource.go:190-203) -- after a
+ * hierarchy exchange, the templates dm_hier_root_tick loaded; any pointer may be NULL */
+int dm_read_config(dm_ctx* ctx, int64_t r0, int64_t n, int32_t* kind, double* capacity, int64_t* lease_length_s,
+                   int64_t* refresh_interval_s, int64_t* learning_end_ns, int64_t* parent_expiry_ns,
+                   double* safe_capacity);
+
 /* ---- the batch algorithm: every client of every resource, one frozen snapshot ---- */
 int dm_apportion(dm_ctx* ctx, int64_t now_ns, uint32_t flags);
 
@@ -208,22 +215,47 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
  * device buffer (16 B x R, interleaved), ready for an RCCL all-gather */
 int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
 
-/* Root server of the hierarchy on one device: `root` holds R resources x n_servers rows
- * (resource r owns rows [r*n_servers, (r+1)*n_servers)); dev_gathered is the all-gather of
- * every intermediate server's dm_publish_totals ([n_servers][R] x 16 B).  Each row becomes that
- * server's GetServerCapacity request (server.go:850-879): wants = SumWants, subclients = Count;
- * a server whose SumWants <= 0 or Count < 1 does not request the resource (server.go:241,863)
- * and its row is released.  Then call dm_apportion on `root`. */
-int dm_hier_load_root(dm_ctx* root, const void* dev_gathered, int n_servers, int64_t now_ns);
-/* server.go:284-296: the leaf (intermediate) store of `server` takes the root's grant as its
- * capacity and the grant's expiry (Unix seconds) as parent expiry; resources it did not
- * request keep their template.  Both contexts must be on the same device. */
-int dm_hier_take_grants(dm_ctx* root, dm_ctx* leaf, int server);
-/* One hierarchy exchange's root work: dm_hier_load_root, dm_apportion(root, WRITEBACK |
-   AGG_RECOMPUTE | ASYNC) and dm_hier_take_grants(root, leaf, server) -- fused into one
-   kernel launch when n_servers <= 8, else those three calls in turn.  Stream-ordered. */
+/* One exchange round of the intermediate-server hierarchy, on the root store of this
+ * server's device (every server evaluates the root redundantly):
+ *
+ *   performRequests        go/server/doorman/server.go:227-323  -> the gathered dm_publish_totals records
+ *   GetServerCapacity      go/server/doorman/server.go:822-901  -> the root's round below
+ *   Server.LoadConfig      go/server/doorman/server.go:187-218  -> this server's new leaf templates
+ *   Resource.LoadConfig    go/server/doorman/resource.go:117-125
+ *
+ * `root` holds R resources x n_servers rows (resource r owns rows
+ * [r*n_servers, (r+1)*n_servers), row g = intermediate server g); dev_gathered is the
+ * all-gather of every server's dm_publish_totals ([n_servers][R] x 16 B).
+ *   - Server g requests resource r when its SumWants > 0 (server.go:241): has 0
+ *     (Has is never filled, :244/:873), wants = SumWants, subclients = Count.
+ *     A band with Count < 1 makes the root reject server g's whole request
+ *     (codes.InvalidArgument, :863-866); Count >= 2^31 (beyond the root's 32-bit
+ *     subclients column) is rejected the same way.  A rejected server requests
+ *     nothing this round and its leaf keeps its templates (:268-272); see
+ *     dm_hier_status.
+ *   - The round's requests are decided against the root store as it was before the
+ *     round (Clean, then Learn or the resource's algorithm with each request's own
+ *     values), then assigned; servers that do not request keep their root lease
+ *     until it expires.  The root's running sums follow Clean + one Assign per
+ *     request in server order.
+ *   - The leaf (`leaf`, this server's store, same device and resources) loads its
+ *     new templates: a requested resource takes the grant as capacity, the grant's
+ *     expiry in Unix seconds as parent expiry, and the root's algorithm (kind, lease
+ *     length, refresh interval) and configured safe capacity (0 when unset,
+ *     :293-296,:894); every other resource drops to the "*" default template
+ *     (capacity 0, safe capacity 0, FAIR_SHARE, lease 20 s, refresh 1 s, no parent
+ *     expiry; server.go:53-63,:305).  Learning-mode end times are kept (fixed when a
+ *     resource is created, resource.go:153-163).
+ * 1 <= n_servers <= 64.  Two stream-ordered launches; returns without waiting. */
 int dm_hier_root_tick(dm_ctx* root, const void* dev_gathered, int n_servers, int64_t now_ns, dm_ctx* leaf,
                       int server);
+/* Per-server outcome of the last dm_hier_root_tick (waits for it): status[g] = 0 when
+ * server g's request was accepted, else DM_HIER_INVALID (a band with num_clients < 1,
+ * server.go:863-866) and/or DM_HIER_COUNT_RANGE.  Returns the number of rejected
+ * servers (>= 0) or a DM_E_* code. */
+#define DM_HIER_INVALID 1u
+#define DM_HIER_COUNT_RANGE 2u
+int dm_hier_status(dm_ctx* root, uint32_t* status, int n_servers);
 
 /* ---- profiling ---- */
 int dm_set_profiling(dm_ctx* ctx, int on);

@@ -1,43 +1,128 @@
-"""Host-side reference model of one hierarchy exchange (test infrastructure):
-builds the root server's store exactly as GetServerCapacity would see the
-intermediate servers' requests (server.go:234-255 -> :850-879) and evaluates it
-with the oracle."""
+"""Reference model of the intermediate-server hierarchy (test infrastructure).
+
+Restated from the reference itself, not from the kernels:
+  * each intermediate's request    go/server/doorman/server.go:227-262 (performRequests):
+        one band per resource whose store SumWants > 0, num_clients = Count,
+        wants = SumWants, Has never filled (:244)
+  * the root's GetServerCapacity   server.go:822-901: bands summed (:850-879), a band
+        with num_clients < 1 fails the whole RPC with InvalidArgument (:863-866);
+        each request decided by Resource.Decide (resource.go:100-113) -- here the
+        oracle's literal restatement, one private store copy per request (the
+        round's snapshot semantics) -- and assigned (store.go:153-167)
+  * the intermediate's reload      server.go:279-313 + Server.LoadConfig (:187-218)
+        + Resource.LoadConfig (resource.go:117-125): capacity = the grant, expiry
+        time = time.Unix(gets.expiry_time, 0), the root's Algorithm and
+        SafeCapacity (config.GetSafeCapacity(): 0 when unset, :894); every other
+        resource falls back to the "*" default template (server.go:53-63, :305)
+        with no expiry time; learningModeEndTime is untouched (set once,
+        resource.go:153-163); a failed RPC loads nothing (:268-272).
+"""
 import numpy as np
 
 from doorman_amd import workloads as W
 from oracle import oracle as O
 
-
-def leaf_totals(snap, now):
-    """What each intermediate publishes per resource: store SumWants and Count after Clean."""
-    out = O.apportion(snap, now)
-    return out["res_sum_wants"], out["res_count"]
-
-
-def root_from_totals(totals, capacity, kind, lease_length_s, prev_has, now):
-    """totals: list over servers g of (sum_wants[R], count[R]).  Rows of servers that do
-    not request (SumWants <= 0 or Count < 1) are released."""
-    G = len(totals)
-    R = len(totals[0][0])
-    wants = np.zeros(R * G)
-    sub = np.zeros(R * G, np.int64)
-    exp = np.full(R * G, W.RELEASED, np.int64)
-    has = np.zeros(R * G)
-    for g, (sw, cnt) in enumerate(totals):
-        for r in range(R):
-            i = r * G + g
-            if sw[r] > 0 and cnt[r] >= 1:
-                wants[i], sub[i], exp[i], has[i] = sw[r], cnt[r], now, prev_has[i]
-    snap = W.make_snapshot(np.full(R, G), wants, has, sub, exp, kind, capacity, lease_length_s, 5)
-    return snap
+# server.go:53-63 defaultResourceTemplate ("*")
+DEFAULT_TEMPLATE = {"kind": W.FAIR_SHARE, "capacity": 0.0, "safe_capacity": 0.0, "lease_length_s": 20,
+                    "refresh_interval_s": 1, "parent_expiry_ns": W.INT64_MAX}
+CFG_FIELDS = W.CFG_FIELDS
 
 
-def grants(root_snap, root_out, G, g):
-    """server.go:284-296: capacity = gets, parent expiry = Unix seconds of the lease expiry."""
-    R = len(root_snap["seg_off"]) - 1
-    idx = np.arange(R) * G + g
-    e = root_out["expiry_ns"][idx]
-    live = e != W.RELEASED
-    cap = root_out["gets"][idx]
-    parent = np.where(live, (e // W.NS) * W.NS, W.INT64_MAX)
-    return cap, parent, live
+def cfg_table(cfg: dict) -> np.ndarray:
+    """dict of per-resource columns -> the oracle's or_resource_cfg rows."""
+    R = len(cfg["kind"])
+    t = np.zeros(R, dtype=O.CFG_DTYPE)
+    for f in O.CFG_DTYPE.names:
+        t[f] = cfg[f]
+    return t
+
+
+class Root:
+    """The root server's resources: one LeaseStore per resource whose clients are the
+    intermediate servers 0..G-1 (client id = server index)."""
+
+    def __init__(self, cfg: dict, n_servers: int):
+        self.cfg = {k: np.array(cfg[k]) for k in CFG_FIELDS}
+        self.tab = cfg_table(self.cfg)
+        self.R, self.G = len(self.tab), n_servers
+        self.stores = [O.Store(n_servers) for _ in range(self.R)]
+
+    def round(self, now: int, requests):
+        """requests[g]: None (server g sent nothing / its RPC failed) or {r: (wants, subclients)}.
+        Returns {(g, r): Lease} for every request, all decided against the stores as they
+        were before the round, then assigned."""
+        out = {}
+        for r in range(self.R):
+            st = self.stores[r]
+            st.clean(now)  # every private copy's Decide starts with the same Clean
+            reqs = [(g, *requests[g][r]) for g in range(self.G) if requests[g] is not None and r in requests[g]]
+            leases = [O.decide(st.clone(), self.tab[r], g, 0.0, w, s, now) for g, w, s in reqs]
+            lease_s, refresh_s = int(self.tab[r]["lease_length_s"]), int(self.tab[r]["refresh_interval_s"])
+            for (g, w, s), l in zip(reqs, leases):
+                st.assign(g, lease_s, refresh_s, l.has, w, s, now)
+                out[(g, r)] = l
+        return out
+
+    def rows(self) -> dict:
+        """The store in the device's root layout (row r*G + g; absent = released)."""
+        R, G = self.R, self.G
+        has, wants = np.zeros(R * G), np.zeros(R * G)
+        sub, exp = np.zeros(R * G, np.int64), np.full(R * G, W.RELEASED, np.int64)
+        for r, st in enumerate(self.stores):
+            for g in range(G):
+                if st.has_client(g):
+                    l = st.get(g)
+                    i = r * G + g
+                    has[i], wants[i], sub[i], exp[i] = l.has, l.wants, l.subclients, l.expiry_ns
+        return {"has": has, "wants": wants, "subclients": sub, "expiry_ns": exp}
+
+    def sums(self) -> dict:
+        return {"count": np.array([s.count() for s in self.stores], np.int64),
+                "sum_has": np.array([s.sum_has() for s in self.stores]),
+                "sum_wants": np.array([s.sum_wants() for s in self.stores])}
+
+
+def server_request(sum_wants, count):
+    """performRequests' request (server.go:234-255) as the root validates it
+    (:858-868): None when some band has num_clients < 1 (InvalidArgument), and --
+    this build's limit -- when a Count does not fit the root's 32-bit column."""
+    req = {r: (float(sum_wants[r]), int(count[r])) for r in range(len(sum_wants)) if sum_wants[r] > 0}
+    if any(c < 1 or c > 2**31 - 1 for _, c in req.values()):
+        return None
+    return req
+
+
+def leaf_templates(prev: dict, g: int, responses: dict, root_cfg: dict) -> dict:
+    """Server g's configuration after the exchange (server.go:279-313)."""
+    new = {k: np.array(prev[k]) for k in CFG_FIELDS}
+    R = len(new["kind"])
+    for r in range(R):
+        l = responses.get((g, r))
+        if l is not None:
+            new["capacity"][r] = l.has
+            safe = root_cfg["safe_capacity"][r]
+            new["safe_capacity"][r] = 0.0 if np.isnan(safe) else safe
+            new["kind"][r] = root_cfg["kind"][r]
+            new["lease_length_s"][r] = root_cfg["lease_length_s"][r]
+            new["refresh_interval_s"][r] = root_cfg["refresh_interval_s"][r]
+            new["parent_expiry_ns"][r] = (l.expiry_ns // W.NS) * W.NS  # time.Unix(Expiry.Unix(), 0)
+        else:
+            for k, v in DEFAULT_TEMPLATE.items():
+                new[k][r] = v
+    return new
+
+
+def default_config(R: int, learning_end_ns=W.INT64_MIN) -> dict:
+    """An intermediate's configuration before its first exchange: the "*" default
+    template for every resource (NewIntermediate, server.go:575-586)."""
+    cfg = {k: np.full(R, v) for k, v in DEFAULT_TEMPLATE.items()}
+    cfg["kind"] = cfg["kind"].astype(np.int32)
+    cfg["learning_end_ns"] = np.broadcast_to(np.asarray(learning_end_ns, np.int64), (R,)).copy()
+    return cfg
+
+
+def with_config(snap: dict, cfg: dict) -> dict:
+    out = dict(snap)
+    for k in CFG_FIELDS:
+        out[k] = np.array(cfg[k])
+    return out

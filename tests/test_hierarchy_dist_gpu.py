@@ -1,0 +1,121 @@
+"""The product hierarchy across processes: two ranks on GPU 0 (gloo, the
+rehearsal of the node's RCCL all-gather) each run HierarchicalTick -- publish,
+all-gather, their own copy of the root's round, their new templates, their leaf
+tick -- for several rounds.  The parent checks every rank against the reference
+model (tests/hier_model.py, server.go:227-323 -> :822-901): root copies and
+templates bit for bit, leaf leases against the oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from doorman_amd import workloads as W
+from oracle import oracle as O
+import hier_model as M
+from parity_util import assert_leases_match
+
+pytestmark = pytest.mark.gpu
+NOW = W.NOW_NS
+TIMES = [NOW, NOW + 4 * W.NS, NOW + 30 * W.NS]
+R = 40
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _root_cfg():
+    rng = np.random.default_rng(11)
+    return {"kind": rng.choice([W.FAIR_SHARE, W.PROPORTIONAL_SHARE, W.STATIC], R).astype(np.int32),
+            "capacity": rng.choice([500.0, 1000.0], R), "lease_length_s": rng.choice([10, 20], R).astype(np.int64),
+            "refresh_interval_s": np.full(R, 5, np.int64), "learning_end_ns": np.full(R, W.INT64_MIN, np.int64),
+            "parent_expiry_ns": np.full(R, W.INT64_MAX, np.int64),
+            "safe_capacity": np.where(np.arange(R) % 3 == 0, 4.5, np.nan)}
+
+
+def _leaf_snap(rank):
+    s = W.uniform(R, 30 + 17 * rank, kind=W.FAIR_SHARE, seed=300 + rank, capacity=1000.0)
+    return M.with_config(s, M.default_config(R))
+
+
+def _rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import HierarchicalTick
+    cfg = _root_cfg()
+    N = R * world
+    leaf, root = Engine(0), Engine(0)
+    leaf.load(_leaf_snap(rank))
+    root.load(W.make_snapshot(np.full(R, world), np.zeros(N), np.zeros(N), np.zeros(N, np.int64),
+                              np.full(N, W.RELEASED), cfg["kind"], cfg["capacity"], cfg["lease_length_s"],
+                              cfg["refresh_interval_s"], cfg["learning_end_ns"], cfg["parent_expiry_ns"],
+                              cfg["safe_capacity"]))
+
+    def gather(src, dst):  # through host memory: every rank shares one GPU here
+        parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, src.cpu())
+        dst.copy_(torch.cat(parts).to(dst.device))
+
+    ht = HierarchicalTick(torch, leaf, root, R, world, rank, gather)
+    out = []
+    for now in TIMES:
+        pre = {**leaf.read_store(), **leaf.resources(safe=False)}
+        ht.tick(now)
+        leaf.sync()
+        ht.check()
+        out.append({"pre": pre, "root": {**root.read_store(), **root.resources(safe=False)}, "cfg": leaf.config(),
+                    "leases": leaf.leases()})
+    q.put((rank, out))
+    leaf.close()
+    root.close()
+    dist.destroy_process_group()
+
+
+def test_hierarchical_tick_two_processes_matches_the_reference_model():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, out = q.get(timeout=240)
+        res[rank] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    model = M.Root(_root_cfg(), world)
+    tpl = [M.default_config(R) for _ in range(world)]
+    seg_off = [_leaf_snap(g)["seg_off"] for g in range(world)]
+    for t, now in enumerate(TIMES):
+        reqs = [M.server_request(res[g][t]["pre"]["sum_wants"], res[g][t]["pre"]["count"]) for g in range(world)]
+        resp = model.round(now, reqs)
+        rows, sums = model.rows(), model.sums()
+        for g in range(world):
+            got = res[g][t]
+            for k in ("has", "wants", "subclients", "expiry_ns"):
+                assert got["root"][k].tobytes() == rows[k].tobytes(), (t, g, k)
+            for k in ("count", "sum_has", "sum_wants"):
+                assert got["root"][k].tobytes() == sums[k].tobytes(), (t, g, k)
+            tpl[g] = M.leaf_templates(tpl[g], g, resp, model.cfg)
+            for k in W.CFG_FIELDS:
+                np.testing.assert_array_equal(got["cfg"][k], tpl[g][k], err_msg=f"round {t} rank {g} {k}")
+            pre = got["pre"]
+            snap = M.with_config({"seg_off": seg_off[g], "wants": pre["wants"], "has": pre["has"],
+                                  "subclients": pre["subclients"], "expiry_ns": pre["expiry_ns"],
+                                  "agg_count": pre["count"], "agg_sum_has": pre["sum_has"],
+                                  "agg_sum_wants": pre["sum_wants"]}, tpl[g])
+            gets, exp = got["leases"]
+            assert_leases_match(snap, gets, exp, O.apportion(snap, now), f"round {t} rank {g}")

@@ -1,12 +1,23 @@
-"""The intermediate-server hierarchy on one GPU: G simulated servers publish
-their totals, the gathered records feed the root store (dm_hier_load_root), the
-root apportions its G server rows per resource, every server takes its grant
-(dm_hier_take_grants) and runs its leaf tick -- all checked against the oracle
-model of GetServerCapacity (tests/hier_model.py)."""
+"""The intermediate-server hierarchy on one GPU (dm_hier_root_tick), against the
+reference model of tests/hier_model.py -- restated from server.go:227-323,
+:822-901 and resource.go:62-70,117-125, not from the kernels.
+
+G servers each publish their store totals, run the root's round on their own
+copy of the root store (as every rank of a node does) and load their new
+templates, then tick their leaf store.  Per round:
+  * every root copy equals the model's root stores bit for bit (rows and running
+    sums: the kernel decides each request literally in the reference's order);
+  * every leaf's configuration equals the model's templates bit for bit (grant,
+    parent expiry in Unix seconds, the root's algorithm and safe capacity, or the
+    "*" default for resources it did not request; learning end kept);
+  * every leaf's leases match the oracle on that leaf's store and templates.
+"""
+import json
+import os
+
 import numpy as np
 import pytest
 
-from doorman_amd import hierarchy as H
 from doorman_amd import workloads as W
 from oracle import oracle as O
 import hier_model as M
@@ -14,72 +25,244 @@ from parity_util import assert_leases_match
 
 pytestmark = pytest.mark.gpu
 NOW = W.NOW_NS
+HERE = os.path.dirname(os.path.abspath(__file__))
+KATS = json.load(open(os.path.join(HERE, "golden", "reference_kats.json")))
 
 
-@pytest.mark.parametrize("G", [2, 3, 8, 20])
-def test_hierarchy_round(G):
-    import torch
+def root_config(R, rng):
+    """The root's own resource configuration: every kind, learning mode on a few,
+    configured and unset safe capacities, several lease lengths."""
+    kind = rng.choice([W.FAIR_SHARE, W.FAIR_SHARE, W.PROPORTIONAL_SHARE, W.STATIC, W.NO_ALGORITHM], R).astype(np.int32)
+    return {"kind": kind, "capacity": rng.choice([100.0, 1000.0, 2500.5], R),
+            "lease_length_s": rng.choice([7, 20, 60], R).astype(np.int64),
+            "refresh_interval_s": rng.choice([1, 5], R).astype(np.int64),
+            "learning_end_ns": np.where(rng.random(R) < 0.1, NOW + 3 * W.NS, W.INT64_MIN).astype(np.int64),
+            "parent_expiry_ns": np.full(R, W.INT64_MAX, np.int64),
+            "safe_capacity": np.where(rng.random(R) < 0.5, np.nan, rng.uniform(1, 9, R))}
+
+
+def root_engine(cfg, G):
     from doorman_amd.engine import Engine
-    R = 64
-    torch.cuda.set_device(0)
-    rng = np.random.default_rng(G)
-    leaves, snaps = [], []
-    for g in range(G):
-        s = W.uniform(R, int(rng.integers(5, 300)), kind=W.FAIR_SHARE, seed=10 * G + g, capacity=1000.0)
-        s["wants"] *= rng.uniform(0.2, 3.0)  # servers differ in appetite
-        if g == 1:
-            s["wants"][: len(s["wants"]) // 4] = 0.0  # some resources not requested by server 1
-        W.add_store_sums(s)
-        e = Engine(0)
-        e.load(s)
-        leaves.append(e)
-        snaps.append(s)
-    root = Engine(0)
-    rsnap = H.root_snapshot(R, G, W.FAIR_SHARE, 1000.0, lease_length_s=20)
-    root.load(rsnap)
-    dev = torch.device("cuda", 0)
-    gathered = torch.empty((G * R, 2), dtype=torch.float64, device=dev)
-    for g, e in enumerate(leaves):
-        e.publish_totals(gathered[g * R:(g + 1) * R].data_ptr())
-        e.sync()
+    R = len(cfg["kind"])
+    N = R * G
+    snap = W.make_snapshot(np.full(R, G), np.zeros(N), np.zeros(N), np.zeros(N, np.int64), np.full(N, W.RELEASED),
+                           cfg["kind"], cfg["capacity"], cfg["lease_length_s"], cfg["refresh_interval_s"],
+                           cfg["learning_end_ns"], cfg["parent_expiry_ns"], cfg["safe_capacity"])
+    e = Engine(0)
+    e.load(snap)
+    return e
+
+
+def leaf_snapshot(e, cfg):
+    """The leaf's store as the device holds it (rows + running sums) under `cfg`."""
+    st = e.read_store()
+    res = e.resources(safe=False)
+    R = e.n_resources
+    snap = dict(cfg)
+    snap.update({"wants": st["wants"], "has": st["has"], "subclients": st["subclients"], "expiry_ns": st["expiry_ns"],
+                 "agg_count": res["count"], "agg_sum_has": res["sum_has"], "agg_sum_wants": res["sum_wants"]})
+    snap["seg_off"] = e.seg_off
+    assert len(snap["seg_off"]) == R + 1
+    return snap
+
+
+def assert_cfg_equal(got, want, label):
+    for k in W.CFG_FIELDS:
+        a, b = np.asarray(got[k]), np.asarray(want[k])
+        same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
+        assert same.all(), f"{label}: template field {k} differs at resources {np.flatnonzero(~same)[:8].tolist()}: " \
+                           f"{a[~same][:4].tolist()} vs {b[~same][:4].tolist()}"
+
+
+def assert_root_equal(e, model, label):
+    st, res = e.read_store(), e.resources(safe=False)
+    rows, sums = model.rows(), model.sums()
+    for k in ("has", "wants", "subclients", "expiry_ns"):
+        assert st[k].tobytes() == rows[k].tobytes(), f"{label}: root {k} rows " \
+            f"{np.flatnonzero(st[k] != rows[k])[:8].tolist()}"
+    for k in ("count", "sum_has", "sum_wants"):
+        assert res[k].tobytes() == sums[k].tobytes(), f"{label}: root running {k}"
+
+
+def published(gathered, G, R):
+    rec = gathered.cpu().numpy()
+    return [(rec[g * R:(g + 1) * R, 0].copy(), rec[g * R:(g + 1) * R, 1].copy().view(np.int64)) for g in range(G)]
+
+
+def exchange_all(L, roots, leaves, gathered, G, now):
     from doorman_amd import _lib
-    _lib.check(_lib.lib().dm_hier_load_root(root._ctx, gathered.data_ptr(), G, NOW), root._ctx)
-    root.apportion(NOW, writeback=True, recompute=True)
-    rg, rexp = root.leases()
-    # model: totals as published (store SumWants / Count, server.go:241-249)
-    host = gathered.cpu().numpy()
-    totals = [(host[g * R:(g + 1) * R, 0].copy(), host[g * R:(g + 1) * R, 1].copy().view(np.int64))
-              for g in range(G)]
     for g in range(G):
-        np.testing.assert_array_equal(totals[g][1], snaps[g]["agg_count"])
-    msnap = M.root_from_totals(totals, 1000.0, W.FAIR_SHARE, 20, np.zeros(R * G), NOW)
-    mout = O.apportion(msnap, NOW)
-    assert_leases_match(msnap, rg, rexp, mout, f"root G={G}")
-    for g, e in enumerate(leaves):
-        _lib.check(_lib.lib().dm_hier_take_grants(root._ctx, e._ctx, g), root._ctx)
-        cap, parent, live = M.grants(msnap, mout, G, g)
-        leaf = dict(snaps[g])
-        leaf["capacity"] = np.where(live, cap, snaps[g]["capacity"])
-        leaf["parent_expiry_ns"] = np.where(live, parent, snaps[g]["parent_expiry_ns"])
-        e.apportion(NOW, writeback=False)
-        gets, exp = e.leases()
-        assert_leases_match(leaf, gets, exp, O.apportion(leaf, NOW), f"leaf {g} of {G}")
-        # and past the grant's expiry the leaf's capacity is 0 (resource.go:62-70)
-        later = NOW + 25 * W.NS
-        e.apportion(later, writeback=False)
-        gets2, exp2 = e.leases()
-        assert_leases_match(leaf, gets2, exp2, O.apportion(leaf, later), f"leaf {g} after parent expiry")
-    for e in leaves + [root]:
+        _lib.check(L.dm_hier_root_tick(roots[g]._ctx, gathered.data_ptr(), G, now, leaves[g]._ctx, g), roots[g]._ctx)
+    for e in roots + leaves:
+        e.sync()
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 8, 20])
+def test_hierarchy_rounds_match_the_reference_model(G):
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    L = _lib.lib()
+    R = 48
+    rng = np.random.default_rng(G)
+    rcfg = root_config(R, rng)
+    leaves, tpl = [], []
+    for g in range(G):
+        s = W.uniform(R, int(rng.integers(3, 120)), kind=W.FAIR_SHARE, seed=10 * G + g, capacity=1000.0)
+        s["wants"] *= rng.uniform(0.2, 3.0)  # servers differ in appetite
+        W.add_store_sums(s)
+        cfg = M.default_config(R, np.where(rng.random(R) < 0.1, NOW + 2 * W.NS, W.INT64_MIN))
+        e = Engine(0)
+        e.load(M.with_config(s, cfg))
+        leaves.append(e)
+        tpl.append(cfg)
+    roots = [root_engine(rcfg, G) for _ in range(G)]
+    model = M.Root(rcfg, G)
+    gathered = torch.zeros((G * R, 2), dtype=torch.float64, device="cuda")
+    for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 40 * W.NS]):
+        if t == 2 and G > 1:  # server 1 stops asking for a quarter of the resources
+            so = leaves[1].seg_off
+            rows = np.arange(so[0], so[R // 4])
+            leaves[1].update_wants(rows, np.zeros(len(rows)))
+        for g in range(G):
+            leaves[g].publish_totals(gathered[g * R:(g + 1) * R].data_ptr())
+            leaves[g].sync()
+        totals = published(gathered, G, R)
+        for g in range(G):  # what the leaves publish: their store's running sums (server.go:235-250)
+            res = leaves[g].resources(safe=False)
+            assert totals[g][0].tobytes() == res["sum_wants"].tobytes()
+            assert totals[g][1].tobytes() == res["count"].tobytes()
+        reqs = [M.server_request(*totals[g]) for g in range(G)]
+        resp = model.round(now, reqs)
+        pre = [leaf_snapshot(leaves[g], tpl[g]) for g in range(G)]
+        exchange_all(L, roots, leaves, gathered, G, now)
+        for g in range(G):
+            if reqs[g] is not None:
+                tpl[g] = M.leaf_templates(tpl[g], g, resp, model.cfg)
+            assert_root_equal(roots[g], model, f"G={G} round {t} root copy {g}")
+            assert_cfg_equal(leaves[g].config(), tpl[g], f"G={G} round {t} leaf {g}")
+        for g in range(G):
+            leaves[g].apportion(now, writeback=True)
+            gets, exp = leaves[g].leases()
+            ref = O.apportion(M.with_config(pre[g], tpl[g]), now)
+            assert_leases_match(pre[g], gets, exp, ref, f"G={G} round {t} leaf {g}")
+            cap, ex, ref_s = leaves[g].leases_proto()
+            live = exp != W.RELEASED
+            so = pre[g]["seg_off"]
+            refresh_row = np.repeat(tpl[g]["refresh_interval_s"], np.diff(so))
+            np.testing.assert_array_equal(ref_s[live], refresh_row[live])  # the root's refresh interval
+    for e in leaves + roots:
         e.close()
 
 
-def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
-    """HierarchicalTick orders publish -> gather -> root -> grants -> leaf tick on one
-    stream (not torch's null stream, which dm_set_stream cannot select): three
-    asynchronous steps leave the same leaf leases as the same steps run with a sync
-    after every stage."""
+def test_rejected_server_keeps_its_templates_and_root_rows():
+    """server.go:863-866: a band with num_clients < 1 fails the server's whole
+    GetServerCapacity (InvalidArgument): that server requests nothing this round,
+    its root leases stay, its leaf templates stay (performRequests returns before
+    LoadConfig, :268-272); the other servers' round is unaffected.  A Count beyond
+    the root's 32-bit column is rejected the same way, never clamped."""
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import HierarchicalTick
+    torch.cuda.set_device(0)
+    L = _lib.lib()
+    R, G = 16, 3
+    rng = np.random.default_rng(5)
+    rcfg = root_config(R, rng)
+    rcfg["learning_end_ns"][:] = W.INT64_MIN
+    model = M.Root(rcfg, G)
+    roots = [root_engine(rcfg, G) for _ in range(G)]
+    leaves, tpl = [], []
+    for g in range(G):
+        s = W.uniform(R, 10, kind=W.FAIR_SHARE, seed=40 + g)
+        cfg = M.default_config(R)
+        e = Engine(0)
+        e.load(M.with_config(s, cfg))
+        leaves.append(e)
+        tpl.append(cfg)
+    rec = np.zeros((G * R, 2))
+    rec[:, 0] = rng.uniform(10.0, 900.0, G * R)
+    cnt = rng.integers(1, 40, G * R).astype(np.int64)
+    for t, (bad, value) in enumerate([(None, None), (1, 0), (2, 2**31), (None, None)]):
+        c = cnt.copy()
+        if bad is not None:
+            c[bad * R + 5] = value
+        rec[:, 1] = c.view(np.float64)
+        gathered = torch.from_numpy(rec).to("cuda")
+        totals = [(rec[g * R:(g + 1) * R, 0], c[g * R:(g + 1) * R]) for g in range(G)]
+        reqs = [M.server_request(*totals[g]) for g in range(G)]
+        now = NOW + t * W.NS
+        resp = model.round(now, reqs)
+        exchange_all(L, roots, leaves, gathered, G, now)
+        st = np.zeros(G, np.uint32)
+        nbad = _lib.check(L.dm_hier_status(roots[0]._ctx, st.ctypes.data, G), roots[0]._ctx)
+        want = np.zeros(G, np.uint32)
+        if bad is not None:
+            want[bad] = _lib.DM_HIER_INVALID if value < 1 else _lib.DM_HIER_COUNT_RANGE
+        np.testing.assert_array_equal(st, want)
+        assert nbad == int((want != 0).sum())
+        for g in range(G):
+            if reqs[g] is not None:
+                tpl[g] = M.leaf_templates(tpl[g], g, resp, model.cfg)
+            assert_root_equal(roots[g], model, f"round {t} root {g}")
+            assert_cfg_equal(leaves[g].config(), tpl[g], f"round {t} leaf {g}")
+    # HierarchicalTick.check() raises for a rejected server
+    ht = HierarchicalTick(torch, leaves[0], roots[0], R, G, 0, lambda src, dst: None)
+    c = cnt.copy()
+    c[3] = 0
+    rec[:, 1] = c.view(np.float64)
+    ht.gathered.copy_(torch.from_numpy(rec))
+    L.dm_hier_root_tick(roots[0]._ctx, ht.gathered.data_ptr(), G, NOW + 9 * W.NS, leaves[0]._ctx, 0)
+    with pytest.raises(_lib.DmError):
+        ht.check()
+    for e in leaves + roots:
+        e.close()
+
+
+@pytest.mark.parametrize("case", KATS["hierarchy"], ids=lambda c: c["name"])
+def test_intermediate_server_update_kat(case):
+    """server_test.go:574-658 through the product: an intermediate whose store holds
+    a downstream server's band (wants 100, 10 subclients) grants 0 under the "*"
+    default template, then 100 once its exchange with the root (FairShare, capacity
+    100) has run."""
     import torch
     from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import HierarchicalTick
+    torch.cuda.set_device(0)
+    rt, it, band = case["root"], case["intermediate_default"], case["band"]
+    leaf_cfg = {"kind": [it["kind"]], "capacity": [float(it["capacity"])], "lease_length_s": [it["lease_length"]],
+                "refresh_interval_s": [it["refresh_interval"]], "learning_end_ns": [W.INT64_MIN],
+                "parent_expiry_ns": [W.INT64_MAX], "safe_capacity": [float(it["safe_capacity"])]}
+    leaf = Engine(0)
+    leaf.load(M.with_config(W.make_snapshot([1], [band["wants"]], [0.0], [band["num_clients"]], [NOW + 60 * W.NS],
+                                            W.FAIR_SHARE, 0.0), leaf_cfg))
+    leaf.apportion(NOW, writeback=True)
+    assert leaf.leases()[0][0] == case["gets_before_exchange"]
+    rcfg = {"kind": np.array([rt["kind"]], np.int32), "capacity": np.array([float(rt["capacity"])]),
+            "lease_length_s": np.array([rt["lease_length"]]), "refresh_interval_s": np.array([rt["refresh_interval"]]),
+            "learning_end_ns": np.array([W.INT64_MIN]), "parent_expiry_ns": np.array([W.INT64_MAX]),
+            "safe_capacity": np.array([np.nan])}
+    root = root_engine(rcfg, 1)
+    ht = HierarchicalTick(torch, leaf, root, 1, 1, 0, lambda src, dst: dst.copy_(src))
+    ht.tick(NOW + W.NS)  # the exchange, then the intermediate decides again
+    leaf.sync()
+    ht.check()
+    assert leaf.leases()[0][0] == case["gets_after_exchange"]
+    assert leaf.config()["capacity"][0] == case["gets_after_exchange"]
+    leaf.close()
+    root.close()
+
+
+def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
+    """HierarchicalTick orders publish -> gather -> root round -> templates -> leaf
+    tick on one stream (not torch's null stream, which dm_set_stream cannot
+    select): three asynchronous steps leave the same leaf leases as the same steps
+    run with a sync after every stage."""
+    import torch
+    from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
     torch.cuda.set_device(0)
     R = 300
     snap = W.uniform(R, 200, kind=W.FAIR_SHARE, seed=77, capacity=1000.0)
@@ -91,8 +274,8 @@ def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
     for sync_each in (False, True):
         leaf, root = Engine(0), Engine(0)
         leaf.load(snap)
-        root.load(H.root_snapshot(R, 1, W.FAIR_SHARE, np.asarray(snap["capacity"]), lease_length_s=20))
-        ht = H.HierarchicalTick(torch, leaf, root, R, 1, 0, gather)
+        root.load(root_snapshot(R, 1, W.FAIR_SHARE, np.asarray(snap["capacity"]), lease_length_s=20))
+        ht = HierarchicalTick(torch, leaf, root, R, 1, 0, gather)
         assert leaf.stream == root.stream == ht.stream.cuda_stream != 0
         for t in range(3):
             if sync_each:
@@ -108,48 +291,3 @@ def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
         root.close()
     (g1, e1), (g2, e2) = outs
     assert g1.tobytes() == g2.tobytes() and e1.tobytes() == e2.tobytes()
-
-
-@pytest.mark.parametrize("G", [1, 2, 3, 8, 20])
-def test_hier_root_tick_matches_separate_calls(G):
-    """dm_hier_root_tick (one fused launch for G <= 8, the three calls above) leaves
-    the root store, its running sums and the leaf's template exactly as
-    dm_hier_load_root + dm_apportion(WRITEBACK | AGG_RECOMPUTE) + dm_hier_take_grants;
-    two rounds, so the second sees the first's root leases."""
-    import torch
-    from doorman_amd import _lib
-    from doorman_amd.engine import Engine
-    torch.cuda.set_device(0)
-    R = 257
-    rng = np.random.default_rng(100 + G)
-    snap = W.uniform(R, 40, kind=W.FAIR_SHARE, seed=5 + G, capacity=1000.0)
-    rec = np.empty((G * R, 2))
-    rec[:, 0] = rng.uniform(0.0, 600.0, G * R) * (rng.random(G * R) > 0.1)
-    rec[:, 1] = rng.integers(0, 50, G * R).astype(np.int64).view(np.float64)
-    gathered = torch.from_numpy(rec).to("cuda")
-    L = _lib.lib()
-    outs = []
-    for fused in (True, False):
-        leaf, root = Engine(0), Engine(0)
-        leaf.load(snap)
-        root.load(H.root_snapshot(R, G, W.FAIR_SHARE, np.asarray(snap["capacity"]) * G, lease_length_s=20))
-        for t in range(2):
-            now = NOW + t * W.NS
-            server = (t + G - 1) % G
-            if fused:
-                _lib.check(L.dm_hier_root_tick(root._ctx, gathered.data_ptr(), G, now, leaf._ctx, server), root._ctx)
-            else:
-                _lib.check(L.dm_hier_load_root(root._ctx, gathered.data_ptr(), G, now), root._ctx)
-                root.apportion(now, writeback=True, recompute=True)
-                _lib.check(L.dm_hier_take_grants(root._ctx, leaf._ctx, server), root._ctx)
-        root.sync()
-        leaf.apportion(NOW + W.NS, writeback=False)
-        outs.append((root.read_store(), root.resources(safe=False), leaf.leases()))
-        leaf.close()
-        root.close()
-    (s1, r1, l1), (s2, r2, l2) = outs
-    for k in ("has", "wants", "subclients", "expiry_ns"):
-        assert s1[k].tobytes() == s2[k].tobytes(), k
-    for k in ("count", "sum_has", "sum_wants"):
-        assert r1[k].tobytes() == r2[k].tobytes(), k
-    assert l1[0].tobytes() == l2[0].tobytes() and l1[1].tobytes() == l2[1].tobytes()

@@ -21,12 +21,12 @@ NOW = W.NOW_NS
 
 @pytest.mark.parametrize("case", KATS["sequential"], ids=lambda c: c["name"])
 def test_sequential_tables(case):
-    """algorithm_test.go:244-272 testAlgorithm: sequential requests, one mutating store."""
+    """algorithm_test.go:34-62 testAlgorithm: sequential requests, one mutating store."""
     ids = {}
     for c in case["cases"]:
         ids.setdefault(c[0], len(ids))
     store = O.Store(len(ids))
-    if case["preload"]:  # :247-254, lease 300 s, refresh 5 s
+    if case["preload"]:  # :37-44, lease 300 s, refresh 5 s
         for name, has, wants, _, sub in case["cases"]:
             store.assign(ids[name], 300, 5, has, wants, sub, NOW)
     for i, (name, has, wants, should_get, sub) in enumerate(case["cases"]):
@@ -110,6 +110,12 @@ def test_server_kats(case):
         assert lease.has == case["gets"]
         return
     store, cfg = O.Store(1), _cfg(case, master_at)
+    if "release" in case:  # TestReleaseCapacity: a lease, then ReleaseCapacity (server.go:668-714)
+        rel = case["release"]
+        O.decide(store, cfg, 0, rel["request"]["has"], rel["request"]["wants"], 1, NOW)
+        store.release(0)  # "resource"; "nonexisting_resource" is unknown and ignored (:705-710)
+        assert store.sum_has() == rel["post_sum_has"]
+        return
     for step in case["steps"]:
         if step.get("new_resource"):
             store, cfg = O.Store(1), _cfg(case, NOW - step["age_s"] * W.NS)
@@ -155,7 +161,8 @@ def test_unknown_kind_is_an_error():
         O.apportion(snap, NOW, "closed")
 
 
-@pytest.mark.parametrize("case", [c for c in KATS["server"] if "error" not in c], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", [c for c in KATS["server"] if "error" not in c and "release" not in c],
+                         ids=lambda c: c["name"])
 def test_server_kats_as_one_row_snapshots(case):
     """For a single client, Decide on an empty store (the reference's first request)
     and the snapshot tick of a store holding only that client agree: count,
@@ -189,3 +196,28 @@ def server_kat_snapshots(case):
                                     cfg["capacity"], cfg["lease_length_s"], cfg["refresh_interval_s"],
                                     cfg["learning_end_ns"]), step["gets"]))
     return out
+
+
+@pytest.mark.parametrize("case", KATS["hierarchy"], ids=lambda c: c["name"])
+def test_hierarchy_kat_model(case):
+    """server_test.go:574-658 replayed on the reference model of the hierarchy
+    (tests/hier_model.py): 0 before the intermediate's first exchange with the root,
+    the full capacity after it."""
+    import hier_model as M
+    rt, it, band = case["root"], case["intermediate_default"], case["band"]
+    root_cfg = {"kind": [rt["kind"]], "capacity": [rt["capacity"]], "lease_length_s": [rt["lease_length"]],
+                "refresh_interval_s": [rt["refresh_interval"]], "learning_end_ns": [W.INT64_MIN],
+                "parent_expiry_ns": [W.INT64_MAX], "safe_capacity": [np.nan]}
+    leaf_cfg = {"kind": [it["kind"]], "capacity": [float(it["capacity"])], "lease_length_s": [it["lease_length"]],
+                "refresh_interval_s": [it["refresh_interval"]], "learning_end_ns": [W.INT64_MIN],
+                "parent_expiry_ns": [W.INT64_MAX], "safe_capacity": [float(it["safe_capacity"])]}
+    leaf = O.Store(1)
+    # the downstream server's band reaches the intermediate before its first exchange
+    lease = O.decide(leaf, M.cfg_table(leaf_cfg)[0], 0, 0.0, band["wants"], band["num_clients"], NOW)
+    assert lease.has == case["gets_before_exchange"]
+    root = M.Root(root_cfg, 1)
+    req = M.server_request([leaf.sum_wants()], [leaf.count()])
+    resp = root.round(NOW, [req])
+    leaf_cfg = M.leaf_templates(leaf_cfg, 0, resp, root.cfg)
+    lease = O.decide(leaf, M.cfg_table(leaf_cfg)[0], 0, 0.0, band["wants"], band["num_clients"], NOW + W.NS)
+    assert lease.has == case["gets_after_exchange"]

@@ -1,6 +1,6 @@
 """Resource sharding and the hierarchy exchange on CPU (no GPU): the partition
-function, and a world_size-2 gloo run of the publish -> all-gather -> root ->
-grant exchange with the oracle as the evaluator."""
+function, and a world_size-2 gloo run of the publish -> all-gather -> root round
+exchange evaluated by the reference model (tests/hier_model.py)."""
 import os
 import socket
 
@@ -54,19 +54,29 @@ def _worker(rank, world, port, R, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     now = W.NOW_NS
     leaf = W.uniform(R, 50 + 10 * rank, kind=W.FAIR_SHARE, seed=100 + rank)
-    sw, cnt = M.leaf_totals(leaf, now)
-    rec = torch.tensor(np.stack([sw, cnt.view(np.float64)], axis=1))  # the 16-byte device records
+    rec = torch.tensor(np.stack([leaf["agg_sum_wants"], leaf["agg_count"].view(np.float64)], axis=1))
     out = [torch.empty_like(rec) for _ in range(world)]
-    dist.all_gather(out, rec)
+    dist.all_gather(out, rec)  # the 16-byte records every rank publishes (server.go:242-253)
     totals = [(o[:, 0].numpy().copy(), o[:, 1].numpy().copy().view(np.int64)) for o in out]
-    root = M.root_from_totals(totals, 1000.0, W.FAIR_SHARE, 20, np.zeros(R * world), now)
-    ro = O.apportion(root, now, "closed")
-    cap, parent, live = M.grants(root, ro, world, rank)
-    q.put((rank, cap, parent, live, sw, cnt))
+    root = M.Root(_root_cfg(R), world)  # every rank evaluates the root redundantly
+    resp = root.round(now, [M.server_request(*t) for t in totals])
+    tpl = M.leaf_templates(M.default_config(R), rank, resp, root.cfg)
+    q.put((rank, tpl["capacity"], tpl["parent_expiry_ns"], leaf["agg_sum_wants"], leaf["agg_count"]))
     dist.destroy_process_group()
 
 
+def _root_cfg(R):
+    return {"kind": np.full(R, W.FAIR_SHARE, np.int32), "capacity": np.full(R, 1000.0),
+            "lease_length_s": np.full(R, 20), "refresh_interval_s": np.full(R, 5),
+            "learning_end_ns": np.full(R, W.INT64_MIN), "parent_expiry_ns": np.full(R, W.INT64_MAX),
+            "safe_capacity": np.full(R, np.nan)}
+
+
 def test_hierarchy_exchange_gloo_world2():
+    """Two ranks exchange their totals over gloo and each evaluates the root's round
+    on the reference model: both agree with a central evaluation of the same
+    requests.
+    (The product path across processes: tests/test_hierarchy_dist_gpu.py.)"""
     import torch.multiprocessing as mp
     R, world = 16, 2
     ctx = mp.get_context("spawn")
@@ -77,22 +87,20 @@ def test_hierarchy_exchange_gloo_world2():
         p.start()
     res = {}
     for _ in range(world):
-        rank, cap, parent, live, sw, cnt = q.get(timeout=120)
-        res[rank] = (cap, parent, live, sw, cnt)
+        rank, cap, parent, sw, cnt = q.get(timeout=120)
+        res[rank] = (cap, parent, sw, cnt)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # the same root, evaluated centrally from both servers' totals
-    totals = [(res[g][3], res[g][4]) for g in range(world)]
-    root = M.root_from_totals(totals, 1000.0, W.FAIR_SHARE, 20, np.zeros(R * world), W.NOW_NS)
-    ro = O.apportion(root, W.NOW_NS)
+    root = M.Root(_root_cfg(R), world)
+    resp = root.round(W.NOW_NS, [M.server_request(res[g][2], res[g][3]) for g in range(world)])
     for g in range(world):
-        cap, parent, live = M.grants(root, ro, world, g)
-        np.testing.assert_array_equal(res[g][0], cap)
-        np.testing.assert_array_equal(res[g][1], parent)
-    # every server asked for more than its share: FairShare splits the capacity by subclients
-    tot = res[0][0] + res[1][0]
-    assert np.all(tot <= 1000.0 + 1e-9)
+        tpl = M.leaf_templates(M.default_config(R), g, resp, root.cfg)
+        np.testing.assert_array_equal(res[g][0], tpl["capacity"])
+        np.testing.assert_array_equal(res[g][1], tpl["parent_expiry_ns"])
+    # both requests see the same (empty) root store, so each may get the whole
+    # capacity this round (the round's snapshot semantics); never more than it
+    assert np.all(res[0][0] <= 1000.0) and np.all(res[1][0] <= 1000.0)
 
 
 def test_rows_to_mask_round_trip():
