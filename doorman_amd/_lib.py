@@ -102,6 +102,7 @@ _SIGS = {
     "dm_aggregate_bands": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "dm_publish_totals": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_decide": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 6),
     "dm_read_config": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 7),
     "dm_hier_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

@@ -140,6 +140,21 @@ struct DevParams {
   int32_t pad;
 };
 
+// dm_decide: one resource and its requests [qlo, qhi) (sorted by row)
+struct ReqItem {
+  int32_t seg;
+  int32_t pad;
+  int64_t qlo, qhi;
+};
+struct ReqArgs {
+  const int64_t* rows;  // the row the request's lease is written to (its client's row, or a free row)
+  const double* has;    // Request.Has (read by Learn only)
+  const double* wants;
+  const int64_t* sub;
+  double* gets;
+  int64_t* expiry;
+};
+
 // dm_hier_root_tick: one exchange round of the hierarchy's root (k_hier_tick)
 constexpr int kHierMaxServers = 64;     // one lane per server row, whole resources per wave
 constexpr uint32_t kHierInvalid = 1u;    // a band with num_clients < 1: InvalidArgument (server.go:863-866)

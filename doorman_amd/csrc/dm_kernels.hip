@@ -16,347 +16,9 @@
 // -ffp-contract=off), minF = `l > r ? r : l`, IEEE division by zero.
 #include <hip/hip_runtime.h>
 
-#include "dm_device.h"
+#include "dm_kernel_util.h"
 
 namespace dm {
-
-// --------------------------------------------------------------------------
-// helpers
-// --------------------------------------------------------------------------
-__device__ __forceinline__ double minF(double l, double r) { return l > r ? r : l; }  // algorithm.go:50-55
-
-struct Res {
-  int32_t kind;
-  int32_t learning;
-  double C;        // Resource.capacity() (resource.go:62-70)
-  double cap_cfg;  // config capacity (SetSafeCapacity, resource.go:92)
-  double safe;
-  int64_t exp_out; // now + lease_length (store.go:161)
-  // the store's running sums, loaded with the config so that no global load
-  // waits behind the first reduction's barrier
-  long long agg_count;
-  double agg_has;
-  double agg_wants;
-};
-
-__device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
-  Res r;
-  const ResCfg c = p.cfg[seg];
-  r.kind = c.kind;
-  r.learning = c.learning_end_ns > p.now;  // resource.go:108 learningModeEndTime.After(now)
-  r.cap_cfg = c.capacity;
-  r.C = (c.parent_expiry_ns < p.now) ? 0.0 : r.cap_cfg;  // expiryTime.Before(now)
-  r.safe = c.safe_capacity;
-  r.exp_out = p.now + c.lease_len_ns;
-  if (!p.recompute) {
-    const ResAgg g = p.agg[seg];
-    r.agg_count = g.count;
-    r.agg_has = g.sum_has;
-    r.agg_wants = g.sum_wants;
-  } else {
-    r.agg_count = 0;
-    r.agg_has = 0.0;
-    r.agg_wants = 0.0;
-  }
-  return r;
-}
-
-template <typename T>
-__device__ __forceinline__ T shfl_any(const T& v, int lane) {
-  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
-  __builtin_memcpy(src, &v, sizeof(T));
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __shfl(src[i], lane, 64);
-  T r;
-  __builtin_memcpy(&r, dst, sizeof(T));
-  return r;
-}
-
-// DPP lane permute of every dword of v (a VALU operand modifier: no LDS trip).
-template <int CTRL, typename T>
-__device__ __forceinline__ T dpp_any(const T& v) {
-  static_assert(sizeof(T) % 4 == 0, "4-byte granular");
-  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
-  __builtin_memcpy(src, &v, sizeof(T));
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i)
-    dst[i] = __builtin_amdgcn_update_dpp(0, src[i], CTRL, 0xF, 0xF, true);
-  T r;
-  __builtin_memcpy(&r, dst, sizeof(T));
-  return r;
-}
-
-template <typename T>
-__device__ __forceinline__ T readlane_any(const T& v, int lane) {
-  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
-  __builtin_memcpy(src, &v, sizeof(T));
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __builtin_amdgcn_readlane(src[i], lane);
-  T r;
-  __builtin_memcpy(&r, dst, sizeof(T));
-  return r;
-}
-
-// Wave reduction: a DPP butterfly inside each 16-lane row (xor 1, xor 2, half
-// mirror, mirror: partner lanes compute a+b and b+a, so every lane of a row holds
-// the same row total), then the four row totals combined in a fixed order from
-// scalar readlanes.  Requires all 64 lanes active.
-// Sub-wave groups (G = 16: one DPP row, G = 32: half a wave) reduce within
-// themselves: every lane of the group gets its group's total.
-template <int G, typename T, typename Op>
-__device__ __forceinline__ T wave_reduce_g(T v, Op op) {
-  static_assert(G == 16 || G == 32 || G == 64, "sub-wave group");
-  v = op(v, dpp_any<0xB1>(v));   // quad_perm [1,0,3,2]
-  v = op(v, dpp_any<0x4E>(v));   // quad_perm [2,3,0,1]
-  v = op(v, dpp_any<0x141>(v));  // row_half_mirror
-  v = op(v, dpp_any<0x140>(v));  // row_mirror
-  if constexpr (G == 16) {
-    return v;
-  } else {
-    const T r0 = readlane_any(v, 0), r1 = readlane_any(v, 16), r2 = readlane_any(v, 32), r3 = readlane_any(v, 48);
-    if constexpr (G == 32) {
-      const T lo = op(r0, r1), hi = op(r2, r3);
-      return (threadIdx.x & 32) ? hi : lo;
-    } else {
-      return op(op(r0, r1), op(r2, r3));
-    }
-  }
-}
-template <typename T, typename Op>
-__device__ __forceinline__ T wave_reduce(T v, Op op) {
-  return wave_reduce_g<64>(v, op);
-}
-
-// Group reduction (G = 64: one wave; G >= 256: the waves' totals through LDS).
-// Every thread combines the wave totals in the same fixed order, so all threads
-// (and all workgroups reducing the same inputs) agree bit for bit.
-// REUSE = false: the LDS slots are written once per workgroup (group_segment
-// gives every reduction its own slots), so the barrier that protects them from
-// the next reduction's writes is dropped.
-template <int G, typename T, typename Op, bool REUSE = true>
-__device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
-  v = wave_reduce_g<(G < 64 ? G : 64)>(v, op);
-  if constexpr (G <= 64) {
-    (void)lds;
-    return v;
-  } else {
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) lds[w] = v;
-    __syncthreads();
-    T r = lds[0];
-#pragma unroll 3
-    for (int i = 1; i < G / 64; ++i) {
-      const T x = lds[i];
-      r = op(r, x);
-    }
-    if constexpr (REUSE) __syncthreads();
-    return r;
-  }
-}
-
-struct AggR {  // every row: the store's sums rebuilt by Assign (recompute mode)
-  long long cnt;
-  double h;
-  double w;
-};
-struct OpR {
-  __device__ AggR operator()(AggR a, AggR b) const {
-    AggR r;
-    r.cnt = a.cnt + b.cnt;
-    r.h = a.h + b.h;
-    r.w = a.w + b.w;
-    return r;
-  }
-};
-
-struct AggA {
-  long long cnt;  // leases Clean releases (expired rows)
-  double h;
-  double w;
-  AggR all;       // filled in recompute mode only
-  int smin;       // live rows' subclients range and any NaN wants
-  int smax;
-  int nan;
-  int pad;
-};
-struct OpA {
-  __device__ AggA operator()(AggA a, AggA b) const {
-    AggA r;
-    r.cnt = a.cnt + b.cnt;
-    r.h = a.h + b.h;
-    r.w = a.w + b.w;
-    r.all = a.all;
-    r.smin = a.smin < b.smin ? a.smin : b.smin;
-    r.smax = a.smax > b.smax ? a.smax : b.smax;
-    r.nan = a.nan | b.nan;
-    r.pad = 0;
-    return r;
-  }
-};
-__device__ __forceinline__ AggA zeroA() {
-  AggA a;
-  a.cnt = 0;
-  a.h = 0.0;
-  a.w = 0.0;
-  a.all = AggR{0, 0.0, 0.0};
-  a.smin = INT32_MAX;
-  a.smax = INT32_MIN;
-  a.nan = 0;
-  a.pad = 0;
-  return a;
-}
-
-struct AggB {
-  double x;    // FS: extra (E)          PS: extraCapacity
-  double y;    //                        PS: extraNeed
-  long long i; // FS: wantExtra (W)
-};
-struct OpB {
-  __device__ AggB operator()(AggB a, AggB b) const {
-    AggB r;
-    r.x = a.x + b.x;
-    r.y = a.y + b.y;
-    r.i = a.i + b.i;
-    return r;
-  }
-};
-
-struct AggC {
-  double ee;      // extraExtra
-  long long sgt;  // sum of subclients of wantExtraClients above T
-};
-struct OpC {
-  __device__ AggC operator()(AggC a, AggC b) const {
-    AggC r;
-    r.ee = a.ee + b.ee;
-    r.sgt = a.sgt + b.sgt;
-    return r;
-  }
-};
-
-struct TMin {
-  double t;
-  int found;
-  int pad;
-};
-struct OpTMin {
-  __device__ TMin operator()(TMin a, TMin b) const {
-    const bool take_b = b.found && (!a.found || b.t < a.t);
-    TMin r;
-    r.t = take_b ? b.t : a.t;
-    r.found = a.found | b.found;
-    r.pad = 0;
-    return r;
-  }
-};
-__device__ __forceinline__ void tmin_add(TMin& m, double T) {
-  const bool take = !m.found || T < m.t;
-  m.t = take ? T : m.t;
-  m.found = 1;
-}
-
-struct SumD {
-  double v;
-};
-struct OpSumD {
-  __device__ SumD operator()(SumD a, SumD b) const { return SumD{a.v + b.v}; }
-};
-
-template <int G>
-struct Lds {  // one slot per wave (unused by groups of one wave or less)
-  static constexpr int W = G >= 64 ? G / 64 : 1;
-  AggA a[W];
-  AggR r[W];
-  AggB b[W];
-  AggC c[W];
-  TMin t[W];
-  SumD d[W];
-};
-
-// Cleaned store sums from pass A (store.go:169-181 applied to the snapshot).
-struct Clean {
-  long long count;
-  double sum_has;
-  double sum_wants;
-};
-__device__ __forceinline__ Clean clean_from(const DevParams& p, const Res& rs, const AggA& a) {
-  // store sums (running, or rebuilt from every row) minus the leases Clean releases
-  Clean c;
-  if (p.recompute) {
-    c.count = a.all.cnt - a.cnt;
-    c.sum_has = a.all.h - a.h;
-    c.sum_wants = a.all.w - a.w;
-  } else {
-    c.count = rs.agg_count - a.cnt;
-    c.sum_has = rs.agg_has - a.h;
-    c.sum_wants = rs.agg_wants - a.w;
-  }
-  return c;
-}
-
-__device__ __forceinline__ void write_resource(const DevParams& p, int seg, const Res& rs, const Clean& c,
-                                               double delta) {
-  ResAgg r;
-  r.count = c.count;
-  r.sum_wants = c.sum_wants;
-  r.sum_has = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
-  r.safe = __builtin_isnan(rs.safe) ? rs.cap_cfg / (double)c.count : rs.safe;  // resource.go:91-95
-  p.res[seg] = r;
-}
-
-// FairShare per-row stage (algorithm.go:115-181).  Returns true when the lease is
-// decided here (gets in *g); otherwise fills T = deservedExtra + deservedShare.
-__device__ __forceinline__ bool fs_stage01(double w, double h, long long s, double C, double sum_has, double eq,
-                                           double E, long long Wc, double* g, double* T) {
-  const double ds = eq * (double)s;              // :126 deservedShare
-  const double avail = C - sum_has + h;          // :120 available
-  if (w <= ds) {                                 // :131
-    *g = minF(w, avail);
-    return true;
-  }
-  const long long Wi = Wc + s - (w > ds ? s : 0);  // :148,168 wantExtra (self counted once)
-  const double dE = (E / (double)Wi) * (double)s;  // :175 deservedExtra
-  if (w < ds + dE) {                               // :179
-    *g = minF(w, avail);
-    return true;
-  }
-  *T = dE + ds;
-  return false;
-}
-
-// Uniform-subclient FairShare: every per-row quantity of algorithm.go:123-204
-// that does not depend on the row's own wants/has is a per-resource constant
-// (deservedShare, deservedExtra, T, and the two possible deservedExtraExtra).
-struct FsU {
-  double ds, dE, T, dee_gt, dee_eq;
-};
-__device__ __forceinline__ FsU make_fsu(double eq, long long s0, double E, long long Wc, AggC c) {
-  FsU f;
-  f.ds = eq * (double)s0;                      // :126
-  f.dE = (E / (double)Wc) * (double)s0;        // :175 (wantExtra == W for every row that gets here)
-  f.T = f.dE + f.ds;                           // :197 deservedExtra + deservedShare
-  f.dee_gt = (c.ee / (double)(s0 + c.sgt - s0)) * (double)s0;  // :203, row above T (excluded, :193)
-  f.dee_eq = (c.ee / (double)(s0 + c.sgt)) * (double)s0;       // :203, row exactly at T
-  return f;
-}
-__device__ __forceinline__ double fs_uniform_row(double w, double h, double C, double sum_has, const FsU& f) {
-  const double avail = C - sum_has + h;  // :120
-  if (w <= f.ds) return minF(w, avail);  // :131
-  if (w < f.ds + f.dE) return minF(w, avail);  // :179
-  return minF(f.ds + f.dE + (w > f.T ? f.dee_gt : f.dee_eq), avail);  // :204
-}
-
-// FairShare round 2 result for a row given the resource's sums at its T (:189-204).
-__device__ __forceinline__ double fs_stage2(double w, double h, long long s, double C, double sum_has, double eq,
-                                            double E, long long Wc, double T, const AggC& c) {
-  const double ds = eq * (double)s;
-  const double avail = C - sum_has + h;
-  const long long Wi = Wc + s - (w > ds ? s : 0);
-  const double dE = (E / (double)Wi) * (double)s;
-  const long long wee = s + c.sgt - ((w > ds && w > T) ? s : 0);  // :189,200 (self excluded, :193)
-  const double dEE = (c.ee / (double)wee) * (double)s;             // :203
-  return minF(ds + dE + dEE, avail);                               // :204
-}
 
 // --------------------------------------------------------------------------
 // Resource-per-group kernel: G threads (a wave or a 256-thread workgroup) own
@@ -570,8 +232,6 @@ __global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __rest
 // and the live bit (sl = live ? s : ~s); Clean's loop runs only when a row of the
 // pack expired; the owners' sumHas loop moves gets - has as one double.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ int shfl_i(int v, int lane) { return __shfl(v, lane, 64); }
-__device__ __forceinline__ double shfl_d(double v, int lane) { return shfl_any(v, lane); }
 
 __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restrict__ packs, int npacks) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);

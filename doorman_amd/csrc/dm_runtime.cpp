@@ -41,6 +41,7 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
+hipError_t launch_decide(const DevParams& p, const ReqItem* items, int nitems, const ReqArgs& q, hipStream_t st);
 hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, hipStream_t st);
 hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st);
 }  // namespace dm
@@ -182,6 +183,10 @@ struct dm_ctx {
   hipEvent_t ev_bat[3] = {};
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
+  // dm_decide: a round's requests (sorted by row), per-resource work items, results
+  DBuf<int64_t> rq_rows, rq_sub, rq_exp;
+  DBuf<double> rq_has, rq_wants, rq_gets;
+  DBuf<ReqItem> rq_items;
   DBuf<uint32_t> hier_status;  // dm_hier_root_tick: per-server rejection flags of the last round
   int hier_servers = 0;
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
@@ -237,6 +242,8 @@ struct dm_ctx {
     if (h_bat_flags) (void)hipHostFree(h_bat_flags);
     h_bat_flags = nullptr;
     row_bits.release(); upd_flags.release(); hier_status.release();
+    rq_rows.release(); rq_sub.release(); rq_exp.release(); rq_has.release(); rq_wants.release(); rq_gets.release();
+    rq_items.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
   }
@@ -751,6 +758,67 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (!(flags & DM_ASYNC)) {
     DM_HIP(c, hipStreamSynchronize(st), "tick");
     c->collect_profile();
+  }
+  return DM_OK;
+}
+
+// A round of requests, each decided by Resource.Decide against the store as it is
+// (dm_round.hip).  Requests are sorted by row on the host so that each resource's
+// requests are one contiguous range; one workgroup per resource with requests.
+int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const double* has, const double* wants,
+              const int64_t* subclients, double* gets, int64_t* expiry_ns) {
+  DM_ENTER(c);
+  int rc = ready(c);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && (!rows || !has || !wants || !subclients || !gets || !expiry_ns)))
+    return c->fail(DM_E_INVAL, "bad requests");
+  if (n == 0) return DM_OK;
+  std::vector<int64_t> order((size_t)n);
+  for (int64_t i = 0; i < n; ++i) order[(size_t)i] = i;
+  std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return rows[a] < rows[b]; });
+  std::vector<int64_t> srows((size_t)n), ssub((size_t)n);
+  std::vector<double> shas((size_t)n), swants((size_t)n);
+  std::vector<ReqItem> items;
+  int64_t seg = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t k = order[(size_t)i], r = rows[k];
+    if (r < 0 || r >= c->N) return c->fail(DM_E_RANGE, "request row out of range");
+    if (i > 0 && r == srows[(size_t)i - 1]) return c->fail(DM_E_INVAL, "one request per row");
+    if (subclients[k] < 0 || subclients[k] > INT32_MAX) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
+    srows[(size_t)i] = r;
+    shas[(size_t)i] = has[k];
+    swants[(size_t)i] = wants[k];
+    ssub[(size_t)i] = subclients[k];
+    while (c->h_seg_off[seg + 1] <= r) ++seg;
+    if (items.empty() || items.back().seg != (int32_t)seg) items.push_back(ReqItem{(int32_t)seg, 0, i, i});
+    items.back().qhi = i + 1;
+  }
+  hipStream_t st = c->stream;
+  DM_HIP(c, upload(c->rq_rows, srows.data(), (size_t)n, st), "stage requests");
+  DM_HIP(c, upload(c->rq_has, shas.data(), (size_t)n, st), "stage requests");
+  DM_HIP(c, upload(c->rq_wants, swants.data(), (size_t)n, st), "stage requests");
+  DM_HIP(c, upload(c->rq_sub, ssub.data(), (size_t)n, st), "stage requests");
+  DM_HIP(c, upload(c->rq_items, items.data(), items.size(), st), "stage requests");
+  DM_HIP(c, c->rq_gets.ensure((size_t)n), "request results");
+  DM_HIP(c, c->rq_exp.ensure((size_t)n), "request results");
+  DevParams p{};
+  p.seg_off = c->seg_off.p;
+  p.wants = c->wants.p;
+  p.has = c->has.p;
+  p.sub = c->sub.p;
+  p.expiry = c->expiry.p;
+  p.cfg = c->cfg.p;
+  p.agg = c->agg.p;
+  p.now = now_ns;
+  p.recompute = 0;
+  const ReqArgs q{c->rq_rows.p, c->rq_has.p, c->rq_wants.p, c->rq_sub.p, c->rq_gets.p, c->rq_exp.p};
+  DM_HIP(c, launch_decide(p, c->rq_items.p, (int)items.size(), q, st), "decide requests");
+  DM_HIP(c, download(shas.data(), (const double*)c->rq_gets.p, 0, n, st), "read decisions");
+  DM_HIP(c, download(ssub.data(), (const int64_t*)c->rq_exp.p, 0, n, st), "read decisions");
+  DM_HIP(c, hipStreamSynchronize(st), "decide requests");
+  for (int64_t i = 0; i < n; ++i) {
+    gets[order[(size_t)i]] = shas[(size_t)i];
+    expiry_ns[order[(size_t)i]] = ssub[(size_t)i];
   }
   return DM_OK;
 }

@@ -8,13 +8,14 @@
 //
 //   1. Clean (store.go:169-181): leases whose expiry passed are released and
 //      their clients forgotten; ReleaseCapacity (server.go:668-714) likewise.
-//   2. Every requesting client's row becomes its request: wants, subclients,
-//      and has = the lease the server holds for it (old.Has, algorithm.go:103,
-//      120) or, in learning mode, the has the client reports (Learn,
-//      algorithm.go:297-302).  New clients take a free row (zero lease).
-//   3. One apportionment tick (dm_apportion, no writeback) decides every row
-//      against that snapshot; the requesting rows' leases are gathered and
-//      assigned (store.go:153-167: sums += new - old, expiry = now + length).
+//   2. New clients take a free row (no lease: store.HasClient is false for them).
+//   3. dm_decide runs Resource.Decide for every request of the round against
+//      the store as it was before the round -- the request's own has (Learn),
+//      wants and subclients for its client, the stored rows for everyone else
+//      (algorithm.go:115,148,157,223-225,263-269) -- and the leases are then
+//      assigned (dm_store_upsert, store.go:153-167: sums += new - old, expiry =
+//      now + length).  A round of one request is exactly the reference's
+//      GetCapacity; a round of many is each request's Decide on the same store.
 //
 // Clients that did not ask this round keep their leases (and count in the
 // sums) until they expire.  The host keeps the client -> row maps, the rows'
@@ -71,6 +72,7 @@ struct dm_server {
   std::vector<Req> pending;
   std::vector<std::pair<int64_t, std::string>> releases;
   std::vector<Out> results;
+  std::string broken;  // set when a re-layout failed half way: every later tick refuses
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -232,26 +234,31 @@ int dm_server_release_capacity(dm_server* s, const char* client, const char* res
 
 int dm_server_tick(dm_server* s, int64_t now) {
   if (!s) return DM_E_INVAL;
+  s->results.clear();  // tickets of a round that fails return an error, never stale leases
+  std::vector<Req> reqs;
+  reqs.swap(s->pending);
+  std::vector<std::pair<int64_t, std::string>> rels;
+  rels.swap(s->releases);
+  if (!s->broken.empty()) return s->fail(DM_E_STATE, "server unusable after a failed re-layout: " + s->broken);
   int rc;
   // 1. Clean (strict After: now > expiry) and ReleaseCapacity
+  std::vector<std::pair<int64_t, int64_t>> popped;
   std::vector<int64_t> drop;
   while (!s->heap.empty() && s->heap.top().first < now) {
     const auto e = s->heap.top();
     s->heap.pop();
+    popped.push_back(e);
     if (s->expiry[e.second] == e.first && !s->row_client[e.second].empty()) drop.push_back(e.second);
   }
-  for (auto& rel : s->releases) {
+  for (auto& rel : rels) {
     auto c = s->clients[rel.first].find(rel.second);
     if (c != s->clients[rel.first].end()) drop.push_back(c->second);
   }
-  s->releases.clear();
-  if ((rc = release_rows(s, drop))) {
-    s->pending.clear();
+  if ((rc = release_rows(s, drop))) {  // the store is untouched: put Clean's heap entries back
+    for (const auto& e : popped) s->heap.push(e);
     return rc;
   }
   // rows for the requests: grow resources that lack free rows first
-  std::vector<Req> reqs;
-  reqs.swap(s->pending);
   {
     std::vector<int64_t> need(s->R, 0);
     std::unordered_map<std::string, int> seen;
@@ -269,80 +276,94 @@ int dm_server_tick(dm_server* s, int64_t now) {
         while (sizes[r] < used + need[r]) sizes[r] = std::max<int64_t>(2 * sizes[r], 1);
       }
     }
-    if (grow && (rc = relayout(s, sizes))) return rc;
+    if (grow && (rc = relayout(s, sizes))) {
+      s->broken = s->err;  // host mirror and device table may disagree now
+      return rc;
+    }
   }
-  // 2. every requesting client's row holds its request (the last one wins)
+  // 2. one request per row (the last one wins); a new client takes a free row,
+  //    which holds no lease (store.HasClient false for the decision)
   std::vector<int64_t> ticket_row(reqs.size());
-  std::unordered_map<int64_t, size_t> row_req;  // row -> index into the upsert batch
-  std::vector<int64_t> rows;
+  std::unordered_map<int64_t, size_t> row_req;  // row -> index into the round's requests
+  std::vector<int64_t> rows, u_sub;
   std::vector<double> u_has, u_wants;
-  std::vector<int64_t> u_sub, u_exp;
+  struct Fresh {
+    int64_t res, row;
+    std::string client;
+  };
+  std::vector<Fresh> fresh;
   for (size_t k = 0; k < reqs.size(); ++k) {
     const Req& q = reqs[k];
     auto& cl = s->clients[q.res];
     auto c = cl.find(q.client);
     int64_t row;
-    if (c == cl.end()) {  // a new client: zero lease in a free row, live for this tick
+    if (c == cl.end()) {
       row = s->free_rows[q.res].back();
       s->free_rows[q.res].pop_back();
       cl.emplace(q.client, row);
       s->row_client[row] = q.client;
-      s->has[row] = 0.0;
-      s->expiry[row] = now;
+      fresh.push_back(Fresh{q.res, row, q.client});
     } else {
       row = c->second;
     }
     ticket_row[k] = row;
-    const bool learning = s->learning_end[q.res] > now;  // resource.go:108
-    const double h = learning ? q.has : s->has[row];
     auto ins = row_req.emplace(row, rows.size());
     if (ins.second) {
       rows.push_back(row);
-      u_has.push_back(h);
+      u_has.push_back(q.has);
       u_wants.push_back(q.wants);
       u_sub.push_back(q.sub);
-      u_exp.push_back(s->expiry[row]);
     } else {
       const size_t j = ins.first->second;
-      u_has[j] = h;
+      u_has[j] = q.has;
       u_wants[j] = q.wants;
       u_sub[j] = q.sub;
     }
   }
-  s->results.assign(reqs.size(), Out{});
+  auto rollback = [&](int code) {  // new clients never got a lease: forget them
+    for (const Fresh& f : fresh) {
+      s->clients[f.res].erase(f.client);
+      s->row_client[f.row].clear();
+      s->free_rows[f.res].push_back(f.row);
+    }
+    return s->ctx_fail(code);
+  };
   if (rows.empty()) return DM_OK;
   const int64_t n = (int64_t)rows.size();
-  if ((rc = dm_store_upsert(s->ctx, n, rows.data(), u_has.data(), u_wants.data(), u_sub.data(), u_exp.data())))
-    return s->ctx_fail(rc);
-  // 3. one tick over the snapshot, then Assign the requesting rows' leases
-  if ((rc = dm_apportion(s->ctx, now, 0u))) return s->ctx_fail(rc);
+  // 3. decide every request against the store as it was before the round
+  //    (Resource.Decide per request), then Assign the leases (store.go:153-167)
   std::vector<double> gets(n);
   std::vector<int64_t> exp(n);
-  if ((rc = dm_read_leases_rows(s->ctx, n, rows.data(), gets.data(), exp.data()))) return s->ctx_fail(rc);
-  // SetSafeCapacity (resource.go:81-96) of the tick, for the resources asked
-  int64_t rlo = s->R, rhi = -1;
-  for (const Req& q : reqs) {
-    rlo = std::min(rlo, q.res);
-    rhi = std::max(rhi, q.res);
-  }
-  std::vector<double> safe((size_t)(rhi - rlo + 1));
-  if ((rc = dm_read_resources(s->ctx, rlo, rhi - rlo + 1, nullptr, nullptr, nullptr, safe.data())))
-    return s->ctx_fail(rc);
+  if ((rc = dm_decide(s->ctx, now, n, rows.data(), u_has.data(), u_wants.data(), u_sub.data(), gets.data(),
+                      exp.data())))
+    return rollback(rc);
   if ((rc = dm_store_upsert(s->ctx, n, rows.data(), gets.data(), u_wants.data(), u_sub.data(), exp.data())))
-    return s->ctx_fail(rc);
+    return rollback(rc);
   for (int64_t j = 0; j < n; ++j) {
     s->has[rows[j]] = gets[j];
     s->expiry[rows[j]] = exp[j];
     s->heap.push({exp[j], rows[j]});
   }
+  // SetSafeCapacity (resource.go:81-96) after the round's Assigns
+  int64_t rlo = s->R, rhi = -1;
+  for (const Req& q : reqs) {
+    rlo = std::min(rlo, q.res);
+    rhi = std::max(rhi, q.res);
+  }
+  std::vector<int64_t> count((size_t)(rhi - rlo + 1));
+  if ((rc = dm_read_resources(s->ctx, rlo, rhi - rlo + 1, count.data(), nullptr, nullptr, nullptr)))
+    return s->ctx_fail(rc);
+  s->results.assign(reqs.size(), Out{});
   for (size_t k = 0; k < reqs.size(); ++k) {
     const size_t j = row_req[ticket_row[k]];
+    const int64_t r = reqs[k].res;
     Out& o = s->results[k];
     o.capacity = gets[j];
     // Lease.Expiry.Unix() (server.go:789): seconds, rounded toward -inf
     o.expiry_s = exp[j] >= 0 ? exp[j] / 1000000000LL : -((-exp[j] + 999999999LL) / 1000000000LL);
-    o.refresh_s = s->refresh_s[reqs[k].res];  // int64(RefreshInterval.Seconds())
-    o.safe = safe[(size_t)(reqs[k].res - rlo)];
+    o.refresh_s = s->refresh_s[r];  // int64(RefreshInterval.Seconds())
+    const double safe = s->safe_capacity[r];
+    o.safe = std::isnan(safe) ? s->capacity[r] / (double)count[(size_t)(r - rlo)] : safe;
   }
   return DM_OK;
 }
@@ -350,7 +371,8 @@ int dm_server_tick(dm_server* s, int64_t now) {
 int dm_server_lease(dm_server* s, int64_t ticket, double* capacity, int64_t* expiry_time_s, int64_t* refresh_s,
                     double* safe_capacity) {
   if (!s) return DM_E_INVAL;
-  if (ticket < 0 || ticket >= (int64_t)s->results.size()) return s->fail(DM_E_RANGE, "no such ticket");
+  if (ticket < 0 || ticket >= (int64_t)s->results.size())
+    return s->fail(DM_E_RANGE, "no such ticket (the last round failed, or had fewer requests)");
   const Out& o = s->results[(size_t)ticket];
   if (capacity) *capacity = o.capacity;
   if (expiry_time_s) *expiry_time_s = o.expiry_s;

@@ -202,6 +202,17 @@ class Engine:
                  | {"auto": 0, "inplace": _lib.DM_WB_INPLACE, "alternate": _lib.DM_WB_ALTERNATE}[wb_columns])
         self._chk(self._L.dm_apportion(self._ctx, int(now_ns), flags))
 
+    def decide(self, now_ns: int, rows, has, wants, subclients):
+        """dm_decide: Resource.Decide for each request of a round against the store as it
+        is (rows[k] = the client's row, or a free row of its resource for a new client);
+        returns (gets, expiry_ns).  The store is not changed."""
+        rows = _c(rows, np.int64)
+        a = [_c(has, np.float64), _c(wants, np.float64), _c(subclients, np.int64)]
+        gets, exp = np.empty(len(rows)), np.empty(len(rows), np.int64)
+        self._chk(self._L.dm_decide(self._ctx, int(now_ns), len(rows), _ptr(rows), *[_ptr(x) for x in a], _ptr(gets),
+                                    _ptr(exp)))
+        return gets, exp
+
     def leases(self, off: int = 0, n: int | None = None):
         n = self.n_leases - off if n is None else n
         gets, exp = np.empty(n), np.empty(n, np.int64)

@@ -3,7 +3,8 @@
 
 Mirrors the reference server's request path (go/server/doorman/server.go:668-817,
 resource.go:100-113): a round's ResourceRequests are queued, then decided together
-by one apportionment tick; each ticket gets the lease GetCapacity would put in its
+round by round (dm_decide: each request against the store as it was before the
+round, then the Assigns); each ticket gets the lease GetCapacity would put in its
 response (capacity, expiry_time in unix seconds, refresh_interval, safe_capacity).
 """
 from __future__ import annotations

@@ -193,6 +193,19 @@ int dm_read_config(dm_ctx* ctx, int64_t r0, int64_t n, int32_t* kind, double* ca
 /* ---- the batch algorithm: every client of every resource, one frozen snapshot ---- */
 int dm_apportion(dm_ctx* ctx, int64_t now_ns, uint32_t flags);
 
+/* A round of individual requests (Resource.Decide, resource.go:100-113, for each):
+ * request k is for the client whose lease lives in row rows[k] -- its existing row,
+ * or a free (released) row of the resource it asks for, which makes it a new client
+ * (store.HasClient false, algorithm.go:223-225).  Every request is decided against
+ * the store as it is (after a Clean at now_ns, which is not written back), with the
+ * request's own has (Learn), wants and subclients for its client and the stored
+ * rows for everyone else (algorithm.go:115,126,148,157,263-269).  gets[k] and
+ * expiry_ns[k] (now + lease length) are the leases; the store is not changed --
+ * Assign them with dm_store_upsert.  Rows unique; subclients in [0, 2^31).
+ * Synchronous. */
+int dm_decide(dm_ctx* ctx, int64_t now_ns, int64_t n, const int64_t* rows, const double* has, const double* wants,
+              const int64_t* subclients, double* gets, int64_t* expiry_ns);
+
 /* lease outputs of the last dm_apportion: gets (Lease.Has), expiry in unix ns
  * (DM_RELEASED for released rows); any pointer may be NULL */
 int dm_read_leases(dm_ctx* ctx, int64_t off, int64_t n, double* gets, int64_t* expiry_ns);
@@ -279,12 +292,14 @@ int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
  *
  * Requests queued during a round are decided together by dm_server_tick: the
  * store first drops expired leases (Clean, store.go:169-181) and released
- * clients (store.go:142-151), then holds every requesting client's row as its
- * request (wants, subclients; has = the lease the server assigned, or the
- * client-reported has in learning mode, algorithm.go:297-302), the tick decides
- * the requesting clients against that one snapshot, and their leases are
- * assigned (store.go:153-167).  Clients that did not ask keep their leases, which
- * expire unless refreshed.  Resources are configured up front (the outcome of
+ * clients (store.go:142-151); then every request is decided by Resource.Decide
+ * against the store as it was before the round (dm_decide: the request's own has,
+ * wants and subclients for its client, new clients absent from the store), and
+ * the round's leases are assigned (store.go:153-167).  A round of one request is
+ * the reference's GetCapacity exactly.  Clients that did not ask keep their
+ * leases, which expire unless refreshed.  A round that fails leaves no leases
+ * (dm_server_lease then reports an error for its tickets) and forgets the new
+ * clients it had placed.  Resources are configured up front (the outcome of
  * the reference's LoadConfig; config parsing and glob matching stay there);
  * every resource's segment of the table grows when it runs out of free rows. */
 typedef struct dm_server dm_server;

@@ -116,6 +116,8 @@ def lib():
         L.or_store_get.argtypes = [vp, i64, ctypes.POINTER(_Lease)]
         L.or_store_release.argtypes = [vp, i64]
         L.or_store_assign.argtypes = [vp, i64, i64, i64, f64, f64, i64, i64, ctypes.POINTER(_Lease)]
+        L.or_store_put.argtypes = [vp, i64, ctypes.POINTER(_Lease)]
+        L.or_store_set_sums.argtypes = [vp, i64, f64, f64]
         L.or_store_clean.restype = i64
         L.or_store_clean.argtypes = [vp, i64]
         L.or_algorithm.restype = ctypes.c_int
@@ -194,6 +196,14 @@ class Store:
 
     def clean(self, now_ns: int) -> int:
         return lib().or_store_clean(self._p, now_ns)
+
+    def put(self, c, expiry_ns, has, wants, sub, refresh_ns=0) -> None:
+        """A stored lease with an explicit expiry (running sums updated as Assign does)."""
+        lib().or_store_put(self._p, c, ctypes.byref(_Lease(expiry_ns, refresh_ns, has, wants, sub)))
+
+    def set_sums(self, count, sum_has, sum_wants) -> None:
+        """Override the running sums (a snapshot's parity-mode aggregates)."""
+        lib().or_store_set_sums(self._p, count, sum_has, sum_wants)
 
 
 def algorithm(kind, store: Store, capacity, client, has, wants, sub, now_ns=0, lease_length_s=0, refresh_s=0) -> Lease:

@@ -14,6 +14,7 @@ import pytest
 
 from doorman_amd import workloads as W
 from oracle import oracle as O
+from parity_util import float_close
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -90,45 +91,50 @@ def test_wrong_number_of_clients_is_invalid_argument():
 
 
 class ServerModel:
-    """The reference server's per-resource stores, decided per round on one
-    snapshot by the CPU oracle (test infrastructure)."""
+    """The reference server (test infrastructure): one LeaseStore per resource (the
+    oracle's restatement of store.go).  A round: Clean, the ReleaseCapacity calls,
+    then every request's Resource.Decide (resource.go:100-113) on a private copy of
+    the store as it was before the round, then their Assigns (store.go:153-167).
+    With one request per round this is exactly the reference's GetCapacity."""
 
     def __init__(self, resources):
         self.ids = list(resources)
         self.cfg = resources
-        self.leases = {r: {} for r in self.ids}  # client -> [has, wants, sub, expiry]
+        self.cid = {}
+        self.stores = {r: O.Store(256) for r in self.ids}
+        self.tab = {r: O.make_cfg(1, kind=c["kind"], capacity=c["capacity"], lease_length_s=c.get("lease_length_s", 300),
+                                  refresh_interval_s=c.get("refresh_interval_s", 5),
+                                  learning_end_ns=c.get("learning_end_ns", I64_MIN),
+                                  parent_expiry_ns=c.get("parent_expiry_ns", I64_MAX),
+                                  safe_capacity=c.get("safe_capacity", np.nan))[0] for r, c in resources.items()}
+
+    def _id(self, c):
+        return self.cid.setdefault(c, len(self.cid))
+
+    def clients(self, r):
+        return sum(self.stores[r].has_client(i) for i in self.cid.values())
 
     def round(self, now, requests, releases):
-        for r in self.ids:  # Clean (store.go:169-181)
-            for c in [c for c, l in self.leases[r].items() if now > l[3]]:
-                del self.leases[r][c]
-        for c, r in releases:  # ReleaseCapacity (store.go:142-151)
-            self.leases[r].pop(c, None)
-        for c, r, has, wants, sub in requests:
-            learning = self.cfg[r].get("learning_end_ns", I64_MIN) > now
-            lease = self.leases[r].setdefault(c, [0.0, 0.0, 0, now])
-            lease[0] = has if learning else lease[0]
-            lease[1], lease[2] = wants, sub
-        sizes, rows = [], []
         for r in self.ids:
-            sizes.append(len(self.leases[r]))
-            rows += [(r, c, *l) for c, l in self.leases[r].items()]
-        col = lambda k, dt: np.array([x[k] for x in rows], dt)  # noqa: E731
-        cfg = lambda f, d: [self.cfg[r].get(f, d) for r in self.ids]  # noqa: E731
-        snap = W.make_snapshot(sizes, col(3, np.float64), col(2, np.float64), col(4, np.int64), col(5, np.int64),
-                               cfg("kind", 0), cfg("capacity", 0.0), cfg("lease_length_s", 300),
-                               cfg("refresh_interval_s", 5), cfg("learning_end_ns", I64_MIN),
-                               cfg("parent_expiry_ns", I64_MAX), cfg("safe_capacity", np.nan))
-        ref = O.apportion(snap, now)
-        where = {(x[0], x[1]): i for i, x in enumerate(rows)}
+            self.stores[r].clean(now)  # store.go:169-181
+        for c, r in releases:  # server.go:705-711
+            if c in self.cid:
+                self.stores[r].release(self.cid[c])
+        last = {}
+        for c, r, has, wants, sub in requests:  # one decision per client and resource
+            last[(c, r)] = (has, wants, sub)
+        decided = [((c, r), O.decide(self.stores[r].clone(), self.tab[r], self._id(c), has, wants, sub, now), wants, sub)
+                   for (c, r), (has, wants, sub) in last.items()]
+        for (c, r), lease, wants, sub in decided:
+            t = self.tab[r]
+            self.stores[r].assign(self.cid[c], int(t["lease_length_s"]), int(t["refresh_interval_s"]), lease.has,
+                                  wants, sub, now)
         out = {}
-        for c, r, *_ in requests:
-            i = where[(r, c)]
-            lease = self.leases[r][c]
-            lease[0], lease[3] = ref["gets"][i], ref["expiry_ns"][i]
-            k = self.ids.index(r)
-            out[(c, r)] = (ref["gets"][i], ref["expiry_ns"][i], self.cfg[r].get("refresh_interval_s", 5),
-                           ref["res_safe_capacity"][k], self.cfg[r]["capacity"])
+        for (c, r), lease, _, _ in decided:
+            t = self.tab[r]
+            safe = t["safe_capacity"]
+            safe = t["capacity"] / float(self.stores[r].count()) if np.isnan(safe) else safe  # resource.go:91-95
+            out[(c, r)] = (lease.has, lease.expiry_ns, int(t["refresh_interval_s"]), safe, float(t["capacity"]))
         return out
 
 
@@ -148,7 +154,8 @@ def test_rounds_match_the_reference_server_model(seed):
     """Clients join, refresh, change wants, release and stop refreshing (their
     leases expire and Clean drops them) on FairShare / ProportionalShare / Static /
     NoAlgorithm / learning resources; resources outgrow their rows.  Every round's
-    leases equal the model's, decided by the oracle on the same snapshot."""
+    leases equal the reference server model's (each request's Decide on the store
+    as it was before the round)."""
     rng = np.random.default_rng(500 + seed)
     kinds = [W.FAIR_SHARE, W.PROPORTIONAL_SHARE, W.FAIR_SHARE, W.STATIC, W.NO_ALGORITHM, W.PROPORTIONAL_SHARE]
     resources = {f"r{k}": {"kind": kd, "capacity": float(rng.choice([10.0, 100.0, 1234.5])),
@@ -180,24 +187,31 @@ def test_rounds_match_the_reference_server_model(seed):
         _check(srv, tickets, model.round(now, reqs, rels), f"seed={seed} round={rnd}")
         for r in resources:
             st = srv.resource(r)
-            assert st["clients"] == len(model.leases[r])
-            assert st["count"] == sum(l[2] for l in model.leases[r].values())
+            assert st["clients"] == model.clients(r)
+            assert st["count"] == model.stores[r].count()
     srv.close()
 
 
 def test_expired_leases_are_cleaned_and_capacity_returns():
     """A client that stops refreshing loses its lease after lease_length
-    (store.go:169-181): the remaining client then gets the whole capacity."""
-    srv = _server({"res": {"kind": W.FAIR_SHARE, "capacity": 100.0, "lease_length_s": 10, "refresh_interval_s": 5}})
+    (store.go:169-181): the remaining client then gets the whole capacity.
+    Round 1: both new clients see the empty store (80 each); round 2: a shares with
+    b's stored lease (FairShare 50, capped by the unused capacity 20); round 3: b
+    has expired and a gets its 80."""
+    res = {"res": {"kind": W.FAIR_SHARE, "capacity": 100.0, "lease_length_s": 10, "refresh_interval_s": 5}}
+    srv = _server(res)
+    model = ServerModel(res)
     a = srv.get_capacity("a", "res", 0.0, 80.0)
     b = srv.get_capacity("b", "res", 0.0, 80.0)
     srv.tick(NOW)
-    assert srv.lease(a).capacity == 50.0 and srv.lease(b).capacity == 50.0
-    a = srv.get_capacity("a", "res", 50.0, 80.0)  # b does not refresh
+    model.round(NOW, [("a", "res", 0.0, 80.0, 1), ("b", "res", 0.0, 80.0, 1)], [])
+    assert srv.lease(a).capacity == 80.0 and srv.lease(b).capacity == 80.0
+    a = srv.get_capacity("a", "res", 80.0, 80.0)  # b does not refresh
     srv.tick(NOW + 5 * W.NS)
-    assert srv.lease(a).capacity == 50.0  # b still holds 50
+    assert model.round(NOW + 5 * W.NS, [("a", "res", 80.0, 80.0, 1)], [])[("a", "res")][0] == 20.0
+    assert srv.lease(a).capacity == 20.0  # b still holds 80
     assert srv.resource("res")["clients"] == 2
-    a = srv.get_capacity("a", "res", 50.0, 80.0)
+    a = srv.get_capacity("a", "res", 20.0, 80.0)
     srv.tick(NOW + 11 * W.NS)  # b's lease (NOW + 10 s) has expired
     assert srv.resource("res")["clients"] == 1
     assert srv.lease(a).capacity == 80.0
@@ -205,14 +219,127 @@ def test_expired_leases_are_cleaned_and_capacity_returns():
 
 
 def test_release_capacity_frees_the_share():
-    srv = _server({"res": {"kind": W.PROPORTIONAL_SHARE, "capacity": 90.0}})
+    """ProportionalShare, capacity 90.  Round 1: three new clients each see the empty
+    store (60 each, what they want).  Round 2: c releases; a and b share 90 but the
+    unused capacity caps them (90 - 120 + 60 = 30 each).  Round 3: the equal share,
+    45 each, and the store's SumHas is the whole capacity."""
+    res = {"res": {"kind": W.PROPORTIONAL_SHARE, "capacity": 90.0}}
+    srv = _server(res)
+    model = ServerModel(res)
     t = [srv.get_capacity(c, "res", 0.0, 60.0) for c in "abc"]
     srv.tick(NOW)
-    assert [srv.lease(x).capacity for x in t] == [30.0, 30.0, 30.0]
+    model.round(NOW, [(c, "res", 0.0, 60.0, 1) for c in "abc"], [])
+    assert [srv.lease(x).capacity for x in t] == [60.0, 60.0, 60.0]
     srv.release_capacity("c", "res")
-    t = [srv.get_capacity(c, "res", 30.0, 60.0) for c in "ab"]
-    srv.tick(NOW + W.NS)
-    assert [srv.lease(x).capacity for x in t] == [45.0, 45.0]
+    for k, (now, has, want) in enumerate([(NOW + W.NS, 60.0, 30.0), (NOW + 2 * W.NS, 30.0, 45.0)]):
+        reqs = [(c, "res", has, 60.0, 1) for c in "ab"]
+        t = [srv.get_capacity(c, "res", has, 60.0) for c in "ab"]
+        srv.tick(now)
+        exp = model.round(now, reqs, [("c", "res")] if k == 0 else [])
+        assert [exp[(c, "res")][0] for c in "ab"] == [want, want]
+        assert [srv.lease(x).capacity for x in t] == [want, want]
     st = srv.resource("res")
     assert st["clients"] == 2 and st["count"] == 2 and st["sum_has"] == 90.0
     srv.close()
+
+
+def test_one_request_sees_the_store_before_its_own_assign():
+    """the reference decides a request on the store as it is -- the
+    client's own old row included, not its new wants (algorithm.go:217,245).
+    Capacity 100; A holds 10 (wants 10), B holds 30 (wants 60); A asks for 60:
+    SumWants is 70 <= 100, so A gets min(60, 100 - 40 + 10) = 60, not the 50 a
+    store already holding A's new wants would give."""
+    res = {"res": {"kind": W.PROPORTIONAL_SHARE, "capacity": 100.0, "lease_length_s": 60,
+                   "learning_end_ns": NOW + W.NS}}
+    srv = _server(res)
+    model = ServerModel(res)
+    reqs = [("a", "res", 10.0, 10.0, 1), ("b", "res", 30.0, 60.0, 1)]  # learning: Learn grants the reported has
+    t = {(c, r): srv.get_capacity(c, r, h, w) for c, r, h, w, _ in reqs}
+    srv.tick(NOW)
+    _check(srv, t, model.round(NOW, reqs, []), "learning round")
+    assert srv.lease(t[("a", "res")]).capacity == 10.0 and srv.lease(t[("b", "res")]).capacity == 30.0
+    t = {("a", "res"): srv.get_capacity("a", "res", 10.0, 60.0)}
+    srv.tick(NOW + 2 * W.NS)
+    expect = model.round(NOW + 2 * W.NS, [("a", "res", 10.0, 60.0, 1)], [])
+    assert expect[("a", "res")][0] == 60.0
+    assert srv.lease(t[("a", "res")]).capacity == 60.0
+    srv.close()
+
+
+def test_release_capacity_kat():
+    """server_test.go:404-433: after ReleaseCapacity the resource's SumHas is 0; an
+    unknown resource in the same call is ignored."""
+    case = next(c for c in KATS["server"] if c["name"] == "TestReleaseCapacity")
+    rel = case["release"]
+    cfg = _res_cfg(case, NOW - W.NS // 2)
+    cfg["safe_capacity"] = case["safe_capacity"]
+    srv = _server({"resource": cfg})
+    t = srv.get_capacity("client", "resource", rel["request"]["has"], rel["request"]["wants"])
+    srv.tick(NOW)
+    assert srv.lease(t).capacity == rel["request"]["has"]  # learning mode (lease length 2 s)
+    assert srv.lease(t).safe_capacity == case["safe_capacity"]
+    for r in rel["release_resources"]:
+        srv.release_capacity("client", r)
+    srv.tick(NOW + W.NS)
+    st = srv.resource("resource")
+    assert st["sum_has"] == rel["post_sum_has"] and st["clients"] == 0
+    srv.close()
+
+
+def test_tickets_of_an_earlier_round_are_not_served():
+    """dm_server_lease answers only the last round's tickets."""
+    from doorman_amd.server import ServerError
+    srv = _server({"res": {"kind": W.FAIR_SHARE, "capacity": 10.0}})
+    t = srv.get_capacity("a", "res", 0.0, 4.0)
+    srv.tick(NOW)
+    assert srv.lease(t).capacity == 4.0
+    srv.tick(NOW + W.NS)  # a round without requests
+    with pytest.raises(ServerError):
+        srv.lease(t)
+    srv.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_decide_matches_or_decide_on_the_store_before_the_round(seed):
+    """dm_decide against the oracle's literal Resource.Decide, one private store copy
+    per request: existing clients with changed wants / subclients, new clients on
+    free rows, clients whose lease expired (Clean drops them first), learning mode,
+    heterogeneous subclients, every kind; parity-mode running sums."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(900 + seed)
+    snap = W.random_snapshot(rng, 30, 60, hetero=seed % 2 == 1, edge=seed == 3)
+    N = len(snap["wants"])
+    free = rng.random(N) < 0.15  # released rows: slots for new clients
+    for k, v in (("wants", 0.0), ("has", 0.0), ("subclients", 0), ("expiry_ns", W.RELEASED)):
+        snap[k][free] = v
+    W.add_store_sums(snap)
+    so = snap["seg_off"]
+    rows = np.flatnonzero(rng.random(N) < 0.4)
+    n = len(rows)
+    cap_row = np.repeat(snap["capacity"], np.diff(so))
+    wants = np.where(rng.random(n) < 0.5, snap["wants"][rows], rng.uniform(0, 2, n) * cap_row[rows] / 10)
+    sub = np.where(rng.random(n) < 0.8, np.maximum(snap["subclients"][rows], 1), rng.integers(1, 5, n))
+    has = rng.uniform(0, 1, n) * cap_row[rows] / 10
+    with Engine(0) as e:
+        e.load(snap)
+        gets, exp = e.decide(NOW, rows, has, wants, sub)
+        after = e.read_store()
+    for k in ("has", "wants", "subclients", "expiry_ns"):  # the store is not changed
+        np.testing.assert_array_equal(after[k], snap[k])
+    cfg = O.make_cfg(len(so) - 1)
+    for f in O.CFG_DTYPE.names:
+        cfg[f] = snap[f]
+    ref_g, ref_e = np.empty(n), np.empty(n, np.int64)
+    for k, row in enumerate(rows):
+        r = int(np.searchsorted(so, row, side="right")) - 1
+        st = O.Store(int(so[r + 1] - so[r]))
+        for j in range(so[r], so[r + 1]):
+            if snap["expiry_ns"][j] != W.RELEASED:
+                st.put(int(j - so[r]), int(snap["expiry_ns"][j]), snap["has"][j], snap["wants"][j],
+                       int(snap["subclients"][j]))
+        st.set_sums(int(snap["agg_count"][r]), snap["agg_sum_has"][r], snap["agg_sum_wants"][r])
+        lease = O.decide(st, cfg[r], int(row - so[r]), has[k], wants[k], int(sub[k]), NOW)
+        ref_g[k], ref_e[k] = lease.has, lease.expiry_ns
+    np.testing.assert_array_equal(exp, ref_e)
+    ok = float_close(gets, ref_g, cap_row[rows])
+    assert ok.all(), (np.flatnonzero(~ok)[:8], gets[~ok][:4], ref_g[~ok][:4])
