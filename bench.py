@@ -97,7 +97,7 @@ def kernel_units(snap):
         m = (sizes >= lo) & (sizes <= hi)
         units[name] = (int(sizes[m].sum()), int(m.sum()))
     big = sizes > 4096
-    for name in ("large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
+    for name in ("large_fused", "large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
         units[name] = (int(sizes[big].sum()), int(big.sum()))
     return units
 

@@ -106,6 +106,7 @@ _SIGS = {
     "dm_read_config": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 7),
     "dm_hier_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "dm_set_large_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_plan_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),

@@ -76,12 +76,36 @@ struct Partials {
   // pass A: live-row mask, one byte per thread of each chunk (bit k = row k*256+tid),
   // so passes B and C read wants (+ subclients for ProportionalShare) and not expiry
   uint8_t* live;
-  // per large resource (kSegTotBytes each): pass A totals left by pass B's first
-  // chunk, pass B totals left by pass C's first chunk, so the map reduces at most
-  // one set of partials
+  // per large resource (kSegTotBytes each): the totals each launch's last arriving
+  // chunk leaves for the next launch (dm_kernels.hip, SegTot)
   uint8_t* tot;
+  // per large resource: arrival counters of launches A, B, C and the map (zero
+  // between launches: each is reset by its last arriver)
+  uint32_t* arrive;
 };
 constexpr int kSegTotBytes = 128;
+
+// One-launch large path (k_large_fused, dm_large.hip): every chunk keeps its rows
+// in VGPRs while the resource's chunks exchange per-resource totals in-launch.
+// Chunk records and totals records are kFusedWords u64 words:
+//   0 cnt  1 has  2 wants  3 all.cnt  4 all.has  5 all.wants  6 smin|smax<<32  7 nan
+//   8 b.x  9 b.y  10 b.i   11 c.ee  12 c.sgt  13 delta
+constexpr int kFusedRows = 8;    // rows per thread: a chunk is G * kFusedRows rows
+constexpr int kFusedWords = 16;
+// per large resource, in u32 words: arrive[4] counters on one 128-B line, then per
+// phase kFusedFlagCopies replicas of its flag, each on its own 128-B line (hundreds
+// of polling chunks spread over the replicas instead of hammering one line)
+constexpr int kFusedFlagCopies = 8;
+constexpr int kFusedSync = 32 + 4 * kFusedFlagCopies * 32;
+struct FusedState {
+  uint32_t* ticket;  // chunk dispenser: chunks start in resource order (co-residency argument)
+  uint32_t* sync;    // [nls * kFusedSync], zero at plan build; counters reset by their last arriver
+  uint64_t* part;    // [nchunks * kFusedWords]
+  uint64_t* tot;     // [nls * kFusedWords]
+  uint32_t* err;     // host-mapped word: a bounded wait gave up (residency bound violated)
+  int32_t nchunks;
+  uint32_t epoch;    // launch number, never 0: the value a phase's flag takes when its totals are out
+};
 
 // row -> resource lookup for store updates: seg_off plus, for every block of
 // 2^kRowBlkShift rows, the resource holding its first row

@@ -346,6 +346,67 @@ __device__ __forceinline__ double fs_stage2(double w, double h, long long s, dou
   return minF(ds + dE + dEE, avail);                               // :204
 }
 
+// --------------------------------------------------------------------------
+// In-launch hand-off between workgroups (MI355X_MICROARCH.md, "Valid forms",
+// first table row): the payload is stored write-through (8- or 4-B agent-scope
+// atomic stores, sc1: no release fence, so no L2 write-back of the workgroup's
+// other dirty lines), the storing wave drains (s_waitcnt vmcnt(0)) before its
+// arrive, and every load of handed-off bytes is an agent-scope atomic load (sc1,
+// L1 bypassed) issued after the arrive returned / the flag matched.
+// --------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+__device__ __forceinline__ void st_wt(uint64_t* a, uint64_t v) {
+  __hip_atomic_store((gu64*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(double* a, double v) { st_wt((uint64_t*)a, __builtin_bit_cast(uint64_t, v)); }
+__device__ __forceinline__ void st_wt(int64_t* a, int64_t v) { st_wt((uint64_t*)a, (uint64_t)v); }
+__device__ __forceinline__ void st_wt(int32_t* a, int32_t v) {
+  __hip_atomic_store((gu32*)a, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_wt(const uint64_t* a) {
+  return __hip_atomic_load((gu64*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* a) { return __builtin_bit_cast(double, ld_wt((const uint64_t*)a)); }
+__device__ __forceinline__ int64_t ld_wt(const int64_t* a) { return (int64_t)ld_wt((const uint64_t*)a); }
+__device__ __forceinline__ int32_t ld_wt(const int32_t* a) {
+  return (int32_t)__hip_atomic_load((gu32*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by wave 0 only, after lane 0 stored the workgroup's partial write-through:
+// lane 0 drains its stores and arrives at counter `ctr` (one of `nch` arrivals);
+// returns, uniformly over the wave, whether this workgroup arrived last.  The last
+// arriver resets the counter for the next launch.  The other waves of the
+// workgroup need not wait: they may have exited already.
+__device__ __forceinline__ bool arrive_last(uint32_t* ctr, int nch) {
+  uint32_t last = 0;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial's stores have landed
+    const uint32_t old = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (uint32_t)nch - 1 ? 1u : 0u;
+    if (last) __hip_atomic_store((gu32*)ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return __builtin_amdgcn_readfirstlane(last) != 0;
+}
+
+// A large resource's state once its pass-A totals are known (all chunks agree).
+struct SegState {
+  AggA a;
+  Clean cl;
+  Res rs;
+  int general;  // FairShare with heterogeneous subclients / NaN wants -> k_general
+};
+
+__device__ __forceinline__ SegState seg_state_of(const DevParams& p, int seg, const AggA& a) {
+  SegState st;
+  st.a = a;
+  st.rs = load_res(p, seg);
+  st.cl = clean_from(p, st.rs, a);
+  st.general = (!st.rs.learning && st.rs.kind == 3 && !(a.smin >= a.smax && !a.nan)) ? 1 : 0;
+  return st;
+}
+
 __device__ __forceinline__ int shfl_i(int v, int lane) { return __shfl(v, lane, 64); }
 __device__ __forceinline__ double shfl_d(double v, int lane) { return shfl_any(v, lane); }
 

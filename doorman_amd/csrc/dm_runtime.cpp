@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -19,10 +20,13 @@ namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       bool hbm_stream, hipStream_t st);
-hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
+hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
                           hipStream_t st);
+hipError_t launch_large_fused(int G, const DevParams& p, const Chunk* chunks, const LargeSeg* ls, const FusedState& F,
+                              int32_t* glist, int32_t* gcount, hipStream_t st);
+hipError_t large_fused_occupancy(int G, int* blocks_per_cu);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
@@ -60,17 +64,17 @@ enum KClass {
   KC_LARGE_B,
   KC_LARGE_C,
   KC_LARGE_MAP,
-  KC_LARGE_FIN,
   KC_GENERAL,
   KC_UPSERT,
   KC_RELEASE,
+  KC_LARGE_FUSED,
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "wave64x1",   "wave64x2",   "wave64x4",   "block256x2",
                                      "block256x4",   "block512x4", "block1024x4", "group16",   "group32",
                                      "large_a",      "large_b",
-                                     "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
-                                     "store_release"};
+                                     "large_c",      "large_map",  "general",    "store_upsert",
+                                     "store_release", "large_fused"};
 
 template <typename T>
 struct DBuf {
@@ -105,7 +109,10 @@ struct dm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   // auxiliary streams: independent size bins of one tick run concurrently
-  static constexpr int kAux = 3;
+  static constexpr int kAux = 4;
+  // auxiliary stream of each work class: bins 0..kNumBins-1, small packs, large chain
+  // (DM_SPLIT="ddddddddddd" overrides, one digit per class, for A/B runs)
+  int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (packs alone)
   hipStream_t aux[kAux] = {};
   hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
   hipEvent_t ev_fork = nullptr, ev_join[kAux] = {};
@@ -160,11 +167,27 @@ struct dm_ctx {
   DBuf<WorkItem> bins[kNumBins];
   DBuf<Chunk> chunks;
   DBuf<LargeSeg> large;
+  // one-launch large path (dm_large.hip): its own chunking (fused_G * kFusedRows rows)
+  int large_mode = DM_LARGE_CHAIN;
+  int fused_G = 512;
+  bool fused_ok = false;       // every large resource within the co-residency bound
+  int64_t fused_max_chunks = 0, fused_cap = 0;
+  uint32_t fused_epoch = 0;
+  std::vector<Chunk> h_fchunks;
+  std::vector<LargeSeg> h_flarge;
+  DBuf<Chunk> fchunks;
+  DBuf<LargeSeg> flarge;
+  DBuf<uint32_t> f_ticket, f_sync;
+  DBuf<uint64_t> f_part, f_tot;
+  uint32_t* h_ferr = nullptr;  // host-mapped: a fused wait gave up
+  uint32_t* d_ferr = nullptr;
+  bool use_fused() const { return large_mode == DM_LARGE_FUSED && fused_ok && !h_fchunks.empty(); }
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
   DBuf<int32_t> pa_nan;
   DBuf<uint8_t> pa_live, p_tot;
+  DBuf<uint32_t> p_arrive;
   // worklist of resources for k_general (heterogeneous-subclient FairShare)
   DBuf<int32_t> glist, gcount;
   bool maybe_general = false;
@@ -232,9 +255,13 @@ struct dm_ctx {
     agg.release(); cfg.release();
     out_gets.release(); out_expiry.release(); res.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
+    fchunks.release(); flarge.release(); f_ticket.release(); f_sync.release(); f_part.release(); f_tot.release();
+    if (h_ferr) (void)hipHostFree(h_ferr);
+    h_ferr = nullptr;
+    d_ferr = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pa_live.release(); p_tot.release();
+    pa_nan.release(); pa_live.release(); p_tot.release(); p_arrive.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
     st_mask.release(); st_blk.release(); st_wpre.release(); st_mwants.release(); st_rel.release();
@@ -301,6 +328,9 @@ static void build_plan(dm_ctx* c) {
   for (auto& b : c->h_bins) b.clear();
   c->h_chunks.clear();
   c->h_large.clear();
+  c->h_fchunks.clear();
+  c->h_flarge.clear();
+  const int64_t frows = (int64_t)c->fused_G * kFusedRows;
   const std::vector<int64_t>& off = c->h_seg_off;
   Pack cur{};
   bool open = false;
@@ -336,6 +366,13 @@ static void build_plan(dm_ctx* c) {
       }
       L.chunk_end = (int32_t)c->h_chunks.size();
       c->h_large.push_back(L);
+      LargeSeg F{(int32_t)r, (int32_t)c->h_fchunks.size(), 0, 0};
+      for (int64_t o = off[r]; o < off[r + 1]; o += frows) {
+        Chunk ch{(int32_t)r, (int32_t)c->h_flarge.size(), o, (int32_t)std::min<int64_t>(frows, off[r + 1] - o), 0};
+        c->h_fchunks.push_back(ch);
+      }
+      F.chunk_end = (int32_t)c->h_fchunks.size();
+      c->h_flarge.push_back(F);
     }
   }
   close();
@@ -347,6 +384,33 @@ static int upload_plan(dm_ctx* c) {
   for (int b = 0; b < kNumBins; ++b) DM_HIP(c, upload(c->bins[b], c->h_bins[b].data(), c->h_bins[b].size(), st), "plan bins");
   DM_HIP(c, upload(c->chunks, c->h_chunks.data(), c->h_chunks.size(), st), "plan chunks");
   DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
+  {  // one-launch large path: chunks, hand-off state, co-residency bound
+    DM_HIP(c, upload(c->fchunks, c->h_fchunks.data(), c->h_fchunks.size(), st), "plan fused chunks");
+    DM_HIP(c, upload(c->flarge, c->h_flarge.data(), c->h_flarge.size(), st), "plan fused large");
+    const size_t nf = std::max<size_t>(c->h_fchunks.size(), 1), nl = std::max<size_t>(c->h_flarge.size(), 1);
+    DM_HIP(c, c->f_ticket.ensure(4), "fused state");
+    DM_HIP(c, c->f_sync.ensure(nl * kFusedSync), "fused state");
+    DM_HIP(c, c->f_part.ensure(nf * kFusedWords), "fused state");
+    DM_HIP(c, c->f_tot.ensure(nl * kFusedWords), "fused state");
+    DM_HIP(c, hipMemsetAsync(c->f_ticket.p, 0, 4 * sizeof(uint32_t), st), "fused state");
+    DM_HIP(c, hipMemsetAsync(c->f_sync.p, 0, nl * kFusedSync * sizeof(uint32_t), st), "fused state");
+    if (!c->h_ferr) {
+      DM_HIP(c, hipHostMalloc((void**)&c->h_ferr, sizeof(uint32_t), hipHostMallocMapped), "fused error word");
+      *c->h_ferr = 0;
+      DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_ferr, c->h_ferr, 0), "fused error word");
+    }
+    c->fused_max_chunks = 0;
+    for (const LargeSeg& L : c->h_flarge)
+      c->fused_max_chunks = std::max<int64_t>(c->fused_max_chunks, L.chunk_end - L.chunk_begin);
+    int per_cu = 0, cus = 0;
+    DM_HIP(c, large_fused_occupancy(c->fused_G, &per_cu), "fused occupancy");
+    DM_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "CU count");
+    c->fused_cap = (int64_t)per_cu * cus;
+    // half the resident workgroups: room for a second process's fused launch on
+    // the same device (dm_large.hip, co-residency)
+    c->fused_ok = c->fused_max_chunks > 0 && 2 * c->fused_max_chunks <= c->fused_cap &&
+                  c->fused_max_chunks <= c->fused_G;  // the last arriver loads one record per thread
+  }
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
   DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
@@ -365,6 +429,9 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
   DM_HIP(c, c->pa_live.ensure(nc * 256), "partials");
   DM_HIP(c, c->p_tot.ensure(std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes), "partials");
+  DM_HIP(c, c->p_arrive.ensure(std::max<size_t>(c->h_large.size(), 1) * 4), "partials");
+  DM_HIP(c, hipMemsetAsync(c->p_arrive.p, 0, std::max<size_t>(c->h_large.size(), 1) * 4 * sizeof(uint32_t), st),
+         "partials");
   c->n_nonsmall = 0;
   for (int64_t r = 0; r < c->R; ++r)
     if (c->h_seg_off[r + 1] - c->h_seg_off[r] > kSmallMax) ++c->n_nonsmall;
@@ -396,6 +463,18 @@ template <typename T>
 static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStream_t st) {
   if (!dst || n == 0) return hipSuccess;
   return hipMemcpyAsync(dst, src + off, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, st);
+}
+
+// A wait of the one-launch large path gave up (its co-residency bound was
+// violated, e.g. by other processes' launches on the same device): the tick's
+// large-resource results are not valid.
+static int check_fused(dm_ctx* c) {
+  if (c->h_ferr && __atomic_load_n(c->h_ferr, __ATOMIC_ACQUIRE)) {
+    __atomic_store_n(c->h_ferr, 0u, __ATOMIC_RELEASE);
+    return c->fail(DM_E_HIP, "large-resource hand-off timed out (too few resident workgroups); the tick's leases "
+                             "are invalid -- retry with dm_set_large_path(ctx, DM_LARGE_CHAIN)");
+  }
+  return DM_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -438,6 +517,9 @@ int dm_create(int device, dm_ctx** out) {
   }
   dm_ctx* c = new dm_ctx();
   c->device = device;
+  if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
+  if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
+    for (int i = 0; i < kNumBins + 2 && sp[i] >= '0' && sp[i] < '0' + dm_ctx::kAux; ++i) c->class_stream[i] = sp[i] - '0';
   e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -515,6 +597,13 @@ int dm_sync(dm_ctx* c) {
   DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   c->collect_profile();
+  return check_fused(c);
+}
+
+int dm_set_large_path(dm_ctx* c, int mode) {
+  DM_ENTER(c);
+  if (mode != DM_LARGE_CHAIN && mode != DM_LARGE_FUSED) return c->fail(DM_E_INVAL, "unknown large-path mode");
+  c->large_mode = mode;
   return DM_OK;
 }
 
@@ -684,7 +773,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p,
-             c->pa_live.p, c->p_tot.p};
+             c->pa_live.p, c->p_tot.p, c->p_arrive.p};
   hipStream_t st = c->stream;
   auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t {
     if (!c->profiling) return fn();
@@ -695,7 +784,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     c->pending.push_back(pe);
     return e;
   };
-  const int nch = (int)c->h_chunks.size(), nls = (int)c->h_large.size();
+  const int nch = (int)c->h_chunks.size();
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
   const bool general = c->maybe_general && c->n_nonsmall > 0;
@@ -706,13 +795,14 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // Independent work classes: large resources (a 5-kernel chain), big groups,
   // small groups + packed.  With more than one class present they run on the
   // auxiliary streams concurrently, forked from and joined back to the main stream.
-  int big_bins = 0, small_bins = 0;
-  auto is_big = [](int b) { return b >= 4 && b <= 6; };  // block256x4, block512x4, block1024x4
-  for (int b = 0; b < kNumBins; ++b) (is_big(b) ? big_bins : small_bins) += !c->h_bins[b].empty();
-  const bool has_small = small_bins > 0 || !c->h_packs.empty();
-  const int classes = (nch > 0) + (big_bins > 0) + has_small;
-  const bool fork = classes > 1;
-  hipStream_t s_large = fork ? c->aux[0] : st, s_big = fork ? c->aux[1] : st, s_small = fork ? c->aux[2] : st;
+  unsigned used = 0;  // auxiliary streams with work this tick
+  for (int b = 0; b < kNumBins; ++b)
+    if (!c->h_bins[b].empty()) used |= 1u << c->class_stream[b];
+  if (!c->h_packs.empty()) used |= 1u << c->class_stream[kNumBins];
+  if (nch > 0) used |= 1u << c->class_stream[kNumBins + 1];
+  const bool fork = __builtin_popcount(used) > 1;
+  auto cls_stream = [&](int cls) { return fork ? c->aux[c->class_stream[cls]] : st; };
+  hipStream_t s_large = cls_stream(kNumBins + 1), s_small = cls_stream(kNumBins);
   if (!fork) {  // everything on the context stream, after any deferred class work
     DM_HIP(c, c->join_aux(), "join");
     c->main_dirty = true;
@@ -721,17 +811,26 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork");
     c->main_dirty = false;
   }
-  for (int ph = 0; ph < 5 && nch > 0; ++ph)
-    DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
-                    [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
-           "large-resource kernels");
+  if (nch > 0 && c->use_fused()) {
+    c->fused_epoch = c->fused_epoch + 1 == 0 ? 1 : c->fused_epoch + 1;
+    const FusedState F{c->f_ticket.p, c->f_sync.p, c->f_part.p, c->f_tot.p, c->d_ferr,
+                       (int32_t)c->h_fchunks.size(), c->fused_epoch};
+    DM_HIP(c, timed(KC_LARGE_FUSED, s_large,
+                    [&] { return launch_large_fused(c->fused_G, p, c->fchunks.p, c->flarge.p, F, gl, gc, s_large); }),
+           "large-resource kernel");
+  } else {
+    for (int ph = 0; ph < 4 && nch > 0; ++ph)
+      DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
+                      [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, P, gl, gc, s_large); }),
+             "large-resource kernels");
+  }
   // a store well beyond the Infinity Cache streams from HBM every tick: group
   // kernels then keep half their row loads in flight (dm_kernels.hip, BATCH)
   const bool hbm_stream = c->N * 48 > kStreamBytes;
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    hipStream_t s = is_big(b) ? s_big : s_small;
+    hipStream_t s = cls_stream(b);
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, hbm_stream, s); }),
            "group kernel");
   }
@@ -758,6 +857,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (!(flags & DM_ASYNC)) {
     DM_HIP(c, hipStreamSynchronize(st), "tick");
     c->collect_profile();
+    if ((rc = check_fused(c))) return rc;
   }
   return DM_OK;
 }
@@ -1384,13 +1484,17 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[4 + kNumBins];
+  int64_t v[8 + kNumBins];
   v[0] = (int64_t)c->h_packs.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
   v[2 + kNumBins] = (int64_t)c->h_chunks.size();
   v[3 + kNumBins] = c->N;
-  const int n = 4 + kNumBins;
+  v[4 + kNumBins] = c->use_fused() ? 1 : 0;
+  v[5 + kNumBins] = (int64_t)c->h_fchunks.size();
+  v[6 + kNumBins] = c->fused_max_chunks;
+  v[7 + kNumBins] = c->fused_cap;
+  const int n = 8 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }

@@ -16,7 +16,8 @@ from ._lib import check, lib
 from .workloads import CFG_FIELDS
 
 _BIN_NAMES = ("small_packs", "wave64x1", "wave64x2", "wave64x4", "block256x2", "block256x4", "block512x4",
-              "block1024x4", "group16", "group32", "large_resources", "large_chunks", "leases")
+              "block1024x4", "group16", "group32", "large_resources", "large_chunks", "leases",
+              "large_fused", "fused_chunks", "fused_max_chunks", "fused_capacity")
 
 
 def _ptr(a):
@@ -247,6 +248,11 @@ class Engine:
         """{SumWants, Count} per resource into a 16 B x R device buffer (server.go:234-255)."""
         self._chk(self._L.dm_publish_totals(self._ctx, ctypes.c_void_p(dev_ptr)))
 
+    def set_large_path(self, fused: bool):
+        """Large resources: the four-launch chain (default) or the one-launch path
+        (DM_LARGE_FUSED, when it fits the device's residency bound)."""
+        self._chk(self._L.dm_set_large_path(self._ctx, 1 if fused else 0))
+
     # -- profiling --
     def set_profiling(self, on: bool):
         self._chk(self._L.dm_set_profiling(self._ctx, 1 if on else 0))
@@ -260,8 +266,8 @@ class Engine:
         self._chk(self._L.dm_reset_kernel_times(self._ctx))
 
     def plan_info(self) -> dict:
-        arr = (ctypes.c_int64 * 16)()
-        n = self._chk(self._L.dm_plan_info(self._ctx, arr, 16))
+        arr = (ctypes.c_int64 * 32)()
+        n = self._chk(self._L.dm_plan_info(self._ctx, arr, 32))
         return {_BIN_NAMES[i]: int(arr[i]) for i in range(min(n, len(_BIN_NAMES)))}
 
 

@@ -41,6 +41,8 @@ def partition(seg_sizes, world: int) -> np.ndarray:
         if b > 0 and abs(csum[b - 1] - target) <= abs(csum[min(b, R)] - target):
             b -= 1
         b = max(b, bounds[-1] + (1 if R - bounds[-1] > world - k else 0))
+        if R >= world:  # leave at least one resource for each later shard
+            b = min(b, R - (world - k))
         bounds.append(min(b, R))
     bounds.append(R)
     return np.asarray(bounds, dtype=np.int64)

@@ -270,13 +270,29 @@ int dm_hier_root_tick(dm_ctx* root, const void* dev_gathered, int n_servers, int
 #define DM_HIER_COUNT_RANGE 2u
 int dm_hier_status(dm_ctx* root, uint32_t* status, int n_servers);
 
+/* ---- large resources (more than 4096 rows) ----
+ * DM_LARGE_CHAIN (default): 2048-row chunks in four stream-ordered launches (Clean
+ * + speculative round 1, round 1 again where Clean released subclients, FairShare
+ * round 2, the map); each launch's last-arriving chunk of a resource leaves the
+ * resource's totals (algorithm.go:156-204, 259-279) for the next.
+ * DM_LARGE_FUSED: one launch in which every chunk keeps its rows in registers while
+ * the chunks of a resource exchange those totals in-launch (one HBM pass); used
+ * only when every large resource has at most half as many chunks as the device
+ * keeps resident, else the chain runs.  Results are bit-identical; dm_plan_info
+ * reports which path a tick takes. */
+#define DM_LARGE_CHAIN 0
+#define DM_LARGE_FUSED 1
+int dm_set_large_path(dm_ctx* ctx, int mode);
+
 /* ---- profiling ---- */
 int dm_set_profiling(dm_ctx* ctx, int on);
 /* fills up to max entries; returns the number of kernel classes (>= 0) */
 int dm_kernel_times(dm_ctx* ctx, dm_kernel_time* out, int max);
 int dm_reset_kernel_times(dm_ctx* ctx);
 /* plan summary of the loaded store: counts per dispatch bin (small packs, 64x1,
- * 256x1..256x16, large chunks) */
+ * 256x1..256x16, large resources, large chunks, leases), then whether ticks use
+ * the one-launch large path, its chunks, the most chunks of one resource and the
+ * device's resident-workgroup bound */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 
 /* ---- round-oriented GetCapacity dispatch (dm_server.cpp) ----

@@ -349,7 +349,7 @@ def test_wrong_number_of_clients_through_the_abi():
 
 
 def test_lease_length_and_refresh_interval_through_the_abi(eng):
-    """algorithm_test.go:495-522: expiry = now + lease_length, refresh as configured."""
+    """algorithm_test.go:285-312: expiry = now + lease_length, refresh as configured."""
     k = KATS["lease_length"]
     snap = W.make_snapshot([1], [k["wants"]], [0.0], [k["sub"]], NOW + W.NS, k["kind"], k["capacity"],
                            k["lease_length"], k["refresh_interval"])

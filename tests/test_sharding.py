@@ -29,6 +29,18 @@ def test_partition_uniform_is_even():
     assert np.all(np.diff(b) == 1250)
 
 
+@pytest.mark.parametrize("sizes,world", [([1, 1, 100], 3), ([100, 1, 1], 3), ([1, 1, 1, 1000, 1], 4),
+                                         ([7] * 8, 8), ([1, 10**6, 1, 1, 1, 1, 1, 1], 8), ([1, 1], 3)])
+def test_partition_every_shard_gets_a_resource(sizes, world):
+    """With at least as many resources as shards no shard is left empty, however
+    skewed the sizes (a huge resource near the front must not swallow the later
+    boundaries)."""
+    b = H.partition(sizes, world)
+    assert b[0] == 0 and b[-1] == len(sizes) and np.all(np.diff(b) >= 0) and len(b) == world + 1
+    if len(sizes) >= world:
+        assert np.all(np.diff(b) >= 1), b
+
+
 def test_shard_roundtrip():
     rng = np.random.default_rng(0)
     snap = W.random_snapshot(rng, 40, 30)

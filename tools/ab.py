@@ -1,6 +1,6 @@
 """Interleaved A/B timing of library builds in ONE process (cdna guide §5.4 rule 24).
 
-  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so ...
+  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:fused] ...
 
 Every build gets its own context with the same snapshot; rounds alternate between
 builds; per build the per-launch kernel time (HIP events) and the tick wall time
@@ -32,8 +32,11 @@ def main():
     snap = make_workload(args.workload, 0)
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
     engines = []
-    for p in args.libs:
-        e = Engine(0, os.path.abspath(p))
+    for p in args.libs:  # LIB.so:fused = the same build with the large-resource chain forced
+        path, _, mode = p.partition(":")
+        e = Engine(0, os.path.abspath(path))
+        if mode.startswith("fused"):
+            e.set_large_path(fused=True)
         e.load(snap)
         for _ in range(3):
             e.apportion(W.NOW_NS, writeback=True)

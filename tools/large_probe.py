@@ -1,0 +1,70 @@
+"""Large-resource class alone: per-kernel times of C2's resources > 4096 rows
+(or the whole C2 tick with --all) for library builds and large-path modes.
+
+  python tools/large_probe.py [--all] LIB.so[:chain] ...
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402,F401
+
+from doorman_amd import workloads as W  # noqa: E402
+from doorman_amd.engine import Engine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--all", action="store_true")
+    ap.add_argument("--small", action="store_true", help="only the resources of <= 4096 rows")
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    snap = W.c2()
+    if not args.all:
+        import numpy as np
+        sizes = np.diff(snap["seg_off"])
+        snap = W.subset(snap, np.flatnonzero((sizes <= 4096) if args.small else (sizes > 4096)))
+    n = len(snap["wants"])
+    for p in args.libs:
+        p, _, envs = p.partition("@")  # LIB[:mode][@VAR=value,...]: environment for that engine
+        for kv in filter(None, envs.split(",")):
+            var, _, val = kv.partition("=")
+            os.environ[var] = val
+        path, _, mode = p.partition(":")
+        os.environ["DM_FUSED_G"] = "256" if mode.endswith("256") else "512"
+        e = Engine(0, os.path.abspath(path))
+        if mode.startswith("fused"):
+            e.set_large_path(fused=True)
+        e.load(snap)
+        for _ in range(5):
+            e.apportion(W.NOW_NS, writeback=True)
+        e.set_profiling(True)
+        e.reset_kernel_times()
+        import time
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+        e.sync()
+        dt = (time.perf_counter() - t0) / args.steps * 1e6
+        kt = e.kernel_times()
+        e.set_profiling(False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+        e.sync()
+        dp = (time.perf_counter() - t0) / args.steps * 1e6
+        e.close()
+        for kv in filter(None, envs.split(",")):
+            os.environ.pop(kv.partition("=")[0], None)
+        ks = "  ".join(f"{k} {ms / cnt * 1e3:.1f}" for k, (cnt, ms) in sorted(kt.items()))
+        print(f"{os.path.basename(p) + '@' + envs:40s} rows {n} tick {dt:7.1f} us, unprofiled {dp:7.1f} us | {ks}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
