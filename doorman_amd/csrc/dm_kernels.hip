@@ -807,19 +807,88 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
 // --------------------------------------------------------------------------
 // General FairShare: resources with heterogeneous subclients or NaN wants, from
 // any size bin (appended to the worklist by the other kernels, which leave such
-// a resource untouched).  One workgroup streams the resource: Clean, round 1,
-// then one round-2 pass per distinct threshold in increasing order.  Only the
-// hierarchy's root level (GetServerCapacity) produces such resources.
+// a resource untouched); only the hierarchy's root level (GetServerCapacity)
+// produces them.  One workgroup per resource: Clean, round 1, then round 2
+// (algorithm.go:188-204), where every row has its own threshold
+// T(s) = deservedExtra + deservedShare -- one value per distinct subclient count.
+// Round 2 by sorted thresholds: the distinct finite thresholds T_1 < ... < T_K are
+// collected in LDS (hash set, then a bitonic sort); one pass puts every
+// wantExtra client's wants into one of 2K+1 buckets (between / equal to the
+// thresholds, binary search) with per-bucket (count, sum of wants, sum of
+// subclients) accumulated per wave in a fixed order (each 64-row tile sorted by
+// bucket, segmented sums, one writer per bucket); prefix sums over the buckets
+// then give every threshold's
+//   extraExtra     = k(T)*T - sum(w_j < T)   (the algebraic form of
+//                                             sum(T - w_j), within the tolerance)
+//   wantExtraExtra = sum(s_j : w_j > T)
+// in O(n log K) instead of one pass over the resource per threshold.  More than
+// kGenMaxT thresholds, or a non-finite one, keep the per-threshold passes.
+constexpr int kGenMaxT = 256;
+constexpr int kGenBuckets = 2 * kGenMaxT + 1;
+constexpr uint64_t kGenEmpty = ~0ull;  // a NaN pattern: never a finite threshold's bits
+struct GenLds {
+  uint64_t set[2 * kGenMaxT];  // threshold bit patterns, open addressing
+  double T[kGenMaxT];          // sorted distinct thresholds
+  double ee[kGenMaxT];         // extraExtra per threshold
+  long long sgt[kGenMaxT];     // wantExtraExtra - own subclients, per threshold
+  double accw[4][kGenBuckets];
+  long long accs[4][kGenBuckets];
+  int accc[4][kGenBuckets];
+  int nT, overflow;
+};
+
+// ascending bitonic sort of one key per lane across the wave
+__device__ __forceinline__ uint32_t wave_sort64(uint32_t key) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t other = (uint32_t)__shfl_xor((int)key, j, 64);
+      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      key = keep_min ? (key < other ? key : other) : (key > other ? key : other);
+    }
+  }
+  return key;
+}
+
+// m = number of thresholds below w; bucket 2m (strictly between) or 2m+1 (== T_m+1)
+__device__ __forceinline__ int gen_bucket(const double* T, int K, double w) {
+  int lo = 0, hi = K;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (T[mid] < w)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (lo < K && T[lo] == w) ? 2 * lo + 1 : 2 * lo;
+}
+
+__device__ __forceinline__ int gen_index(const double* T, int K, double t) {  // T[k] == t
+  int lo = 0, hi = K;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (T[mid] < t)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count) {
   __shared__ Lds<256> lds;
+  __shared__ GenLds gs;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int nlist = *count;
   for (int idx = blockIdx.x; idx < nlist; idx += gridDim.x) {
     const int seg = list[idx];
     const int64_t lo = p.seg_off[seg], hi = p.seg_off[seg + 1];
     const Res rs = load_res(p, seg);
     AggA a = zeroA();
-    for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+    for (int64_t row = lo + t; row < hi; row += 256) {
       const double w = p.wants[row], h = p.has[row];
       const long long s = p.sub[row];
       const bool lv = !(p.now > p.expiry[row]);
@@ -835,16 +904,16 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
       }
     }
     {
-    const AggR all_part = a.all;
-    a = group_reduce<256>(a, OpA(), lds.a);
-    if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
-  }
+      const AggR all_part = a.all;
+      a = group_reduce<256>(a, OpA(), lds.a);
+      if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
+    }
     const Clean cl = clean_from(p, rs, a);
     const double C = rs.C;
     const double eq = C / (double)cl.count;
     // round 1 sums (algorithm.go:156-171)
     AggB b{0.0, 0.0, 0};
-    for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+    for (int64_t row = lo + t; row < hi; row += 256) {
       if (p.now > p.expiry[row]) continue;
       const double w = p.wants[row];
       const long long s = p.sub[row];
@@ -855,9 +924,16 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         b.i += s;
     }
     b = group_reduce<256>(b, OpB(), lds.b);
-    // rows decided in round 0/1, released rows, NaN thresholds
+    for (int i = t; i < 2 * kGenMaxT; i += 256) gs.set[i] = kGenEmpty;
+    if (t == 0) {
+      gs.nT = 0;
+      gs.overflow = 0;
+    }
+    __syncthreads();
+    // rows decided in round 0/1, released rows, NaN thresholds; the other rows'
+    // thresholds into the set
     SumD delta{0.0};
-    for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+    for (int64_t row = lo + t; row < hi; row += 256) {
       const double w = p.wants[row], h = p.has[row];
       const long long s = p.sub[row];
       if (p.now > p.expiry[row]) {
@@ -879,55 +955,182 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         __builtin_nontemporal_store(g, p.out_gets + row);
         __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
         delta.v += g - h;
+      } else if (!__builtin_isfinite(T)) {
+        gs.overflow = 1;  // +-Inf threshold: the per-threshold passes below
+      } else {
+        const uint64_t key = __builtin_bit_cast(uint64_t, T);
+        uint32_t slot = (uint32_t)((key ^ (key >> 29)) * 0x9E3779B97F4A7C15ull >> 40) & (2 * kGenMaxT - 1);
+        for (int probe = 0; probe < 2 * kGenMaxT; ++probe, slot = (slot + 1) & (2 * kGenMaxT - 1)) {
+          uint64_t cur = gs.set[slot];
+          if (cur == key) break;
+          if (cur == kGenEmpty) {
+            cur = atomicCAS((unsigned long long*)&gs.set[slot], (unsigned long long)kGenEmpty, (unsigned long long)key);
+            if (cur == kGenEmpty) {
+              if (atomicAdd(&gs.nT, 1) >= kGenMaxT) gs.overflow = 1;
+              break;
+            }
+            if (cur == key) break;
+          }
+        }
       }
     }
-    // round 2 (algorithm.go:188-204), one distinct threshold at a time.  The rows
-    // written above keep their inputs in registers only within their own pass, so
-    // round 2 re-reads has from a resource that is already partly written back:
-    // only rows that are still undecided are read, and those are untouched.
-    double prev = 0.0;
-    int have_prev = 0;
-    for (;;) {
-      TMin tm{0.0, 0, 0};
-      for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
-        if (p.now > p.expiry[row]) continue;
-        double g, T = 0.0;
-        if (fs_stage01(p.wants[row], p.has[row], p.sub[row], C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
-        if (__builtin_isnan(T) || (have_prev && !(T > prev))) continue;
-        tmin_add(tm, T);
+    __syncthreads();
+    const bool buckets = !gs.overflow;
+    const int K = gs.nT;
+    if (buckets && K > 0) {
+      // the distinct thresholds, sorted: compact the set, pad with +Inf, bitonic sort
+      __shared__ int nfill;
+      if (t == 0) nfill = 0;
+      __syncthreads();
+      for (int i = t; i < 2 * kGenMaxT; i += 256)
+        if (gs.set[i] != kGenEmpty) gs.T[atomicAdd(&nfill, 1)] = __builtin_bit_cast(double, gs.set[i]);
+      __syncthreads();
+      if (t >= K) gs.T[t] = __builtin_inf();
+      for (int k = 2; k <= kGenMaxT; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          __syncthreads();
+          const int q = t ^ j;
+          if (q > t) {
+            const double x = gs.T[t], y = gs.T[q];
+            const bool asc = (t & k) == 0;
+            if ((x > y) == asc) {
+              gs.T[t] = y;
+              gs.T[q] = x;
+            }
+          }
+        }
+      for (int i = t; i < 4 * kGenBuckets; i += 256) {
+        (&gs.accw[0][0])[i] = 0.0;
+        (&gs.accs[0][0])[i] = 0;
+        (&gs.accc[0][0])[i] = 0;
       }
-      tm = group_reduce<256>(tm, OpTMin(), lds.t);
-      if (!tm.found) break;
-      const double Ts = tm.t;
-      AggC c{0.0, 0};
-      for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
-        if (p.now > p.expiry[row]) continue;
-        const double w = p.wants[row];
-        const long long s = p.sub[row];
-        if (!(w > (double)s * eq)) continue;
-        if (w < Ts)
-          c.ee += Ts - w;
-        else if (w > Ts)
-          c.sgt += s;
+      __syncthreads();
+      // bucket pass over the wantExtra clients (w > d, algorithm.go:165-169): wave wv
+      // takes 64-row tiles wv, wv+4, ... in order; in a tile the lanes are sorted by
+      // bucket and each bucket's run summed in lane order
+      for (int64_t base = lo + (int64_t)wv * 64; base < hi; base += 256) {
+        const int64_t row = base + lane;
+        double w = 0.0;
+        long long s = 0;
+        uint32_t bk = 0xFFFFu;
+        if (row < hi && !(p.now > p.expiry[row])) {
+          w = p.wants[row];
+          s = p.sub[row];
+          if (w > (double)s * eq) bk = (uint32_t)gen_bucket(gs.T, K, w);
+        }
+        const uint32_t key = wave_sort64(bk << 6 | (uint32_t)lane);
+        const int src = (int)(key & 63);
+        const int mb = (int)(key >> 6);
+        double vw = shfl_d(w, src);
+        long long vs = __shfl(s, src, 64);
+        int vc = mb != 0xFFFF ? 1 : 0;
+        const int prevb = __shfl_up(mb, 1, 64);
+        int run = (lane == 0 || prevb != mb) ? 1 : 0;  // first lane of its bucket's run
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {  // segmented inclusive scan, earlier + later
+          const double ow = shfl_d(vw, lane >= off ? lane - off : lane);
+          const long long os = __shfl(vs, lane >= off ? lane - off : lane, 64);
+          const int oc = __shfl(vc, lane >= off ? lane - off : lane, 64);
+          const int orun = __shfl(run, lane >= off ? lane - off : lane, 64);
+          if (lane >= off && !run) {
+            vw = ow + vw;
+            vs = os + vs;
+            vc = oc + vc;
+            run = orun;
+          }
+        }
+        const int nextb = __shfl_down(mb, 1, 64);
+        if (mb != 0xFFFF && (lane == 63 || nextb != mb)) {  // last lane of its run: one writer per bucket
+          gs.accw[wv][mb] += vw;
+          gs.accs[wv][mb] += vs;
+          gs.accc[wv][mb] += vc;
+        }
       }
-      c = group_reduce<256>(c, OpC(), lds.c);
-      for (int64_t row = lo + threadIdx.x; row < hi; row += 256) {
+      __syncthreads();
+      if (t == 0) {  // prefix over the buckets, waves combined in a fixed order
+        long long cnt = 0, stot = 0;
+        double sw = 0.0;
+        for (int bb = 0; bb < 2 * K + 1; ++bb)
+          stot += gs.accs[0][bb] + gs.accs[1][bb] + gs.accs[2][bb] + gs.accs[3][bb];
+        long long sle = 0;  // subclients of buckets <= 2k-1 (w <= T_k)
+        for (int k = 0; k < K; ++k) {
+          // buckets 2k (below T_k) join the "below" sums; 2k+1 is w == T_k
+          const int bl = 2 * k;
+          cnt += gs.accc[0][bl] + gs.accc[1][bl] + gs.accc[2][bl] + gs.accc[3][bl];
+          sw = sw + gs.accw[0][bl] + gs.accw[1][bl] + gs.accw[2][bl] + gs.accw[3][bl];
+          sle += gs.accs[0][bl] + gs.accs[1][bl] + gs.accs[2][bl] + gs.accs[3][bl];
+          const long long seq = gs.accs[0][bl + 1] + gs.accs[1][bl + 1] + gs.accs[2][bl + 1] + gs.accs[3][bl + 1];
+          gs.ee[k] = cnt == 0 ? 0.0 : (double)cnt * gs.T[k] - sw;  // :197-198
+          gs.sgt[k] = stot - sle - seq;                              // :199-200
+          sle += seq;
+          cnt += gs.accc[0][bl + 1] + gs.accc[1][bl + 1] + gs.accc[2][bl + 1] + gs.accc[3][bl + 1];
+          sw = sw + gs.accw[0][bl + 1] + gs.accw[1][bl + 1] + gs.accw[2][bl + 1] + gs.accw[3][bl + 1];
+        }
+      }
+      __syncthreads();
+      for (int64_t row = lo + t; row < hi; row += 256) {
         if (p.now > p.expiry[row]) continue;
         const double w = p.wants[row], h = p.has[row];
         const long long s = p.sub[row];
         double g, T = 0.0;
         if (fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
-        if (!(T == Ts)) continue;
-        g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, c);
+        if (__builtin_isnan(T)) continue;  // decided above
+        const int k = gen_index(gs.T, K, T);
+        g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, AggC{gs.ee[k], gs.sgt[k]});
         __builtin_nontemporal_store(g, p.out_gets + row);
         __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
         delta.v += g - h;
       }
-      prev = Ts;
-      have_prev = 1;
+    } else if (!buckets) {
+      // round 2 one distinct threshold at a time.  The rows written above keep
+      // their inputs in registers only within their own pass, so round 2 re-reads
+      // has from a resource that is already partly written back: only rows that are
+      // still undecided are read, and those are untouched.
+      double prev = 0.0;
+      int have_prev = 0;
+      for (;;) {
+        TMin tm{0.0, 0, 0};
+        for (int64_t row = lo + t; row < hi; row += 256) {
+          if (p.now > p.expiry[row]) continue;
+          double g, T = 0.0;
+          if (fs_stage01(p.wants[row], p.has[row], p.sub[row], C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+          if (__builtin_isnan(T) || (have_prev && !(T > prev))) continue;
+          tmin_add(tm, T);
+        }
+        tm = group_reduce<256>(tm, OpTMin(), lds.t);
+        if (!tm.found) break;
+        const double Ts = tm.t;
+        AggC c{0.0, 0};
+        for (int64_t row = lo + t; row < hi; row += 256) {
+          if (p.now > p.expiry[row]) continue;
+          const double w = p.wants[row];
+          const long long s = p.sub[row];
+          if (!(w > (double)s * eq)) continue;
+          if (w < Ts)
+            c.ee += Ts - w;
+          else if (w > Ts)
+            c.sgt += s;
+        }
+        c = group_reduce<256>(c, OpC(), lds.c);
+        for (int64_t row = lo + t; row < hi; row += 256) {
+          if (p.now > p.expiry[row]) continue;
+          const double w = p.wants[row], h = p.has[row];
+          const long long s = p.sub[row];
+          double g, T = 0.0;
+          if (fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+          if (!(T == Ts)) continue;
+          g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, c);
+          __builtin_nontemporal_store(g, p.out_gets + row);
+          __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
+          delta.v += g - h;
+        }
+        prev = Ts;
+        have_prev = 1;
+      }
     }
     delta = group_reduce<256>(delta, OpSumD(), lds.d);
-    if (threadIdx.x == 0) write_resource(p, seg, rs, cl, delta.v);
+    if (t == 0) write_resource(p, seg, rs, cl, delta.v);
+    __syncthreads();  // the next resource reuses the LDS
   }
 }
 

@@ -145,6 +145,23 @@ def test_closed_form_equals_literal(seed):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
+@pytest.mark.parametrize("variant", ["uniform", "hetero", "edge", "hetero_edge"])
+def test_closed_form_equals_literal_large_resources(variant):
+    """The same identity on resources of 1k-5k rows (every GPU parity test compares
+    against the closed form at up to 1M rows per resource): FairShare and
+    ProportionalShare with contention, heterogeneous subclients and IEEE edge values."""
+    from parity_util import snapshot_with_sizes
+    rng = np.random.default_rng(["uniform", "hetero", "edge", "hetero_edge"].index(variant) + 40)
+    sizes = np.asarray([1000, 1800, 2500, 5000], dtype=np.int64)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(2, 3), hetero="hetero" in variant, edge="edge" in variant,
+                               learning_frac=0.0, parent_expired_frac=0.0)
+    snap["kind"] = np.asarray([2, 3, 3, 3], dtype=np.int32)
+    a = O.apportion(snap, NOW, "literal")
+    b = O.apportion(snap, NOW, "closed")
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
 def test_threaded_closed_form_matches():
     """The OpenMP comparator (bench.py cpu_baseline 'closed_mt') gives the same bits."""
     rng = np.random.default_rng(7)
