@@ -9,15 +9,16 @@ constexpr int64_t kNs = 1000000000LL;
 
 // Dispatch bins.  A segment of n rows goes to:
 //   n <= kSmallMax            : wave-packed literal path (many resources per wave)
-//   n <= 16 / 32              : 16- / 32-lane groups, 4 / 2 resources per wave (bins 7, 8)
-//   n <= 64 / 128 / 256       : one wave per resource, R = 1, 2, 4 rows per lane (4 resources per workgroup)
+//   n <= 16 / 32              : 8- / 16-lane groups, 2 rows per lane, 8 / 4 resources per wave (bins 7, 8)
+//   n <= 64 / 128             : 16- / 32-lane groups, 4 rows per lane, 4 / 2 resources per wave (bins 0, 1)
+//   n <= 256                  : one wave per resource, 4 rows per lane (4 resources per workgroup)
 //   n <= 512 / 1024           : one 256-thread workgroup, R = 2, 4 rows per thread in VGPRs
 //   n <= 2048 / 4096          : one 512- / 1024-thread workgroup, 4 rows per thread
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
 constexpr int kSmallMax = 8;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
-constexpr int kNumBins = 9;  // wave64x{1,2,4}, block256x{2,4}, block512x4, block1024x4, group16, group32
+constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block256x{2,4}, block512x4, block1024x4, sub8x2, sub16x2
 // Lease-table footprint (48 B per lease) above which a tick is taken to stream
 // from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
 constexpr int64_t kStreamBytes = 1LL << 30;

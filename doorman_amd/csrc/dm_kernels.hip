@@ -211,16 +211,19 @@ __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __res
   group_segment<64, R, BATCH>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
 }
 
-// Sub-wave groups: G = 16 or 32 lanes own one resource of up to G rows, so a
-// wave decides 64 / G resources with one set of reduction chains (DPP inside
-// each 16-lane row, plus one readlane combine for G = 32).
-template <int G>
+// Sub-wave groups: G = 16 or 32 lanes own one resource of up to G*R rows (R rows
+// per lane), so a wave decides 64 / G resources with one set of reduction chains
+// (DPP inside each 16-lane row, plus one readlane combine for G = 32).  Small
+// resources are VALU-bound on their per-resource reductions (~28 reduced dwords
+// per pass set, 4 DPP steps each): narrow groups with several rows per lane share
+// every DPP step among 64 / G resources.
+template <int G, int R = 1>
 __global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   Lds<G> lds;  // unused by sub-wave reductions
   const int i = blockIdx.x * (256 / G) + (int)(threadIdx.x / G);
   if (i >= nitems) return;  // whole groups only: reductions never cross a group
-  group_segment<G, 1, 1>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
+  group_segment<G, R, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -1725,8 +1728,8 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
   if (n <= 0) return hipSuccess;
   const unsigned wg4 = (unsigned)((n + 3) / 4);
   switch (bin) {
-    case 0: k_wave<1><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 1: k_wave<2><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 0: k_sub<16, 4><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 1: k_sub<32, 4><<<(unsigned)((n + 7) / 8), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 2:
       if (hbm_stream) k_wave<4, 2><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount);
       else k_wave<4><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount);
@@ -1744,8 +1747,8 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
       if (hbm_stream) k_block<1024, 4, 2><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
       else k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
       break;
-    case 7: k_sub<16><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 8: k_sub<32><<<(unsigned)((n + 7) / 8), 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 7: k_sub<8, 2><<<(unsigned)((n + 31) / 32), 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 8: k_sub<16, 2><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
