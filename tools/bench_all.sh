@@ -1,5 +1,6 @@
 #!/bin/bash
-# Every bench workload once (one GPU), JSON lines into gpurun_out/bench_all/.
+# Every bench workload once (one GPU), JSON lines into gpurun_out/bench_all/
+# (c3 runs the hierarchy exchange by default; hier.json is c3 without it).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/bench_all
@@ -8,6 +9,6 @@ for w in ${WORKLOADS:-c1 c1ps c2 c3 c4}; do
     > gpurun_out/bench_all/$w.json 2> gpurun_out/bench_all/$w.err
   s=$?; echo "$w status $s"; [ $s -ne 0 ] && { tail -3 gpurun_out/bench_all/$w.err; exit $s; }
 done
-timeout -k 10 600 python bench.py --hier --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline \
+timeout -k 10 600 python bench.py --workload c3 --hier off --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline \
   > gpurun_out/bench_all/hier.json 2> gpurun_out/bench_all/hier.err
-s=$?; echo "hier status $s"; exit $s
+s=$?; echo "c3 without hierarchy: status $s"; exit $s

@@ -21,13 +21,19 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--all", action="store_true")
     ap.add_argument("--small", action="store_true", help="only the resources of <= 4096 rows")
+    ap.add_argument("--sizes", default=None, help="LO-HI: only resources with LO <= rows <= HI")
     ap.add_argument("--steps", type=int, default=20)
     args = ap.parse_args()
     snap = W.c2()
     if not args.all:
         import numpy as np
         sizes = np.diff(snap["seg_off"])
-        snap = W.subset(snap, np.flatnonzero((sizes <= 4096) if args.small else (sizes > 4096)))
+        if args.sizes:
+            lo, hi = (int(x) for x in args.sizes.split("-"))
+            keep = (sizes >= lo) & (sizes <= hi)
+        else:
+            keep = (sizes <= 4096) if args.small else (sizes > 4096)
+        snap = W.subset(snap, np.flatnonzero(keep))
     n = len(snap["wants"])
     for p in args.libs:
         p, _, envs = p.partition("@")  # LIB[:mode][@VAR=value,...]: environment for that engine
