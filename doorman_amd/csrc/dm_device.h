@@ -77,12 +77,10 @@ struct Partials {
   // pass A: live-row mask, one byte per thread of each chunk (bit k = row k*256+tid),
   // so passes B and C read wants (+ subclients for ProportionalShare) and not expiry
   uint8_t* live;
-  // per large resource (kSegTotBytes each): the totals each launch's last arriving
-  // chunk leaves for the next launch (dm_kernels.hip, SegTot)
+  // per large resource (kSegTotBytes each): pass A totals left by pass B's first
+  // chunk, pass B totals left by pass C's first chunk, so the map reduces at most
+  // one set of partials
   uint8_t* tot;
-  // per large resource: arrival counters of launches A, B, C and the map (zero
-  // between launches: each is reset by its last arriver)
-  uint32_t* arrive;
 };
 constexpr int kSegTotBytes = 128;
 

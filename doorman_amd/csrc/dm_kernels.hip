@@ -417,76 +417,57 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
 }
 
 // --------------------------------------------------------------------------
-// Large resources (n > kLargeMin): kChunkRows-row chunks, one workgroup each, in
-// stream-ordered launches A (Clean + speculative round 1), B (round 1 again, only
-// where Clean released subclients), C (FairShare round 2) and the map.  In each
-// launch every chunk stores its partial sums write-through and arrives at a
-// per-resource counter (wave 0 only: the other waves exit as soon as the
-// workgroup's partial is reduced); the last arriver (told by its add's return
-// value) reduces the resource's partials with one fixed tree (a 64-lane strided
-// loop over the chunks, then a wave reduction) and leaves the totals (SegTot) for
-// the next launch.  No chunk waits for another, every chunk of a resource reads the
-// same totals, and no launch re-reduces all partials in every chunk.
+// Large resources (n > kLargeMin): kChunkRows-row chunks, one workgroup each.
+// Per-resource totals are re-derived in every workgroup from the chunk partials
+// with the same fixed reduction tree, so all chunks of a resource agree exactly.
 // --------------------------------------------------------------------------
 struct SegTot {
-  AggA a;           // Clean totals (launch A)
-  AggB b;           // round 1 / ProportionalShare sums: speculative from A, or launch B
-  AggC c;           // FairShare round 2 (launch C)
-  int32_t need_b;   // launch B recomputes round 1 (Clean released subclients, or recompute mode)
-  int32_t general;  // heterogeneous-subclient FairShare: k_general decides the resource
+  AggA a;
+  AggB b;
 };
 static_assert(sizeof(SegTot) <= kSegTotBytes, "SegTot slot");
 __device__ __forceinline__ SegTot* seg_tot(const Partials& P, int lseg) {
   return reinterpret_cast<SegTot*>(P.tot + (size_t)lseg * kSegTotBytes);
 }
 
-// Last arriver, wave 0: the resource's pass-A totals from every chunk's partial.
-__device__ __forceinline__ AggA reduce_a(const DevParams& p, const Partials& P, const LargeSeg& L) {
+template <int G>
+__device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials& P, const LargeSeg& L,
+                                              Lds<G>& lds) {
   AggA a = zeroA();
-  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 64) {
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += G) {
     AggA x;
-    x.cnt = ld_wt(P.a_cnt + c);
-    x.h = ld_wt(P.a_has + c);
-    x.w = ld_wt(P.a_wants + c);
-    x.all = AggR{ld_wt(P.a_cnt_all + c), ld_wt(P.a_has_all + c), ld_wt(P.a_wants_all + c)};
-    x.smin = (int)ld_wt(P.a_smin + c);
-    x.smax = (int)ld_wt(P.a_smax + c);
-    x.nan = ld_wt(P.a_nan + c);
+    x.cnt = P.a_cnt[c];
+    x.h = P.a_has[c];
+    x.w = P.a_wants[c];
+    x.all = AggR{P.a_cnt_all[c], P.a_has_all[c], P.a_wants_all[c]};
+    x.smin = (int)P.a_smin[c];
+    x.smax = (int)P.a_smax[c];
+    x.nan = P.a_nan[c];
     x.pad = 0;
     const AggR all = OpR()(a.all, x.all);  // OpA carries `all` through unchanged
     a = OpA()(a, x);
     a.all = all;
   }
-  const AggR all_part = a.all;
-  a = wave_reduce(a, OpA());
-  if (p.recompute) a.all = wave_reduce(all_part, OpR());
-  return a;
+  {
+    const AggR all_part = a.all;
+    a = group_reduce<G>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce<G>(all_part, OpR(), lds.r);
+  }
+  return seg_state_of(p, L.seg, a);
 }
 
-__device__ __forceinline__ AggB reduce_b(const Partials& P, const LargeSeg& L) {
+template <int G>
+__device__ __forceinline__ AggB seg_b(const Partials& P, const LargeSeg& L, Lds<G>& lds) {
   AggB b{0.0, 0.0, 0};
-  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 64)
-    b = OpB()(b, AggB{ld_wt(P.b_x + c), ld_wt(P.b_y + c), (long long)ld_wt(P.b_w + c)});
-  return wave_reduce(b, OpB());
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += G) b = OpB()(b, AggB{P.b_x[c], P.b_y[c], P.b_w[c]});
+  return group_reduce<G>(b, OpB(), lds.b);
 }
 
-__device__ __forceinline__ AggC reduce_c(const Partials& P, const LargeSeg& L) {
+template <int G>
+__device__ __forceinline__ AggC seg_c(const Partials& P, const LargeSeg& L, Lds<G>& lds) {
   AggC c{0.0, 0};
-  for (int q = L.chunk_begin + (int)threadIdx.x; q < L.chunk_end; q += 64)
-    c = OpC()(c, AggC{ld_wt(P.c_ee + q), (long long)ld_wt(P.c_sgt + q)});
-  return wave_reduce(c, OpC());
-}
-
-__device__ __forceinline__ SumD reduce_d(const Partials& P, const LargeSeg& L) {
-  SumD d{0.0};
-  for (int q = L.chunk_begin + (int)threadIdx.x; q < L.chunk_end; q += 64) d.v += ld_wt(P.d_delta + q);
-  return wave_reduce(d, OpSumD());
-}
-
-__device__ __forceinline__ void store_b_partial(const Partials& P, int c, const AggB& b) {
-  st_wt(P.b_x + c, b.x);
-  st_wt(P.b_y + c, b.y);
-  st_wt(P.b_w + c, (int64_t)b.i);
+  for (int q = L.chunk_begin + (int)threadIdx.x; q < L.chunk_end; q += G) c = OpC()(c, AggC{P.c_ee[q], P.c_sgt[q]});
+  return group_reduce<G>(c, OpC(), lds.c);
 }
 
 // kChunkRows rows of one chunk, kLR per thread, loaded in one batch (all loads in
@@ -526,8 +507,8 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   }
 }
 
-// Launches B, C and the map: wants (plus has / subclients where the pass uses them)
-// of the chunk's rows and the live mask launch A left instead of re-reading expiry.
+// Passes B, C and the map: wants (plus has / subclients where the pass uses them)
+// of the chunk's rows and the live mask pass A left instead of re-reading expiry.
 __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials& P, const Chunk& ch,
                                              ChunkRows& r, bool with_sub, bool with_has = false) {
   const double* __restrict__ wb = p.wants + ch.row0;
@@ -551,9 +532,7 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
   }
 }
 
-__global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks,
-                                                 const LargeSeg* __restrict__ ls, Partials P, int32_t* general_list,
-                                                 int32_t* general_count) {
+__global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
   ChunkRows rw;
@@ -581,13 +560,12 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
     }
   }
   P.live[(size_t)blockIdx.x * 256 + threadIdx.x] = (uint8_t)rw.live;
-  // Speculative round 1 (ProportionalShare / FairShare outside learning mode) with
-  // equalShare from the store's running Count.  It is exactly round 1 whenever
-  // Clean releases no subclients of the resource (same eq, same live rows, same
-  // per-chunk summation order); otherwise launch B recomputes it.  Saves launch B's
-  // row reads (12 B per lease) in the steady state.
-  const bool need_tot = !rs.learning && rs.kind >= 2;
-  const bool spec = !p.recompute && need_tot;
+  // Speculative pass B (ProportionalShare / FairShare outside learning mode) with
+  // equalShare from the store's running Count.  It is exactly pass B's result
+  // whenever Clean releases no subclients of the resource (same eq, same live
+  // rows, same per-chunk summation order); k_large_b checks that and recomputes
+  // otherwise.  Saves pass B's row reads (12 B per lease) in the steady state.
+  const bool spec = !p.recompute && !rs.learning && rs.kind >= 2;
   AggB b{0.0, 0.0, 0};
   if (spec) {
     const double eq = rs.C / (double)rs.agg_count;
@@ -617,34 +595,22 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
     if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
     if (spec) b = group_reduce<256>(b, OpB(), lds.b);
   }
-  const int c = blockIdx.x;
   if (threadIdx.x == 0) {
-    if (spec) store_b_partial(P, c, b);
-    st_wt(P.a_cnt + c, (int64_t)a.cnt);
-    st_wt(P.a_cnt_all + c, (int64_t)a.all.cnt);
-    st_wt(P.a_has_all + c, a.all.h);
-    st_wt(P.a_wants_all + c, a.all.w);
-    st_wt(P.a_has + c, a.h);
-    st_wt(P.a_wants + c, a.w);
-    st_wt(P.a_smin + c, (int64_t)a.smin);
-    st_wt(P.a_smax + c, (int64_t)a.smax);
-    st_wt(P.a_nan + c, (int32_t)a.nan);
-  }
-  if (threadIdx.x >= 64) return;
-  const LargeSeg L = ls[ch.lseg];
-  if (!arrive_last(P.arrive + (size_t)ch.lseg * 4 + 0, L.chunk_end - L.chunk_begin)) return;
-  // last chunk of the resource: its totals for the later launches
-  const AggA ta = reduce_a(p, P, L);
-  const AggB tb = spec ? reduce_b(P, L) : AggB{0.0, 0.0, 0};
-  if (threadIdx.x == 0) {
-    const SegState st = seg_state_of(p, ch.seg, ta);
-    SegTot* T = seg_tot(P, ch.lseg);
-    T->a = ta;
-    T->b = tb;
-    T->c = AggC{0.0, 0};
-    T->general = st.general;
-    T->need_b = need_tot && !st.general && !(spec && ta.cnt == 0);
-    if (st.general) general_list[atomicAdd(general_count, 1)] = ch.seg;
+    const int c = blockIdx.x;
+    if (spec) {
+      P.b_x[c] = b.x;
+      P.b_y[c] = b.y;
+      P.b_w[c] = b.i;
+    }
+    P.a_cnt[c] = a.cnt;
+    P.a_cnt_all[c] = a.all.cnt;
+    P.a_has_all[c] = a.all.h;
+    P.a_wants_all[c] = a.all.w;
+    P.a_has[c] = a.h;
+    P.a_wants[c] = a.w;
+    P.a_smin[c] = a.smin;
+    P.a_smax[c] = a.smax;
+    P.a_nan[c] = a.nan;
   }
 }
 
@@ -653,16 +619,18 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
   bool ps;
-  {  // only ProportionalShare / FairShare outside learning mode have a round 1
+  {  // only ProportionalShare / FairShare outside learning mode need this pass
     const ResCfg cf = p.cfg[ch.seg];
     if (cf.learning_end_ns > p.now || cf.kind < 2) return;
     ps = cf.kind == 2;
   }
-  SegTot* T = seg_tot(P, ch.lseg);
-  if (!T->need_b) return;  // launch A's speculative round 1 is exact
+  const LargeSeg L = ls[ch.lseg];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->a = st.a;
+  if (st.general || st.rs.learning || st.rs.kind < 2) return;
+  if (!p.recompute && st.a.cnt == 0) return;  // pass A's speculative partials are exact
   ChunkRows rw;
   load_chunk_w(p, P, ch, rw, ps);
-  const SegState st = seg_state_of(p, ch.seg, T->a);
   const double eq = st.rs.C / (double)st.cl.count;
   if (!ps) {  // FairShare reaches here only with uniform subclients
 #pragma unroll
@@ -674,7 +642,7 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
     if (!(rw.live >> k & 1)) continue;
     const double w = rw.w[k];
     const int s = rw.s[k];
-    if (ps) {
+    if (st.rs.kind == 2) {
       const double e = eq * (double)s;
       if (w < e)
         b.x += e - w;
@@ -689,12 +657,11 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
     }
   }
   b = group_reduce<256>(b, OpB(), lds.b);
-  if (threadIdx.x >= 64) return;
-  if (threadIdx.x == 0) store_b_partial(P, blockIdx.x, b);
-  const LargeSeg L = ls[ch.lseg];
-  if (!arrive_last(P.arrive + (size_t)ch.lseg * 4 + 1, L.chunk_end - L.chunk_begin)) return;
-  const AggB tb = reduce_b(P, L);
-  if (threadIdx.x == 0) T->b = tb;
+  if (threadIdx.x == 0) {
+    P.b_x[blockIdx.x] = b.x;
+    P.b_y[blockIdx.x] = b.y;
+    P.b_w[blockIdx.x] = b.i;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __restrict__ chunks,
@@ -706,38 +673,34 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
     if (cf.learning_end_ns > p.now || cf.kind != 3) return;
   }
   ChunkRows rw;
-  load_chunk_w(p, P, ch, rw, false);  // rows in flight while the totals are read
-  SegTot* T = seg_tot(P, ch.lseg);
-  if (T->general) return;
-  const SegState st = seg_state_of(p, ch.seg, T->a);
-  const AggB b = T->b;
+  load_chunk_w(p, P, ch, rw, false);  // rows in flight while the resource's partials are reduced
+  const LargeSeg L = ls[ch.lseg];
+  const SegState st = seg_state_of(p, L.seg, seg_tot(P, ch.lseg)->a);  // left by pass B
+  if (st.general || st.rs.learning || st.rs.kind != 3) return;
 #pragma unroll
   for (int k = 0; k < kLR; ++k) rw.s[k] = st.a.smin;  // uniform subclients here
+  const AggB b = seg_b<256>(P, L, lds);
+  if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->b = b;
   const double eq = st.rs.C / (double)st.cl.count;
   const double s0 = (double)st.a.smin;
-  const double Tu = (b.x / (double)b.i) * s0 + eq * s0;  // algorithm.go:175,197
+  const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
   AggC c{0.0, 0};
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     if (!(rw.live >> k & 1)) continue;
     const double w = rw.w[k];
     const int s = rw.s[k];
-    if (!(w > (double)s * eq)) continue;  // wantExtraClients (:165-169)
+    if (!(w > (double)s * eq)) continue;
     if (w < Tu)
-      c.ee += Tu - w;  // :197-198
+      c.ee += Tu - w;
     else if (w > Tu)
-      c.sgt += s;  // :199-200
+      c.sgt += s;
   }
   c = group_reduce<256>(c, OpC(), lds.c);
-  if (threadIdx.x >= 64) return;
   if (threadIdx.x == 0) {
-    st_wt(P.c_ee + blockIdx.x, c.ee);
-    st_wt(P.c_sgt + blockIdx.x, (int64_t)c.sgt);
+    P.c_ee[blockIdx.x] = c.ee;
+    P.c_sgt[blockIdx.x] = c.sgt;
   }
-  const LargeSeg L = ls[ch.lseg];
-  if (!arrive_last(P.arrive + (size_t)ch.lseg * 4 + 2, L.chunk_end - L.chunk_begin)) return;
-  const AggC tc = reduce_c(P, L);
-  if (threadIdx.x == 0) T->c = tc;
 }
 
 __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __restrict__ chunks,
@@ -752,15 +715,21 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     fs = !lrn && cf.kind == 3;
   }
   ChunkRows rw;
-  load_chunk_w(p, P, ch, rw, ps, true);  // rows in flight while the totals are read
-  const SegTot* T = seg_tot(P, ch.lseg);
-  if (T->general) return;
-  const SegState st = seg_state_of(p, ch.seg, T->a);
+  load_chunk_w(p, P, ch, rw, ps, true);  // rows in flight while the resource's partials are reduced
+  const LargeSeg L = ls[ch.lseg];
+  // pass A totals: left by pass B for ProportionalShare / FairShare
+  const SegState st = (ps || fs) ? seg_state_of(p, L.seg, seg_tot(P, ch.lseg)->a) : seg_state<256>(p, P, L, lds);
+  if (st.general) return;
   const Res& rs = st.rs;
   const double C = rs.C;
   const double eq = C / (double)st.cl.count;
-  const AggB b = (ps || fs) ? T->b : AggB{0.0, 0.0, 0};
-  const AggC c = fs ? T->c : AggC{0.0, 0};
+  AggB b{0.0, 0.0, 0};
+  AggC c{0.0, 0};
+  if (ps) b = seg_b<256>(P, L, lds);
+  if (fs) {
+    b = seg_tot(P, ch.lseg)->b;  // left by pass C
+    c = seg_c<256>(P, L, lds);
+  }
   const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
   double* gb = p.out_gets + ch.row0;
   int64_t* xb = p.out_expiry + ch.row0;
@@ -798,13 +767,22 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);
-  if (threadIdx.x >= 64) return;
-  if (threadIdx.x == 0) st_wt(P.d_delta + blockIdx.x, delta.v);
-  // the last chunk of the resource writes its record (store sums + safe capacity)
-  const LargeSeg L = ls[ch.lseg];
-  if (!arrive_last(P.arrive + (size_t)ch.lseg * 4 + 3, L.chunk_end - L.chunk_begin)) return;
-  const SumD d = reduce_d(P, L);
-  if (threadIdx.x == 0) write_resource(p, ch.seg, rs, st.cl, d.v);
+  if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
+}
+
+__global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P,
+                                                   int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<256> lds;
+  const LargeSeg L = ls[blockIdx.x];
+  const SegState st = seg_state<256>(p, P, L, lds);
+  if (st.general) {
+    if (threadIdx.x == 0) general_list[atomicAdd(general_count, 1)] = L.seg;
+    return;
+  }
+  SumD d{0.0};
+  for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 256) d.v += P.d_delta[c];
+  d = group_reduce<256>(d, OpSumD(), lds.d);
+  if (threadIdx.x == 0) write_resource(p, L.seg, st.rs, st.cl, d.v);
 }
 
 // --------------------------------------------------------------------------
@@ -1488,8 +1466,12 @@ __global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __
 // (performRequests returns before LoadConfig, server.go:268-272).  A Count that
 // does not fit the root's 32-bit subclients column is rejected the same way
 // (kHierCountRange) instead of being clamped.
-__global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ gathered, uint32_t* status) {
+// The status words are double-buffered by round: this round's words were zeroed by
+// the previous round's launch, and this launch zeroes the next round's (no memset).
+__global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ gathered, uint32_t* status,
+                                uint32_t* zero_next) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < G) zero_next[i] = 0;
   if (i >= R * G) return;
   const double2 v = gathered[i];
   if (!(v.x > 0.0)) return;  // not requested (server.go:241)
@@ -1754,14 +1736,15 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
   return hipGetLastError();
 }
 
-hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
+hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st) {
   if (nchunks <= 0) return hipSuccess;
   switch (phase) {
-    case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, glist, gcount); break;
+    case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
     case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1842,9 +1825,11 @@ hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, hipStream_t st) {
+hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, uint32_t* zero_next,
+                                hipStream_t st) {
   if (R * G <= 0) return hipSuccess;
-  k_hier_validate<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, status);
+  k_hier_validate<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, status,
+                                                                      zero_next);
   return hipGetLastError();
 }
 

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     xw = tk;
   }
   __syncthreads();
-  const int ci = (int)xw;
+  const int ci = __builtin_amdgcn_readfirstlane((int)xw);  // uniform: the chunk record and row bases stay scalar
   const Chunk ch = chunks[ci];
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;

@@ -20,7 +20,7 @@ namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       bool hbm_stream, hipStream_t st);
-hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
+hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
                           hipStream_t st);
@@ -46,7 +46,8 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
 hipError_t launch_decide(const DevParams& p, const ReqItem* items, int nitems, const ReqArgs& q, hipStream_t st);
-hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, hipStream_t st);
+hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, uint32_t* zero_next,
+                                hipStream_t st);
 hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st);
 }  // namespace dm
 
@@ -64,6 +65,7 @@ enum KClass {
   KC_LARGE_B,
   KC_LARGE_C,
   KC_LARGE_MAP,
+  KC_LARGE_FIN,
   KC_GENERAL,
   KC_UPSERT,
   KC_RELEASE,
@@ -73,7 +75,7 @@ enum KClass {
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block256x2",
                                      "block256x4",   "block512x4", "block1024x4", "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
-                                     "large_c",      "large_map",  "general",    "store_upsert",
+                                     "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release", "large_fused"};
 
 template <typename T>
@@ -187,7 +189,6 @@ struct dm_ctx {
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
   DBuf<int32_t> pa_nan;
   DBuf<uint8_t> pa_live, p_tot;
-  DBuf<uint32_t> p_arrive;
   // worklist of resources for k_general (heterogeneous-subclient FairShare)
   DBuf<int32_t> glist, gcount;
   bool maybe_general = false;
@@ -210,7 +211,11 @@ struct dm_ctx {
   DBuf<int64_t> rq_rows, rq_sub, rq_exp;
   DBuf<double> rq_has, rq_wants, rq_gets;
   DBuf<ReqItem> rq_items;
-  DBuf<uint32_t> hier_status;  // dm_hier_root_tick: per-server rejection flags of the last round
+  // dm_hier_root_tick: per-server rejection flags, two rounds' worth (round r uses
+  // words [(r & 1) * kHierMaxServers, +G)); each round zeroes the next round's words
+  DBuf<uint32_t> hier_status;
+  uint32_t hier_round = 0;
+  int hier_status_g = 0;  // G the buffer was last zeroed for
   int hier_servers = 0;
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
@@ -261,7 +266,7 @@ struct dm_ctx {
     d_ferr = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pa_live.release(); p_tot.release(); p_arrive.release();
+    pa_nan.release(); pa_live.release(); p_tot.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
     st_mask.release(); st_blk.release(); st_wpre.release(); st_mwants.release(); st_rel.release();
@@ -429,9 +434,6 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
   DM_HIP(c, c->pa_live.ensure(nc * 256), "partials");
   DM_HIP(c, c->p_tot.ensure(std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes), "partials");
-  DM_HIP(c, c->p_arrive.ensure(std::max<size_t>(c->h_large.size(), 1) * 4), "partials");
-  DM_HIP(c, hipMemsetAsync(c->p_arrive.p, 0, std::max<size_t>(c->h_large.size(), 1) * 4 * sizeof(uint32_t), st),
-         "partials");
   c->n_nonsmall = 0;
   for (int64_t r = 0; r < c->R; ++r)
     if (c->h_seg_off[r + 1] - c->h_seg_off[r] > kSmallMax) ++c->n_nonsmall;
@@ -773,7 +775,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p,
-             c->pa_live.p, c->p_tot.p, c->p_arrive.p};
+             c->pa_live.p, c->p_tot.p};
   hipStream_t st = c->stream;
   auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t {
     if (!c->profiling) return fn();
@@ -819,9 +821,10 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                     [&] { return launch_large_fused(c->fused_G, p, c->fchunks.p, c->flarge.p, F, gl, gc, s_large); }),
            "large-resource kernel");
   } else {
-    for (int ph = 0; ph < 4 && nch > 0; ++ph)
+    const int nls = (int)c->h_large.size();
+    for (int ph = 0; ph < 5 && nch > 0; ++ph)
       DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
-                      [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, P, gl, gc, s_large); }),
+                      [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
   }
   // a store well beyond the Infinity Cache streams from HBM every tick: group
@@ -1402,16 +1405,22 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
   DM_HIP(root, leaf->join_aux(), "join leaf streams");
   leaf->main_dirty = true;
-  DM_HIP(root, root->hier_status.ensure((size_t)n_servers), "hierarchy status");
+  DM_HIP(root, root->hier_status.ensure(2 * (size_t)kHierMaxServers), "hierarchy status");
   root->hier_servers = n_servers;
   const bool same = root->stream == leaf->stream;
   if (!same) {  // root after the leaf's prior work (its config is rewritten)
     DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
     DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
   }
-  DM_HIP(root, hipMemsetAsync(root->hier_status.p, 0, (size_t)n_servers * sizeof(uint32_t), root->stream),
-         "hierarchy status");
-  DM_HIP(root, launch_hier_validate(root->R, n_servers, gathered, root->hier_status.p, root->stream),
+  if (root->hier_status_g != n_servers) {  // first round (or a new server count): both rounds' words
+    DM_HIP(root, hipMemsetAsync(root->hier_status.p, 0, 2 * kHierMaxServers * sizeof(uint32_t), root->stream),
+           "hierarchy status");
+    root->hier_status_g = n_servers;
+  }
+  root->hier_round += 1;
+  uint32_t* status = root->hier_status.p + (root->hier_round & 1) * kHierMaxServers;
+  uint32_t* status_next = root->hier_status.p + ((root->hier_round + 1) & 1) * kHierMaxServers;
+  DM_HIP(root, launch_hier_validate(root->R, n_servers, gathered, status, status_next, root->stream),
          "hierarchy validate");
   DevParams p{};
   p.seg_off = root->seg_off.p;
@@ -1428,7 +1437,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   p.res = root->agg.p;
   p.now = now_ns;
   p.recompute = 0;  // the root's running sums, updated as the reference's Clean + Assigns
-  const HierArgs ha{(const double2*)gathered, root->hier_status.p, leaf->cfg.p, root->R, n_servers, server};
+  const HierArgs ha{(const double2*)gathered, status, leaf->cfg.p, root->R, n_servers, server};
   DM_HIP(root, launch_hier_tick(p, ha, root->stream), "hierarchy root tick");
   if (!same) {  // the leaf's next tick after its new template
     DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
@@ -1446,7 +1455,9 @@ int dm_hier_status(dm_ctx* root, uint32_t* status, int n) {
   if (!status || n < 0) return root->fail(DM_E_INVAL, "bad status buffer");
   if (root->hier_servers == 0) return root->fail(DM_E_STATE, "no dm_hier_root_tick yet");
   if (n != root->hier_servers) return root->fail(DM_E_INVAL, "status buffer must hold one word per server");
-  DM_HIP(root, download(status, (const uint32_t*)root->hier_status.p, 0, n, root->stream), "hierarchy status");
+  DM_HIP(root, download(status, (const uint32_t*)root->hier_status.p + (root->hier_round & 1) * kHierMaxServers, 0, n,
+                        root->stream),
+         "hierarchy status");
   DM_HIP(root, hipStreamSynchronize(root->stream), "hierarchy status");
   int bad = 0;
   for (int g = 0; g < n; ++g) bad += status[g] != 0;

@@ -249,7 +249,7 @@ class Engine:
         self._chk(self._L.dm_publish_totals(self._ctx, ctypes.c_void_p(dev_ptr)))
 
     def set_large_path(self, fused: bool):
-        """Large resources: the four-launch chain (default) or the one-launch path
+        """Large resources: the five-launch chain (default) or the one-launch path
         (DM_LARGE_FUSED, when it fits the device's residency bound)."""
         self._chk(self._L.dm_set_large_path(self._ctx, 1 if fused else 0))
 

@@ -78,7 +78,9 @@ class HierarchicalTick:
         self.gather = gather
         dev = torch.device("cuda", torch.cuda.current_device())
         self.totals = torch.empty((self.R, 2), dtype=torch.float64, device=dev)
-        self.gathered = torch.empty((self.G * self.R, 2), dtype=torch.float64, device=dev)
+        # one server: the all-gather is the identity, so the root reads the totals in place
+        self.gathered = self.totals if self.G == 1 else torch.empty((self.G * self.R, 2), dtype=torch.float64,
+                                                                      device=dev)
         # The library's kernels and torch's collective share ONE stream, so publish ->
         # all-gather -> root -> grants -> leaf tick are ordered without host syncs.  It
         # is a stream of its own: torch's default stream is the HIP null stream, which
@@ -92,8 +94,9 @@ class HierarchicalTick:
         """publish -> all-gather -> the root's round -> this server's new templates."""
         from . import _lib
         self.leaf.publish_totals(self.totals.data_ptr())
-        with self.torch.cuda.stream(self.stream):  # the collective orders with our stream
-            self.gather(self.totals, self.gathered)
+        if self.G > 1:
+            with self.torch.cuda.stream(self.stream):  # the collective orders with our stream
+                self.gather(self.totals, self.gathered)
         L = self.root._L
         _lib.check(L.dm_hier_root_tick(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns),
                                        self.leaf._ctx, self.g), self.root._ctx, L)

@@ -271,10 +271,11 @@ int dm_hier_root_tick(dm_ctx* root, const void* dev_gathered, int n_servers, int
 int dm_hier_status(dm_ctx* root, uint32_t* status, int n_servers);
 
 /* ---- large resources (more than 4096 rows) ----
- * DM_LARGE_CHAIN (default): 2048-row chunks in four stream-ordered launches (Clean
+ * DM_LARGE_CHAIN (default): 2048-row chunks in five stream-ordered launches (Clean
  * + speculative round 1, round 1 again where Clean released subclients, FairShare
- * round 2, the map); each launch's last-arriving chunk of a resource leaves the
- * resource's totals (algorithm.go:156-204, 259-279) for the next.
+ * round 2, the map, the resource records); every chunk re-derives the resource's
+ * totals (algorithm.go:156-204, 259-279) from the previous launch's per-chunk
+ * partials with one fixed tree.
  * DM_LARGE_FUSED: one launch in which every chunk keeps its rows in registers while
  * the chunks of a resource exchange those totals in-launch (one HBM pass); used
  * only when every large resource has at most half as many chunks as the device

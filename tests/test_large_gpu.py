@@ -1,5 +1,5 @@
-"""Large resources (> 4096 rows): the four-launch chain (default; each launch's
-last-arriving chunk leaves the resource's totals for the next) and the one-launch
+"""Large resources (> 4096 rows): the five-launch chain (default; every chunk
+re-derives the resource's totals from the previous launch's partials) and the one-launch
 path (DM_LARGE_FUSED, dm_large.hip: rows resident in VGPRs, totals exchanged
 in-launch) against each other and against the oracle (SURVEY.md §8c bar, with the
 observed error reported).  Each path is deterministic; the two differ only in the
