@@ -73,15 +73,21 @@ def make_workload(name: str, rank: int):
     raise SystemExit(f"unknown workload {name}")
 
 
-LEASE_BYTES = 44  # read wants 8 + has 8 + subclients 4 + expiry 8, write gets 8 + expiry 8
+# A writeback tick (every bench step) reads wants 8 + has 8 + subclients 4 and writes
+# gets 8 per lease: the leases it grants follow their resource's expiry, so no 8-B
+# expiry is read or written per lease.  SURVEY.md section 8(d)'s
+# canonical layout moves 48 B (int64 subclients, expiry read and written per lease).
+LEASE_BYTES = 28
+SURVEY_LEASE_BYTES = 48
+RESOURCE_BYTES = 112  # config 48 B + running sums 32 B read, 32 B written
 
 
 def algorithmic_bytes(n_leases: int, n_resources: int) -> int:
-    # BASELINE.md §3 / SURVEY.md §8(d) per lease: read wants, has, subclients, expiry; write
-    # gets, expiry.  The device table holds subclients as int32 (the boundary already
-    # restricts them to [0, 2^31)), so a lease is 44 B, not the 48 B of an int64 column;
-    # per resource config + offsets + outputs (64 B).  Re-reads are not counted.
-    return LEASE_BYTES * n_leases + 64 * n_resources
+    """Bytes a writeback tick must move with this store layout: per lease read wants,
+    has, subclients (int32: the boundary restricts them to [0, 2^31 - 1)), write gets;
+    per resource the config record and the running sums in and out.  Re-reads are
+    not counted."""
+    return LEASE_BYTES * n_leases + RESOURCE_BYTES * n_resources
 
 
 def kernel_units(snap):
@@ -342,7 +348,12 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
             "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
             "traffic_source": f"profiles/pmc_{workload}.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, calibrated)",
-            "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2),
+            "algorithmic_bytes_per_launch": alg,
+            "bytes_model": (f"{LEASE_BYTES} B per lease (read wants, has, int32 subclients; write gets: granted "
+                            f"leases follow their resource's expiry) + {RESOURCE_BYTES} B per resource; the "
+                            f"canonical layout of SURVEY.md 8(d) moves {SURVEY_LEASE_BYTES} B per lease"),
+            "survey_layout_equivalent_GBs": round((SURVEY_LEASE_BYTES * leases_k + 64 * res_k) / avg_s / 1e9, 1),
+            "avg_launch_us": round(avg_s * 1e6, 2),
             "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
             "timed_region_stream_us_per_step": round(run["stream_ms"] * 1e3 / steps, 2),
             "duration_source": ("HIP event pair around the timed region on the kernel's stream (one kernel "

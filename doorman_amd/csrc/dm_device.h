@@ -7,6 +7,20 @@ namespace dm {
 constexpr int64_t kReleased = INT64_MIN;
 constexpr int64_t kNs = 1000000000LL;
 
+// The subclients column (4 B per lease) also says where a lease's expiry lives:
+//   bit 31 clear         a follower: subclients = the value; its expiry is its
+//                        resource's follow_exp (every lease a writeback tick grants on
+//                        one resource expires at now + lease length, store.go:161),
+//                        so the tick neither reads nor writes an 8-B expiry per lease
+//   kSubReleased         released by Clean / Release: subclients 0, expiry DM_RELEASED
+//   bit 31 set otherwise explicit: subclients = value & 0x7FFFFFFF, expiry in the
+//                        expiry column (rows loaded or upserted by the host)
+// A writeback tick leaves every row a follower or released; the values a lease
+// reads back (dm_read_store / dm_read_leases) are the same either way.
+constexpr uint32_t kSubExplicit = 0x80000000u;
+constexpr uint32_t kSubReleased = 0xFFFFFFFFu;
+constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
+
 // Dispatch bins.  A segment of n rows goes to:
 //   n <= kSmallMax            : wave-packed literal path (many resources per wave)
 //   n <= 16 / 32              : 8- / 16-lane groups, 2 rows per lane, 8 / 4 resources per wave (bins 7, 8)
@@ -74,9 +88,10 @@ struct Partials {
   int64_t* c_sgt;
   // map pass: sum of (gets - has) over live rows
   double* d_delta;
-  // pass A: live-row mask, one byte per thread of each chunk (bit k = row k*256+tid),
-  // so passes B and C read wants (+ subclients for ProportionalShare) and not expiry
-  uint8_t* live;
+  // pass A: per thread of each chunk, bit k (row k*256+tid) of byte 0 = live, byte 1 =
+  // explicit expiry, byte 2 = already marked released; passes B, C and the map read
+  // wants (+ subclients for ProportionalShare) and not expiry
+  uint32_t* live;
   // per large resource (kSegTotBytes each): pass A totals left by pass B's first
   // chunk, pass B totals left by pass C's first chunk, so the map reduces at most
   // one set of partials
@@ -118,7 +133,7 @@ struct RowIndex {
 // store-update validation flags (k_check_rows)
 constexpr uint32_t kUpdRange = 1u;   // row outside [0, N)
 constexpr uint32_t kUpdDup = 2u;     // row twice in one call
-constexpr uint32_t kUpdSub = 4u;     // subclients outside [0, 2^31)
+constexpr uint32_t kUpdSub = 4u;     // subclients outside [0, kSubMax]
 constexpr uint32_t kUpdNaN = 8u;     // NaN wants (FairShare then needs k_general)
 constexpr uint32_t kUpdNotOne = 16u; // subclients != 1 (may make a resource heterogeneous)
 constexpr uint32_t kUpdCount = 32u;  // packed values != set bits of the row mask
@@ -135,12 +150,13 @@ struct ResCfg {
   int32_t refresh_s;        // Algorithm.refresh_interval (seconds; < 2^31, checked at load)
 };
 
-// The store's running sums (store.go:105-111) and the tick's SetSafeCapacity value.
+// The store's running sums (store.go:105-111) and the expiry of the resource's
+// follower rows (SetSafeCapacity's value is derived from count at read time).
 struct ResAgg {
   int64_t count;
   double sum_has;
   double sum_wants;
-  double safe;
+  int64_t follow_exp;
 };
 
 struct DevParams {
@@ -148,7 +164,7 @@ struct DevParams {
   // lease table (SoA).  out_* alias these in writeback mode, so no __restrict__.
   const double* wants;
   const double* has;
-  const int32_t* sub;   // subclients < 2^31 (checked at the boundary): 4 B per lease
+  const int32_t* sub;   // subclients in [0, kSubMax] + the expiry encoding above: 4 B per lease
   const int64_t* expiry;
   const ResCfg* cfg;
   const ResAgg* agg;  // running sums read by the tick (parity mode)
@@ -160,7 +176,7 @@ struct DevParams {
   ResAgg* res;        // per-resource results (== agg in writeback mode)
   int64_t now;
   int32_t recompute;
-  int32_t pad;
+  int32_t writeback;  // rows become followers / released in the store; out_expiry unused
 };
 
 // dm_decide: one resource and its requests [qlo, qhi) (sorted by row)
@@ -181,7 +197,7 @@ struct ReqArgs {
 // dm_hier_root_tick: one exchange round of the hierarchy's root (k_hier_tick)
 constexpr int kHierMaxServers = 64;     // one lane per server row, whole resources per wave
 constexpr uint32_t kHierInvalid = 1u;    // a band with num_clients < 1: InvalidArgument (server.go:863-866)
-constexpr uint32_t kHierCountRange = 2u; // Count >= 2^31: beyond the root's 32-bit subclients column
+constexpr uint32_t kHierCountRange = 2u; // Count > kSubMax: beyond the root's 32-bit subclients column
 struct HierArgs {
   const double2* gathered;  // [G][R] {SumWants, Count as bits} (k_publish records)
   const uint32_t* status;   // [G] k_hier_validate flags; a flagged server requests nothing

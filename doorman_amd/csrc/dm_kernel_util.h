@@ -16,10 +16,9 @@ __device__ __forceinline__ double minF(double l, double r) { return l > r ? r : 
 struct Res {
   int32_t kind;
   int32_t learning;
-  double C;        // Resource.capacity() (resource.go:62-70)
-  double cap_cfg;  // config capacity (SetSafeCapacity, resource.go:92)
-  double safe;
-  int64_t exp_out; // now + lease_length (store.go:161)
+  double C;           // Resource.capacity() (resource.go:62-70)
+  int64_t exp_out;    // now + lease_length (store.go:161)
+  int64_t follow_exp; // the expiry of the resource's follower rows (dm_device.h)
   // the store's running sums, loaded with the config so that no global load
   // waits behind the first reduction's barrier
   long long agg_count;
@@ -32,12 +31,11 @@ __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
   const ResCfg c = p.cfg[seg];
   r.kind = c.kind;
   r.learning = c.learning_end_ns > p.now;  // resource.go:108 learningModeEndTime.After(now)
-  r.cap_cfg = c.capacity;
-  r.C = (c.parent_expiry_ns < p.now) ? 0.0 : r.cap_cfg;  // expiryTime.Before(now)
-  r.safe = c.safe_capacity;
+  r.C = (c.parent_expiry_ns < p.now) ? 0.0 : c.capacity;  // expiryTime.Before(now)
   r.exp_out = p.now + c.lease_len_ns;
+  const ResAgg g = p.agg[seg];
+  r.follow_exp = g.follow_exp;
   if (!p.recompute) {
-    const ResAgg g = p.agg[seg];
     r.agg_count = g.count;
     r.agg_has = g.sum_has;
     r.agg_wants = g.sum_wants;
@@ -289,8 +287,40 @@ __device__ __forceinline__ void write_resource(const DevParams& p, int seg, cons
   r.count = c.count;
   r.sum_wants = c.sum_wants;
   r.sum_has = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
-  r.safe = __builtin_isnan(rs.safe) ? rs.cap_cfg / (double)c.count : rs.safe;  // resource.go:91-95
+  r.follow_exp = p.writeback ? rs.exp_out : rs.follow_exp;  // a writeback tick's leases follow exp_out
   p.res[seg] = r;
+}
+
+// ---- the subclients column's expiry encoding (dm_device.h) ----
+__device__ __forceinline__ int sub_value(int32_t raw) { return (uint32_t)raw == kSubReleased ? 0 : (raw & 0x7FFFFFFF); }
+__device__ __forceinline__ bool sub_released(int32_t raw) { return (uint32_t)raw == kSubReleased; }
+__device__ __forceinline__ bool sub_explicit(int32_t raw) { return raw < 0 && (uint32_t)raw != kSubReleased; }
+// A row's expiry, for kernels off the tick's hot path (one dependent load at most).
+__device__ __forceinline__ int64_t row_expiry(const DevParams& p, int64_t row, int32_t raw, int64_t follow_exp) {
+  return sub_released(raw) ? kReleased : (raw < 0 ? p.expiry[row] : follow_exp);
+}
+// Store a decided live row: its gets, and in a writeback tick it becomes a follower
+// (only an explicit row's subclients word changes); otherwise its expiry.
+__device__ __forceinline__ void put_live(const DevParams& p, int64_t row, double g, const Res& rs, int32_t raw) {
+  __builtin_nontemporal_store(g, p.out_gets + row);
+  if (p.writeback) {
+    if (raw < 0) p.out_sub[row] = raw & 0x7FFFFFFF;
+  } else {
+    __builtin_nontemporal_store((int64_t)rs.exp_out, p.out_expiry + row);
+  }
+}
+// Store a row Clean released: no lease; in a writeback tick the row is zeroed and
+// marked released (once: an already released row is left alone).
+__device__ __forceinline__ void put_released(const DevParams& p, int64_t row, int32_t raw) {
+  __builtin_nontemporal_store(0.0, p.out_gets + row);
+  if (p.writeback) {
+    if (!sub_released(raw)) {
+      p.out_wants[row] = 0.0;
+      p.out_sub[row] = (int32_t)kSubReleased;
+    }
+  } else {
+    __builtin_nontemporal_store((int64_t)kReleased, p.out_expiry + row);
+  }
 }
 
 // FairShare per-row stage (algorithm.go:115-181).  Returns true when the lease is

@@ -39,12 +39,10 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   const double* __restrict__ hb = p.has + lo;
   const int32_t* __restrict__ sb = p.sub + lo;
   const int64_t* __restrict__ eb = p.expiry + lo;
-  double* gb = p.out_gets + lo;
-  int64_t* xb = p.out_expiry + lo;
   // the rows stay in VGPRs for every pass: 6 registers per row
   double w[R], h[R];
-  int s[R];  // subclients < 2^31 (checked by the host at load/upsert)
-  int64_t e[R];
+  int s[R];   // subclients in [0, kSubMax]
+  int sr[R];  // the raw subclients words: where each row's expiry lives (dm_device.h)
   unsigned valid = 0, live = 0;
   // Every load is issued before any is consumed: lanes past the segment end
   // re-read row n-1 (same cache line, n >= 1 in every bin) instead of branching
@@ -57,17 +55,34 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
     w[k] = wb[u];
     h[k] = hb[u];
-    s[k] = sb[u];
-    e[k] = eb[u];
+    sr[k] = sb[u];
     if (BATCH < R && (k + 1) % BATCH == 0 && k + 1 < R) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
+  const Res rs = load_res(p, seg);
+  // Followers expire with their resource; only explicit rows (loaded / upserted by
+  // the host, none after a writeback tick) need their 8-B expiry: a second round
+  // trip for the waves that have one.
+  int64_t e[R];
+  bool any_explicit = false;
+#pragma unroll
+  for (int k = 0; k < R; ++k) any_explicit |= sub_explicit(sr[k]);
+#pragma unroll
+  for (int k = 0; k < R; ++k) e[k] = rs.follow_exp;
+  if (__any(any_explicit)) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = k * G + t;
+      if (sub_explicit(sr[k])) e[k] = eb[(unsigned)(i < n ? i : n - 1)];
+    }
   }
 #pragma unroll
   for (int k = 0; k < R; ++k) {  // rows past the end stay out of valid/live, so every pass skips them
     const unsigned vk = (k * G + t < n) ? 1u : 0u;
     valid |= vk << k;
+    if (sub_released(sr[k])) e[k] = kReleased;
     live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;  // store.go:174 when.After(expiry)
+    s[k] = sub_value(sr[k]);
   }
-  const Res rs = load_res(p, seg);
 
   // ---- pass A: Clean ----
   AggA a = zeroA();
@@ -159,12 +174,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      __builtin_nontemporal_store(0.0, gb + u);
-      __builtin_nontemporal_store((int64_t)(kReleased), xb + u);
-      if (p.out_wants) {
-        p.out_wants[lo + u] = 0.0;
-        p.out_sub[lo + u] = 0;
-      }
+      put_released(p, lo + u, sr[k]);
       continue;
     }
     double g;
@@ -182,8 +192,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     } else {
       g = fs_uniform_row(w[k], h[k], C, cl.sum_has, fu);
     }
-    __builtin_nontemporal_store(g, gb + u);
-    __builtin_nontemporal_store((int64_t)(rs.exp_out), xb + u);
+    put_live(p, lo + u, g, rs, sr[k]);
     delta.v += g - h[k];
   }
 
@@ -247,14 +256,12 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   // rows first (every lane loads; lanes past the pack re-read its last row), so
   // their latency overlaps the segment search and the config gathers
   double w = 0.0, h = 0.0;
-  int s = 0;
-  int64_t e = 0;
+  int sr = 0;  // raw subclients word (expiry encoding, dm_device.h)
+  const int64_t myrow = row0 + (valid ? lane : (nrows > 0 ? nrows - 1 : 0));
   if (nrows > 0) {
-    const int64_t row = row0 + (valid ? lane : nrows - 1);
-    w = p.wants[row];
-    h = p.has[row];
-    s = p.sub[row];
-    e = p.expiry[row];
+    w = p.wants[myrow];
+    h = p.has[myrow];
+    sr = p.sub[myrow];
   }
   // resource of this row: last k < nseg with rel[k] <= lane (offsets relative to row0)
   const int offk = lane <= nseg ? (int)pkr.rel[lane] : INT32_MAX;
@@ -271,7 +278,11 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   const int hi = valid ? seg_hi : 0;
   const int seg = first_seg + k;
   const Res rs = load_res(p, seg);
+  int64_t e = rs.follow_exp;  // followers expire with their resource; explicit rows read theirs
+  if (__any(nrows > 0 && sub_explicit(sr)) && sub_explicit(sr)) e = p.expiry[myrow];
+  if (sub_released(sr)) e = kReleased;
   const int lv = (valid && !(p.now > e)) ? 1 : 0;  // store.go:174
+  int s = sub_value(sr);
   if (!valid) {
     w = 0.0;
     h = 0.0;
@@ -373,17 +384,10 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     if (need2) g = fs_stage2(w, h, s, C, sh, eq, x, wi, T, c);
   }
   if (valid) {
-    if (lv) {
-      __builtin_nontemporal_store(g, p.out_gets + row0 + lane);
-      __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row0 + lane);
-    } else {
-      __builtin_nontemporal_store(0.0, p.out_gets + row0 + lane);
-      __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row0 + lane);
-      if (p.out_wants) {
-        p.out_wants[row0 + lane] = 0.0;
-        p.out_sub[row0 + lane] = 0;
-      }
-    }
+    if (lv)
+      put_live(p, row0 + lane, g, rs, sr);
+    else
+      put_released(p, row0 + lane, sr);
   }
   // per-resource results: lane k (< nseg) owns resource first_seg + k
   const bool owner = lane < nseg;
@@ -398,18 +402,18 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     const int sj = shfl_i(sl, j & 63);
     if (owner && j < ohi && sj >= 0) osh += dj;
   }
-  // SetSafeCapacity inputs from the resource's first row lane (no second config load)
+  // the record's expiries from the resource's first row lane (no second config load)
   Res ors;
-  ors.cap_cfg = shfl_d(rs.cap_cfg, olo & 63);
-  ors.safe = shfl_d(rs.safe, olo & 63);
+  ors.exp_out = shfl_any(rs.exp_out, olo & 63);
+  ors.follow_exp = shfl_any(rs.follow_exp, olo & 63);
   if (owner) {
     const int oseg = first_seg + lane;
     if (olo == ohi) {  // resource without rows
       ocount = p.recompute ? 0 : p.agg[oseg].count;
       osh = p.recompute ? 0.0 : p.agg[oseg].sum_has;
       osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
-      ors.cap_cfg = p.cfg[oseg].capacity;
-      ors.safe = p.cfg[oseg].safe_capacity;
+      ors.exp_out = p.now + p.cfg[oseg].lease_len_ns;
+      ors.follow_exp = p.agg[oseg].follow_exp;
     }
     Clean oc{ocount, osh, osw};
     write_resource(p, oseg, ors, oc, 0.0);
@@ -477,33 +481,51 @@ struct ChunkRows {
   double w[kLR], h[kLR];
   int s[kLR];
   unsigned valid, live;
+  unsigned expl, rel;  // rows whose expiry is explicit / already marked released (dm_device.h)
 };
-__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r) {
+// Pass A: every column of the chunk's rows (loads issued before any is consumed,
+// see group_segment), then liveness from the expiry encoding.
+__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, int64_t follow_exp) {
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;
   const int32_t* __restrict__ sb = p.sub + ch.row0;
   const int64_t* __restrict__ eb = p.expiry + ch.row0;
-  r.valid = 0;
-  r.live = 0;
-  int64_t e[kLR];
-  // loads issued before any is consumed (see group_segment)
+  r.valid = r.live = r.expl = r.rel = 0;
+  int sr[kLR];
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
     const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
     r.w[k] = wb[u];
     r.h[k] = hb[u];
-    r.s[k] = sb[u];
-    e[k] = eb[u];
+    sr[k] = sb[u];
     // two round trips of half the rows: with all 32 loads per lane in flight the
     // vector-memory pipe backs up (64 % of wave time issue-stalled); C2 -3 %
     if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
+  int64_t e[kLR];
+  bool any_explicit = false;
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    e[k] = follow_exp;
+    any_explicit |= sub_explicit(sr[k]);
+  }
+  if (__any(any_explicit)) {
+#pragma unroll
+    for (int k = 0; k < kLR; ++k) {
+      const int i = k * 256 + threadIdx.x;
+      if (sub_explicit(sr[k])) e[k] = eb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+    }
   }
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const unsigned vk = (k * 256 + (int)threadIdx.x < ch.nrows) ? 1u : 0u;
     r.valid |= vk << k;
+    if (sub_released(sr[k])) e[k] = kReleased;
     r.live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;
+    r.expl |= (sub_explicit(sr[k]) ? 1u : 0u) << k;
+    r.rel |= (sub_released(sr[k]) ? 1u : 0u) << k;
+    r.s[k] = sub_value(sr[k]);
   }
 }
 
@@ -515,7 +537,10 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
   const double* __restrict__ hb = p.has + ch.row0;
   const int32_t* __restrict__ sb = p.sub + ch.row0;
   r.valid = 0;
-  r.live = P.live[(size_t)blockIdx.x * 256 + threadIdx.x];
+  const uint32_t m = P.live[(size_t)blockIdx.x * 256 + threadIdx.x];
+  r.live = m & 0xFFu;
+  r.expl = (m >> 8) & 0xFFu;
+  r.rel = (m >> 16) & 0xFFu;
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
@@ -526,7 +551,7 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
       const unsigned u = (unsigned)i;
       r.w[k] = wb[u];
       if (with_has) r.h[k] = hb[u];
-      if (with_sub) r.s[k] = sb[u];
+      if (with_sub) r.s[k] = sub_value(sb[u]);
       r.valid |= 1u << k;
     }
   }
@@ -535,9 +560,9 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
 __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
-  ChunkRows rw;
-  load_chunk(p, ch, rw);
   const Res rs = load_res(p, ch.seg);
+  ChunkRows rw;
+  load_chunk(p, ch, rw, rs.follow_exp);
   AggA a = zeroA();
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
@@ -559,7 +584,7 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
       a.nan |= __builtin_isnan(rw.w[k]) ? 1 : 0;
     }
   }
-  P.live[(size_t)blockIdx.x * 256 + threadIdx.x] = (uint8_t)rw.live;
+  P.live[(size_t)blockIdx.x * 256 + threadIdx.x] = rw.live | rw.expl << 8 | rw.rel << 16;
   // Speculative pass B (ProportionalShare / FairShare outside learning mode) with
   // equalShare from the store's running Count.  It is exactly pass B's result
   // whenever Clean releases no subclients of the resource (same eq, same live
@@ -731,21 +756,14 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     c = seg_c<256>(P, L, lds);
   }
   const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
-  double* gb = p.out_gets + ch.row0;
-  int64_t* xb = p.out_expiry + ch.row0;
   SumD delta{0.0};
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     if (!(rw.valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * 256 + threadIdx.x);
     const double w = rw.w[k], h = rw.h[k];
-    if (!(rw.live >> k & 1)) {
-      __builtin_nontemporal_store(0.0, gb + u);
-      __builtin_nontemporal_store((int64_t)kReleased, xb + u);
-      if (p.out_wants) {
-        p.out_wants[ch.row0 + u] = 0.0;
-        p.out_sub[ch.row0 + u] = 0;
-      }
+    if (!(rw.live >> k & 1)) {  // released by Clean (the raw word for put_released: marked or not)
+      put_released(p, ch.row0 + u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
       continue;
     }
     double g;
@@ -762,8 +780,8 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     } else {
       g = fs_uniform_row(w, h, C, st.cl.sum_has, fu);
     }
-    __builtin_nontemporal_store(g, gb + u);
-    __builtin_nontemporal_store((int64_t)rs.exp_out, xb + u);
+    // an explicit row becomes a follower (its subclients word without the flag)
+    put_live(p, ch.row0 + u, g, rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);
@@ -868,11 +886,15 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
     const int seg = list[idx];
     const int64_t lo = p.seg_off[seg], hi = p.seg_off[seg + 1];
     const Res rs = load_res(p, seg);
+    // liveness and subclients from the expiry encoding (dm_device.h); explicit rows
+    // keep their flag until the last pass, so every pass sees the same live set
+    auto dead = [&](int64_t row) { return p.now > row_expiry(p, row, p.sub[row], rs.follow_exp); };
+    auto sub_at = [&](int64_t row) -> long long { return sub_value(p.sub[row]); };
     AggA a = zeroA();
     for (int64_t row = lo + t; row < hi; row += 256) {
       const double w = p.wants[row], h = p.has[row];
-      const long long s = p.sub[row];
-      const bool lv = !(p.now > p.expiry[row]);
+      const long long s = sub_at(row);
+      const bool lv = !(dead(row));
       if (!lv) {
         a.cnt += s;
         a.h += h;
@@ -895,9 +917,9 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
     // round 1 sums (algorithm.go:156-171)
     AggB b{0.0, 0.0, 0};
     for (int64_t row = lo + t; row < hi; row += 256) {
-      if (p.now > p.expiry[row]) continue;
+      if (dead(row)) continue;
       const double w = p.wants[row];
-      const long long s = p.sub[row];
+      const long long s = sub_at(row);
       const double d = (double)s * eq;
       if (w < d)
         b.x += d - w;
@@ -916,14 +938,9 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
     SumD delta{0.0};
     for (int64_t row = lo + t; row < hi; row += 256) {
       const double w = p.wants[row], h = p.has[row];
-      const long long s = p.sub[row];
-      if (p.now > p.expiry[row]) {
-        __builtin_nontemporal_store(0.0, p.out_gets + row);
-        __builtin_nontemporal_store((int64_t)(kReleased), p.out_expiry + row);
-        if (p.out_wants) {
-          p.out_wants[row] = 0.0;
-          p.out_sub[row] = 0;
-        }
+      const long long s = sub_at(row);
+      if (dead(row)) {
+        put_released(p, row, p.sub[row]);
         continue;
       }
       double g, T = 0.0;
@@ -934,7 +951,7 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
       }
       if (done) {
         __builtin_nontemporal_store(g, p.out_gets + row);
-        __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
+        if (!p.writeback) __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
         delta.v += g - h;
       } else if (!__builtin_isfinite(T)) {
         gs.overflow = 1;  // +-Inf threshold: the per-threshold passes below
@@ -994,9 +1011,9 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         double w = 0.0;
         long long s = 0;
         uint32_t bk = 0xFFFFu;
-        if (row < hi && !(p.now > p.expiry[row])) {
+        if (row < hi && !(dead(row))) {
           w = p.wants[row];
-          s = p.sub[row];
+          s = sub_at(row);
           if (w > (double)s * eq) bk = (uint32_t)gen_bucket(gs.T, K, w);
         }
         const uint32_t key = wave_sort64(bk << 6 | (uint32_t)lane);
@@ -1050,16 +1067,16 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
       }
       __syncthreads();
       for (int64_t row = lo + t; row < hi; row += 256) {
-        if (p.now > p.expiry[row]) continue;
+        if (dead(row)) continue;
         const double w = p.wants[row], h = p.has[row];
-        const long long s = p.sub[row];
+        const long long s = sub_at(row);
         double g, T = 0.0;
         if (fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
         if (__builtin_isnan(T)) continue;  // decided above
         const int k = gen_index(gs.T, K, T);
         g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, AggC{gs.ee[k], gs.sgt[k]});
         __builtin_nontemporal_store(g, p.out_gets + row);
-        __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
+        if (!p.writeback) __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
         delta.v += g - h;
       }
     } else if (!buckets) {
@@ -1072,9 +1089,9 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
       for (;;) {
         TMin tm{0.0, 0, 0};
         for (int64_t row = lo + t; row < hi; row += 256) {
-          if (p.now > p.expiry[row]) continue;
+          if (dead(row)) continue;
           double g, T = 0.0;
-          if (fs_stage01(p.wants[row], p.has[row], p.sub[row], C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
+          if (fs_stage01(p.wants[row], p.has[row], sub_at(row), C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
           if (__builtin_isnan(T) || (have_prev && !(T > prev))) continue;
           tmin_add(tm, T);
         }
@@ -1083,9 +1100,9 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         const double Ts = tm.t;
         AggC c{0.0, 0};
         for (int64_t row = lo + t; row < hi; row += 256) {
-          if (p.now > p.expiry[row]) continue;
+          if (dead(row)) continue;
           const double w = p.wants[row];
-          const long long s = p.sub[row];
+          const long long s = sub_at(row);
           if (!(w > (double)s * eq)) continue;
           if (w < Ts)
             c.ee += Ts - w;
@@ -1094,19 +1111,26 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
         }
         c = group_reduce<256>(c, OpC(), lds.c);
         for (int64_t row = lo + t; row < hi; row += 256) {
-          if (p.now > p.expiry[row]) continue;
+          if (dead(row)) continue;
           const double w = p.wants[row], h = p.has[row];
-          const long long s = p.sub[row];
+          const long long s = sub_at(row);
           double g, T = 0.0;
           if (fs_stage01(w, h, s, C, cl.sum_has, eq, b.x, b.i, &g, &T)) continue;
           if (!(T == Ts)) continue;
           g = fs_stage2(w, h, s, C, cl.sum_has, eq, b.x, b.i, T, c);
           __builtin_nontemporal_store(g, p.out_gets + row);
-          __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
+          if (!p.writeback) __builtin_nontemporal_store((int64_t)(rs.exp_out), p.out_expiry + row);
           delta.v += g - h;
         }
         prev = Ts;
         have_prev = 1;
+      }
+    }
+    if (p.writeback) {  // every live explicit row becomes a follower of the resource's new expiry
+      __syncthreads();
+      for (int64_t row = lo + t; row < hi; row += 256) {
+        const int32_t raw = p.sub[row];
+        if (sub_explicit(raw) && !(p.now > p.expiry[row])) p.out_sub[row] = raw & 0x7FFFFFFF;
       }
     }
     delta = group_reduce<256>(delta, OpSumD(), lds.d);
@@ -1193,7 +1217,7 @@ __global__ void k_check_rows(int64_t n, const int64_t* __restrict__ rows, int64_
     if (wants && __builtin_isnan(wants[i])) f |= kUpdNaN;
     if (sub) {
       const int64_t v = sub[i];
-      if (v < 0 || v > 2147483647LL) f |= kUpdSub;
+      if (v < 0 || v > kSubMax) f |= kUpdSub;
       if (v != 1) f |= kUpdNotOne;
     }
   }
@@ -1229,10 +1253,10 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
     seg = seg_of_row(ix, r);
     dh = has[i] - s_has[r];
     dw = wants[i] - s_wants[r];
-    ds = sub[i] - s_sub[r];
+    ds = sub[i] - sub_value(s_sub[r]);
     s_has[r] = has[i];
     s_wants[r] = wants[i];
-    s_sub[r] = (int32_t)sub[i];  // in [0, 2^31) (k_check_rows)
+    s_sub[r] = (int32_t)((uint32_t)sub[i] | kSubExplicit);  // in [0, kSubMax] (k_check_rows); expiry explicit
     s_exp[r] = expiry[i];
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
@@ -1251,10 +1275,10 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex 
     seg = seg_of_row(ix, r);
     dh = -s_has[r];
     dw = -s_wants[r];
-    ds = -(long long)s_sub[r];
+    ds = -(long long)sub_value(s_sub[r]);
     s_has[r] = 0.0;
     s_wants[r] = 0.0;
-    s_sub[r] = 0;
+    s_sub[r] = (int32_t)kSubReleased;
     s_exp[r] = kReleased;
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
@@ -1435,13 +1459,34 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
 __global__ void k_carry_reject(const uint32_t* __restrict__ from, uint32_t* to) { *to |= *from & kUpdReject; }
 
 // gets / expiry of scattered rows (dm_read_leases_rows)
+// Rows as the store holds them (dm_device.h encoding), for the host: the expiry of
+// row r (a follower's is its resource's follow_exp) and its subclients value.
+// rows == nullptr: rows off .. off+n-1.
+__global__ void k_resolve_rows(int64_t n, const int64_t* __restrict__ rows, int64_t off, const int32_t* __restrict__ sub,
+                               const int64_t* __restrict__ expiry, RowIndex ix, const ResAgg* __restrict__ agg,
+                               int64_t* out_exp, int64_t* out_sub) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows ? rows[i] : off + i;
+  const int32_t raw = sub[r];
+  int64_t e;
+  if (sub_released(raw))
+    e = kReleased;
+  else if (raw < 0)
+    e = expiry[r];
+  else
+    e = agg[seg_of_row(ix, r)].follow_exp;
+  if (out_exp) out_exp[i] = e;
+  if (out_sub) out_sub[i] = sub_value(raw);
+}
+
 __global__ void k_gather_leases(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ gets,
                                 const int64_t* __restrict__ expiry, double* out_gets, int64_t* out_exp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = rows[i];
   out_gets[i] = gets[r];
-  out_exp[i] = expiry[r];
+  if (expiry) out_exp[i] = expiry[r];  // else resolved by k_resolve_rows
 }
 
 // server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
@@ -1478,7 +1523,7 @@ __global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ ga
   const long long count = __double_as_longlong(v.y);
   uint32_t f = 0;
   if (count < 1) f |= kHierInvalid;
-  if (count > 2147483647LL) f |= kHierCountRange;
+  if (count > kSubMax) f |= kHierCountRange;
   if (f) atomicOr(&status[i / R], f);
 }
 
@@ -1517,17 +1562,18 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   int s = 0, rs = 0;
   int64_t e = kReleased;
   bool req = false;
+  const Res rs_cfg = load_res(p, (int)rr);
   if (valid) {
     w = p.wants[row];
     h = p.has[row];
-    s = p.sub[row];
-    e = p.expiry[row];
+    const int32_t raw = p.sub[row];  // expiry encoding (dm_device.h): root rows are explicit or released
+    s = sub_value(raw);
+    e = row_expiry(p, row, raw, rs_cfg.follow_exp);
     const double2 v = ha.gathered[(int64_t)g * ha.R + rr];
-    req = ha.status[g] == 0u && v.x > 0.0;  // count in [1, 2^31) when status is clear
+    req = ha.status[g] == 0u && v.x > 0.0;  // count in [1, kSubMax] when status is clear
     rw = v.x;
     rs = req ? (int)__double_as_longlong(v.y) : 0;
   }
-  const Res rs_cfg = load_res(p, (int)rr);
   const bool released = e == kReleased;
   const bool live = valid && !released && !(p.now > e);     // present after Clean (store.go:174)
   const bool expired = valid && !released && (p.now > e);   // released by this round's Clean
@@ -1642,12 +1688,12 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     if (req) {  // the root store is written in place (out_* alias its columns)
       p.out_gets[row] = gets;
       p.out_wants[row] = rw;
-      p.out_sub[row] = rs;
+      p.out_sub[row] = (int32_t)((uint32_t)rs | kSubExplicit);
       p.out_expiry[row] = exp_new;
     } else if (expired) {
       p.out_gets[row] = 0.0;
       p.out_wants[row] = 0.0;
-      p.out_sub[row] = 0;
+      p.out_sub[row] = (int32_t)kSubReleased;
       p.out_expiry[row] = kReleased;
     }
   }
@@ -1669,7 +1715,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     a.count = count;
     a.sum_has = sh;
     a.sum_wants = sw;
-    a.safe = __builtin_isnan(rs_cfg.safe) ? rs_cfg.cap_cfg / (double)count : rs_cfg.safe;  // resource.go:91-95
+    a.follow_exp = rs_cfg.follow_exp;
     p.res[rr] = a;
   }
 
@@ -1777,6 +1823,14 @@ hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wan
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, ix, s_wants, agg, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_resolve_rows(int64_t n, const int64_t* rows, int64_t off, const int32_t* sub, const int64_t* expiry,
+                               const RowIndex& ix, const ResAgg* agg, int64_t* out_exp, int64_t* out_sub,
+                               hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_resolve_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, off, sub, expiry, ix, agg, out_exp, out_sub);
   return hipGetLastError();
 }
 

@@ -188,30 +188,44 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
   const int32_t* __restrict__ sb = p.sub + ch.row0;
   const int64_t* __restrict__ eb = p.expiry + ch.row0;
   double w[kFR], h[kFR];
-  int s[kFR];
+  int s[kFR], sr[kFR];  // subclients, and the raw words (expiry encoding, dm_device.h)
   unsigned valid = 0, live = 0;
+  const Res rs = load_res(p, ch.seg);
   {
-    int64_t e[kFR];
 #pragma unroll
     for (int k = 0; k < kFR; ++k) {  // every load issued before the first use (dm_kernels.hip, load_chunk)
       const int i = k * G + t;
       const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
       w[k] = wb[u];
       h[k] = hb[u];
-      s[k] = sb[u];
-      e[k] = eb[u];
+      sr[k] = sb[u];
       if (k == kFR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // two round trips of half the rows
+    }
+    int64_t e[kFR];
+    bool any_explicit = false;
+#pragma unroll
+    for (int k = 0; k < kFR; ++k) {
+      e[k] = rs.follow_exp;
+      any_explicit |= sub_explicit(sr[k]);
+    }
+    if (__any(any_explicit)) {
+#pragma unroll
+      for (int k = 0; k < kFR; ++k) {
+        const int i = k * G + t;
+        if (sub_explicit(sr[k])) e[k] = eb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+      }
     }
 #pragma unroll
     for (int k = 0; k < kFR; ++k) {
       const unsigned vk = (k * G + t < ch.nrows) ? 1u : 0u;
       valid |= vk << k;
+      if (sub_released(sr[k])) e[k] = kReleased;
       live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;  // store.go:174
+      s[k] = sub_value(sr[k]);
     }
   }
   const LargeSeg L = ls[ch.lseg];
   const int nch = L.chunk_end - L.chunk_begin;
-  const Res rs = load_res(p, ch.seg);
   uint32_t* sy = F.sync + (size_t)ch.lseg * kFusedSync;  // arrive[0..3]; flags of phase k at sy + flag_at(k)
   uint64_t* prec = F.part + (size_t)ci * kFusedWords;
   uint64_t* trec = F.tot + (size_t)ch.lseg * kFusedWords;
@@ -343,20 +357,13 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
 
   // ---- map: decide and write every lease (store.go:153-167 Assign) ----
   const FsU fu = fs ? make_fsu(eq, st.a.smin, tb.x, tb.i, tc) : FsU{0.0, 0.0, 0.0, 0.0, 0.0};
-  double* gb = p.out_gets + ch.row0;
-  int64_t* xb = p.out_expiry + ch.row0;
   SumD delta{0.0};
 #pragma unroll
   for (int k = 0; k < kFR; ++k) {
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      __builtin_nontemporal_store(0.0, gb + u);
-      __builtin_nontemporal_store((int64_t)kReleased, xb + u);
-      if (p.out_wants) {
-        p.out_wants[ch.row0 + u] = 0.0;
-        p.out_sub[ch.row0 + u] = 0;
-      }
+      put_released(p, ch.row0 + u, sr[k]);
       continue;
     }
     double g;
@@ -374,8 +381,7 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     } else {
       g = fs_uniform_row(w[k], h[k], C, st.cl.sum_has, fu);
     }
-    __builtin_nontemporal_store(g, gb + u);
-    __builtin_nontemporal_store((int64_t)rs.exp_out, xb + u);
+    put_live(p, ch.row0 + u, g, rs, sr[k]);
     delta.v += g - h[k];
   }
   delta = group_reduce<G>(delta, OpSumD(), lds.d);

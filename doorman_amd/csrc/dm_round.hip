@@ -27,8 +27,8 @@ __global__ __launch_bounds__(256) void k_decide(DevParams p, const ReqItem* __re
   // Clean (store.go:169-181): the rows it releases, off the running sums
   AggA a = zeroA();
   for (int64_t j = lo + threadIdx.x; j < hi; j += 256) {
-    if (p.now > p.expiry[j]) {
-      a.cnt += p.sub[j];
+    if (p.now > row_expiry(p, j, p.sub[j], rs.follow_exp)) {
+      a.cnt += sub_value(p.sub[j]);
       a.h += p.has[j];
       a.w += p.wants[j];
     }
@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void k_decide(DevParams p, const ReqItem* __re
     const int64_t row = q.rows[k];
     const double rh = q.has[k], rw = q.wants[k];
     const long long rsub = q.sub[k];
-    const bool self_live = !(p.now > p.expiry[row]);  // HasClient after Clean
+    const bool self_live = !(p.now > row_expiry(p, row, p.sub[row], rs.follow_exp));  // HasClient after Clean
     const double old_h = self_live ? p.has[row] : 0.0;  // store.Get: zero Lease if absent
-    const long long old_s = self_live ? (long long)p.sub[row] : 0;
+    const long long old_s = self_live ? (long long)sub_value(p.sub[row]) : 0;
     double g;
     if (rs.learning) {
       g = rh;  // Learn (algorithm.go:297-302)
@@ -60,10 +60,10 @@ __global__ __launch_bounds__(256) void k_decide(DevParams p, const ReqItem* __re
       } else {
         AggB b{0.0, 0.0, 0};
         for (int64_t j = lo + threadIdx.x; j < hi; j += 256) {  // store.Map (:259-279)
-          if (p.now > p.expiry[j]) continue;
+          if (p.now > row_expiry(p, j, p.sub[j], rs.follow_exp)) continue;
           const bool self = j == row;
           const double wv = self ? rw : p.wants[j];
-          const long long sv = self ? rsub : (long long)p.sub[j];
+          const long long sv = self ? rsub : (long long)sub_value(p.sub[j]);
           const double esp = eq * (double)sv;  // :273
           if (wv < esp)
             b.x += esp - wv;
@@ -83,9 +83,9 @@ __global__ __launch_bounds__(256) void k_decide(DevParams p, const ReqItem* __re
       } else {
         AggB b{0.0, 0.0, 0};
         for (int64_t j = lo + threadIdx.x; j < hi; j += 256) {  // round 1 (:156-171), self skipped
-          if (j == row || p.now > p.expiry[j]) continue;
+          if (j == row || p.now > row_expiry(p, j, p.sub[j], rs.follow_exp)) continue;
           const double wj = p.wants[j];
-          const long long sj = p.sub[j];
+          const long long sj = sub_value(p.sub[j]);
           const double d = (double)sj * eq;  // :160
           if (wj < d)
             b.x += d - wj;
@@ -100,9 +100,9 @@ __global__ __launch_bounds__(256) void k_decide(DevParams p, const ReqItem* __re
           const double T = dE + ds;  // :197
           AggC c{0.0, 0};
           for (int64_t j = lo + threadIdx.x; j < hi; j += 256) {  // round 2 (:192-202)
-            if (j == row || p.now > p.expiry[j]) continue;
+            if (j == row || p.now > row_expiry(p, j, p.sub[j], rs.follow_exp)) continue;
             const double wj = p.wants[j];
-            const long long sj = p.sub[j];
+            const long long sj = sub_value(p.sub[j]);
             if (!(wj > (double)sj * eq)) continue;  // wantExtraClients (:165-169)
             if (wj < T)
               c.ee += T - wj;

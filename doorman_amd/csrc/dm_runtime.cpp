@@ -35,6 +35,9 @@ hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, do
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
                              const int64_t* sub, uint32_t* flags, hipStream_t st);
 hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st);
+hipError_t launch_resolve_rows(int64_t n, const int64_t* rows, int64_t off, const int32_t* sub, const int64_t* expiry,
+                               const RowIndex& ix, const ResAgg* agg, int64_t* out_exp, int64_t* out_sub,
+                               hipStream_t st);
 hipError_t launch_gather_leases(int64_t n, const int64_t* rows, const double* gets, const int64_t* expiry,
                                double* out_gets, int64_t* out_exp, hipStream_t st);
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
@@ -188,7 +191,8 @@ struct dm_ctx {
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
   DBuf<int32_t> pa_nan;
-  DBuf<uint8_t> pa_live, p_tot;
+  DBuf<uint32_t> pa_live;
+  DBuf<uint8_t> p_tot;
   // worklist of resources for k_general (heterogeneous-subclient FairShare)
   DBuf<int32_t> glist, gcount;
   bool maybe_general = false;
@@ -620,8 +624,8 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   for (int64_t r = 0; r < R; ++r)
     if (s->seg_off[r + 1] < s->seg_off[r]) return c->fail(DM_E_INVAL, "seg_off must be non-decreasing");
   for (int64_t i = 0; i < N; ++i)
-    if (s->subclients[i] < 0 || s->subclients[i] > INT32_MAX)
-      return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
+    if (s->subclients[i] < 0 || s->subclients[i] > kSubMax)
+      return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-2]");
   const bool have_agg = s->agg_count && s->agg_sum_has && s->agg_sum_wants;
   if ((s->agg_count || s->agg_sum_has || s->agg_sum_wants) && !have_agg)
     return c->fail(DM_E_INVAL, "give all three running sums or none");
@@ -647,7 +651,9 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_HIP(c, upload(c->has, s->has, (size_t)N, st), "upload has");
   {
     std::vector<int32_t> sub32((size_t)N);
-    for (int64_t i = 0; i < N; ++i) sub32[i] = (int32_t)s->subclients[i];  // range checked above
+    // every loaded row keeps its own expiry (explicit, dm_device.h); a writeback tick
+    // turns the live ones into followers of their resource's expiry
+    for (int64_t i = 0; i < N; ++i) sub32[i] = (int32_t)((uint32_t)s->subclients[i] | kSubExplicit);
     DM_HIP(c, upload(c->sub, sub32.data(), (size_t)N, st), "upload subclients");
     DM_HIP(c, hipStreamSynchronize(st), "upload subclients");  // sub32 leaves scope
   }
@@ -672,7 +678,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     aw = sw.data();
   }
   std::vector<ResAgg> agg(R);
-  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], NAN};
+  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], 0};
   DM_HIP(c, upload(c->agg, agg.data(), (size_t)R, st), "upload running sums");
   build_plan(c);
   int rc = upload_plan(c);
@@ -750,15 +756,22 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     return c->fail(DM_E_INVAL, "DM_WB_INPLACE and DM_WB_ALTERNATE are exclusive");
   const bool pingpong =
       wb && !(flags & DM_WB_INPLACE) && ((flags & DM_WB_ALTERNATE) || c->N * 48 > kStreamBytes);
-  if (!wb || pingpong) {
+  // A writeback tick writes no per-lease expiry: the leases it grants follow their
+  // resource's expiry (dm_device.h), so only gets (and rare subclients words) move.
+  if (!wb) {
     DM_HIP(c, c->out_gets.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_gets");
     DM_HIP(c, c->out_expiry.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_expiry");
     p.out_gets = c->out_gets.p;
     p.out_expiry = c->out_expiry.p;
+  } else if (pingpong) {
+    DM_HIP(c, c->out_gets.ensure((size_t)std::max<int64_t>(c->N, 1)), "alloc out_gets");
+    p.out_gets = c->out_gets.p;
+    p.out_expiry = nullptr;
   } else {
     p.out_gets = c->has.p;
-    p.out_expiry = c->expiry.p;
+    p.out_expiry = nullptr;
   }
+  p.writeback = wb ? 1 : 0;
   if (wb) {
     p.out_wants = c->wants.p;
     p.out_sub = c->sub.p;
@@ -851,10 +864,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     DM_HIP(c, timed(KC_GENERAL, st, [&] { return launch_general(p, gl, gc, blocks, st); }), "general kernel");
     c->main_dirty = true;
   }
-  if (pingpong) {  // the written columns become the store's (stream order keeps later work correct)
-    std::swap(c->has, c->out_gets);
-    std::swap(c->expiry, c->out_expiry);
-  }
+  if (pingpong) std::swap(c->has, c->out_gets);  // the written column becomes the store's (stream order)
   c->last_writeback = wb;
   c->have_result = true;
   if (!(flags & DM_ASYNC)) {
@@ -887,7 +897,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
     const int64_t k = order[(size_t)i], r = rows[k];
     if (r < 0 || r >= c->N) return c->fail(DM_E_RANGE, "request row out of range");
     if (i > 0 && r == srows[(size_t)i - 1]) return c->fail(DM_E_INVAL, "one request per row");
-    if (subclients[k] < 0 || subclients[k] > INT32_MAX) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
+    if (subclients[k] < 0 || subclients[k] > kSubMax) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-2]");
     srows[(size_t)i] = r;
     shas[(size_t)i] = has[k];
     swants[(size_t)i] = wants[k];
@@ -936,10 +946,16 @@ int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* exp
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
-  const double* g = c->last_writeback ? c->has.p : c->out_gets.p;
-  const int64_t* e = c->last_writeback ? c->expiry.p : c->out_expiry.p;
-  DM_HIP(c, download(gets, g, off, n, c->stream), "read gets");
-  DM_HIP(c, download(expiry_ns, e, off, n, c->stream), "read expiry");
+  DM_HIP(c, download(gets, c->last_writeback ? c->has.p : c->out_gets.p, off, n, c->stream), "read gets");
+  if (expiry_ns && c->last_writeback) {  // the store's encoding, resolved on the device
+    DM_HIP(c, c->st_exp.ensure((size_t)std::max<int64_t>(n, 1)), "stage expiry");
+    DM_HIP(c, launch_resolve_rows(n, nullptr, off, c->sub.p, c->expiry.p, c->row_index(), c->agg.p, c->st_exp.p,
+                                  nullptr, c->stream),
+           "resolve expiry");
+    DM_HIP(c, download(expiry_ns, (const int64_t*)c->st_exp.p, 0, n, c->stream), "read expiry");
+  } else {
+    DM_HIP(c, download(expiry_ns, (const int64_t*)c->out_expiry.p, off, n, c->stream), "read expiry");
+  }
   DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
   return DM_OK;
 }
@@ -952,12 +968,16 @@ int dm_read_leases_rows(dm_ctx* c, int64_t n, const int64_t* rows, double* gets,
   for (int64_t i = 0; i < n; ++i)
     if (rows[i] < 0 || rows[i] >= c->N) return c->fail(DM_E_RANGE, "row out of range");
   const double* g = c->last_writeback ? c->has.p : c->out_gets.p;
-  const int64_t* e = c->last_writeback ? c->expiry.p : c->out_expiry.p;
+  const int64_t* e = c->last_writeback ? nullptr : c->out_expiry.p;  // the store's encoding: resolved below
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   DM_HIP(c, c->st_has.ensure((size_t)n), "stage gets");
   DM_HIP(c, c->st_exp.ensure((size_t)n), "stage expiry");
   DM_HIP(c, hipMemcpyAsync(c->st_rows.p, rows, (size_t)n * 8, hipMemcpyHostToDevice, c->stream), "stage rows");
   DM_HIP(c, launch_gather_leases(n, c->st_rows.p, g, e, c->st_has.p, c->st_exp.p, c->stream), "gather leases");
+  if (!e)
+    DM_HIP(c, launch_resolve_rows(n, c->st_rows.p, 0, c->sub.p, c->expiry.p, c->row_index(), c->agg.p, c->st_exp.p,
+                                  nullptr, c->stream),
+           "resolve expiry");
   DM_HIP(c, download(gets, (const double*)c->st_has.p, 0, n, c->stream), "read gets");
   DM_HIP(c, download(expiry_ns, (const int64_t*)c->st_exp.p, 0, n, c->stream), "read expiry");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
@@ -1007,13 +1027,17 @@ int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* 
   if (safe && !c->have_result) return c->fail(DM_E_STATE, "safe capacity needs a dm_apportion result");
   const bool wb = !c->have_result || c->last_writeback;
   std::vector<ResAgg> v(n > 0 ? n : 0);
+  std::vector<ResCfg> cf(safe && n > 0 ? n : 0);
   DM_HIP(c, download(v.data(), (const ResAgg*)(wb ? c->agg.p : c->res.p), r0, n, c->stream), "read resources");
+  // the device config: a hierarchy exchange rewrites a leaf's templates (dm_hier_root_tick)
+  if (safe) DM_HIP(c, download(cf.data(), (const ResCfg*)c->cfg.p, r0, n, c->stream), "read config");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read resources");
   for (int64_t i = 0; i < n; ++i) {
     if (count) count[i] = v[i].count;
     if (sum_has) sum_has[i] = v[i].sum_has;
     if (sum_wants) sum_wants[i] = v[i].sum_wants;
-    if (safe) safe[i] = v[i].safe;
+    // SetSafeCapacity (resource.go:81-96) after the tick's Clean: configured, or capacity / Count
+    if (safe) safe[i] = std::isnan(cf[i].safe_capacity) ? cf[i].capacity / (double)v[i].count : cf[i].safe_capacity;
   }
   return DM_OK;
 }
@@ -1047,11 +1071,16 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
   if (rc) return rc;
   DM_HIP(c, download(has, (const double*)c->has.p, off, n, c->stream), "read has");
   DM_HIP(c, download(wants, (const double*)c->wants.p, off, n, c->stream), "read wants");
-  std::vector<int32_t> sub32(sub ? (size_t)n : 0);
-  DM_HIP(c, download(sub ? sub32.data() : nullptr, (const int32_t*)c->sub.p, off, n, c->stream), "read sub");
-  DM_HIP(c, download(exp, (const int64_t*)c->expiry.p, off, n, c->stream), "read expiry");
+  if ((sub || exp) && n > 0) {  // subclients and expiry from the column encoding (dm_device.h)
+    DM_HIP(c, c->st_exp.ensure((size_t)n), "stage expiry");
+    DM_HIP(c, c->st_sub.ensure((size_t)n), "stage subclients");
+    DM_HIP(c, launch_resolve_rows(n, nullptr, off, c->sub.p, c->expiry.p, c->row_index(), c->agg.p,
+                                  exp ? c->st_exp.p : nullptr, sub ? c->st_sub.p : nullptr, c->stream),
+           "resolve rows");
+    DM_HIP(c, download(exp, (const int64_t*)c->st_exp.p, 0, n, c->stream), "read expiry");
+    DM_HIP(c, download(sub, (const int64_t*)c->st_sub.p, 0, n, c->stream), "read subclients");
+  }
   DM_HIP(c, hipStreamSynchronize(c->stream), "read store");
-  for (int64_t i = 0; sub && i < n; ++i) sub[i] = sub32[i];
   return DM_OK;
 }
 
@@ -1112,7 +1141,7 @@ static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
   *flags_out = f;
   if (f & kUpdRange) return c->fail(DM_E_RANGE, "row out of range");
   if (f & kUpdDup) return c->fail(DM_E_INVAL, "rows must be unique within one call");
-  if (f & kUpdSub) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-1]");
+  if (f & kUpdSub) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-2]");
   return DM_OK;
 }
 
@@ -1327,7 +1356,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     if (f & kUpdRange) return c->fail(DM_E_RANGE, p + ": row out of range");
     if (f & kUpdCount) return c->fail(DM_E_INVAL, p + ": packed values must match the mask's set bits");
     if (f & kUpdDup) return c->fail(DM_E_INVAL, p + ": rows must be unique within one part");
-    return c->fail(DM_E_INVAL, p + ": subclients must be in [0, 2^31-1]");
+    return c->fail(DM_E_INVAL, p + ": subclients must be in [0, 2^31-2]");
   };
   if (f0 & kUpdReject) return reject(f0, "wants refresh");
   if (f0 & kUpdNaN) c->maybe_general = true;

@@ -217,8 +217,8 @@ int dm_server_get_capacity(dm_server* s, const char* client, const char* resourc
   if (!s || !client || !resource || !ticket) return DM_E_INVAL;
   auto it = s->res_index.find(resource);
   if (it == s->res_index.end()) return s->fail(DM_E_RANGE, std::string("unknown resource ") + resource);
-  if (subclients < 1 || subclients > INT32_MAX)
-    return s->fail(DM_E_ARGUMENT, "subclients must be in [1, 2^31) (server.go:863-866)");
+  if (subclients < 1 || subclients > 2147483646LL)  // the store's column holds [0, 2^31 - 2] (dm_device.h)
+    return s->fail(DM_E_ARGUMENT, "subclients must be in [1, 2^31 - 1) (server.go:863-866)");
   *ticket = (int64_t)s->pending.size();
   s->pending.push_back(Req{it->second, client, has, wants, subclients});
   return DM_OK;

@@ -220,6 +220,13 @@ class Engine:
         self._chk(self._L.dm_read_leases(self._ctx, off, n, _ptr(gets), _ptr(exp)))
         return gets, exp
 
+    def leases_rows(self, rows):
+        """dm_read_leases_rows: the last tick's leases of scattered rows (gathered on the device)."""
+        rows = _c(rows, np.int64)
+        gets, exp = np.empty(len(rows)), np.empty(len(rows), np.int64)
+        self._chk(self._L.dm_read_leases_rows(self._ctx, len(rows), _ptr(rows), _ptr(gets), _ptr(exp)))
+        return gets, exp
+
     def leases_proto(self, off: int = 0, n: int | None = None):
         n = self.n_leases - off if n is None else n
         cap, exp, ref = np.empty(n), np.empty(n, np.int64), np.empty(n, np.int64)

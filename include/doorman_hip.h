@@ -86,7 +86,7 @@ typedef struct {
   const int64_t* seg_off;    /* [R+1] resource r owns rows [seg_off[r], seg_off[r+1]) */
   const double* wants;       /* [N] Lease.Wants */
   const double* has;         /* [N] Lease.Has */
-  const int64_t* subclients; /* [N] Lease.Subclients, 0 <= v < 2^31 (DM_E_INVAL otherwise) */
+  const int64_t* subclients; /* [N] Lease.Subclients, 0 <= v < 2^31 - 1 (DM_E_INVAL otherwise) */
   const int64_t* expiry_ns;  /* [N] Lease.Expiry, unix ns */
   const int64_t* agg_count;  /* [R] or NULL: store.count     (running sum; NULL = recompute) */
   const double* agg_sum_has; /* [R] or NULL: store.sumHas */
@@ -173,7 +173,7 @@ int dm_store_release(dm_ctx* ctx, int64_t n, const int64_t* rows);
    and later ones are not applied.  Synchronous on return, like the single calls. */
 int dm_store_apply(dm_ctx* ctx, const dm_store_batch* batch);
 /* The three update calls validate on the device (rows in [0, N), unique within the
- * call, subclients in [0, 2^31)); a rejected call (DM_E_RANGE / DM_E_INVAL) leaves the
+ * call, subclients in [0, 2^31 - 1)); a rejected call (DM_E_RANGE / DM_E_INVAL) leaves the
  * store untouched.  They return after the update is applied, so the caller may reuse
  * its buffers.  Buffers from dm_host_alloc (page-locked) go over PCIe by DMA at full
  * rate; ordinary host memory is staged by the HIP runtime. */
@@ -201,7 +201,7 @@ int dm_apportion(dm_ctx* ctx, int64_t now_ns, uint32_t flags);
  * request's own has (Learn), wants and subclients for its client and the stored
  * rows for everyone else (algorithm.go:115,126,148,157,263-269).  gets[k] and
  * expiry_ns[k] (now + lease length) are the leases; the store is not changed --
- * Assign them with dm_store_upsert.  Rows unique; subclients in [0, 2^31).
+ * Assign them with dm_store_upsert.  Rows unique; subclients in [0, 2^31 - 1).
  * Synchronous. */
 int dm_decide(dm_ctx* ctx, int64_t now_ns, int64_t n, const int64_t* rows, const double* has, const double* wants,
               const int64_t* subclients, double* gets, int64_t* expiry_ns);
@@ -242,7 +242,7 @@ int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
  *   - Server g requests resource r when its SumWants > 0 (server.go:241): has 0
  *     (Has is never filled, :244/:873), wants = SumWants, subclients = Count.
  *     A band with Count < 1 makes the root reject server g's whole request
- *     (codes.InvalidArgument, :863-866); Count >= 2^31 (beyond the root's 32-bit
+ *     (codes.InvalidArgument, :863-866); Count >= 2^31 - 1 (beyond the root's 32-bit
  *     subclients column) is rejected the same way.  A rejected server requests
  *     nothing this round and its leaf keeps its templates (:268-272); see
  *     dm_hier_status.

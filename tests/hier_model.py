@@ -87,7 +87,7 @@ def server_request(sum_wants, count):
     (:858-868): None when some band has num_clients < 1 (InvalidArgument), and --
     this build's limit -- when a Count does not fit the root's 32-bit column."""
     req = {r: (float(sum_wants[r]), int(count[r])) for r in range(len(sum_wants)) if sum_wants[r] > 0}
-    if any(c < 1 or c > 2**31 - 1 for _, c in req.values()):
+    if any(c < 1 or c > 2**31 - 2 for _, c in req.values()):  # the device column's bound (include/doorman_hip.h)
         return None
     return req
 

@@ -673,3 +673,46 @@ def test_store_apply_stops_at_the_first_rejected_part(eng):
     st = eng.read_store()
     for k in ("has", "wants", "subclients", "expiry_ns"):
         assert st[k].tobytes() == before[k].tobytes(), k
+
+
+@pytest.mark.parametrize("cols", ["inplace", "alternate"])
+def test_follower_expiry_encoding(eng, cols):
+    """A writeback tick leaves every lease a follower of its resource's expiry (only
+    gets move per lease, include/doorman_hip.h): followers expire together when no
+    tick refreshes them, rows upserted in between keep their own expiry, released
+    rows stay released; leases, the store read back and the next ticks match the
+    oracle on a host copy that stores every expiry explicitly."""
+    rng = np.random.default_rng(91)
+    sizes = binned_sizes(rng, per_bin=2)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(0, 1, 2, 3), expired_frac=0.05, learning_frac=0.1)
+    snap["lease_length_s"] = np.where(rng.random(len(sizes)) < 0.5, 10, 400).astype(np.int64)
+    eng.load(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    N = len(host["wants"])
+    for rnd, dt in enumerate([0, 5, 25, 30, 31]):  # the 10-s resources' followers lapse at +25
+        now = NOW + dt * W.NS
+        if rnd == 3:  # explicit rows between ticks: refreshed leases with their own expiry
+            rows = np.sort(rng.choice(N, N // 20, replace=False))
+            nw = rng.uniform(0.0, 2.0, len(rows))
+            ne = now + rng.integers(-3, 60, len(rows)) * W.NS
+            eng.upsert(rows, np.zeros(len(rows)), nw, np.ones(len(rows), np.int64), ne)
+            host["wants"][rows], host["has"][rows], host["subclients"][rows], host["expiry_ns"][rows] = nw, 0.0, 1, ne
+            W.add_store_sums(host)
+        eng.apportion(now, writeback=True, wb_columns=cols)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now)
+        assert_leases_match(host, gets, exp, ref, f"tick {rnd}")
+        live = ref["expiry_ns"] != W.RELEASED
+        host["has"] = np.where(live, ref["gets"], 0.0)
+        host["wants"] = np.where(live, host["wants"], 0.0)
+        host["subclients"] = np.where(live, host["subclients"], 0)
+        host["expiry_ns"] = ref["expiry_ns"].copy()
+        W.add_store_sums(host)
+        st = eng.read_store()
+        np.testing.assert_array_equal(st["expiry_ns"], host["expiry_ns"], err_msg=f"tick {rnd}")
+        np.testing.assert_array_equal(st["subclients"], host["subclients"], err_msg=f"tick {rnd}")
+        assert st["has"].tobytes() == gets.tobytes()
+        rows = np.sort(rng.choice(N, 64, replace=False))  # the scattered-row read (server path)
+        g2, e2 = eng.leases_rows(rows)
+        np.testing.assert_array_equal(e2, exp[rows])
+        assert g2.tobytes() == gets[rows].tobytes()
