@@ -157,6 +157,9 @@ struct ResAgg {
   double sum_has;
   double sum_wants;
   int64_t follow_exp;
+  int32_t explicit_rows;  // 1: some row may carry an explicit expiry (loaded, upserted,
+                          // hierarchy-written); 0 after a writeback tick (every row follows)
+  int32_t pad;
 };
 
 struct DevParams {

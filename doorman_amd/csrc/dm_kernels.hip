@@ -24,11 +24,7 @@ namespace dm {
 // Resource-per-group kernel: G threads (a wave or a 256-thread workgroup) own
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
-// BATCH = row-blocks whose loads share one memory round trip (R: all at once).
-// All at once wins while repeated ticks are partly served by the Infinity Cache
-// (C1, 480 MB: +14%); on a store that streams from HBM (C3, 4.8 GB) two
-// round trips of half the requests each are ~10% faster (tools/ab.py).
-template <int G, int R, int BATCH>
+template <int G, int R>
 __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, int t, Lds<G>& lds,
                                               int32_t* general_list, int32_t* general_count) {
   const int seg = wi.seg;
@@ -56,23 +52,21 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     w[k] = wb[u];
     h[k] = hb[u];
     sr[k] = sb[u];
-    if (BATCH < R && (k + 1) % BATCH == 0 && k + 1 < R) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
   const Res rs = load_res(p, seg);
-  // Followers expire with their resource; only explicit rows (loaded / upserted by
-  // the host, none after a writeback tick) need their 8-B expiry: a second round
-  // trip for the waves that have one.
+  // Followers expire with their resource; only a resource whose rows may carry an
+  // explicit expiry (loaded / upserted by the host, none after a writeback tick)
+  // reads the 8-B expiry column.  The test is the resource's flag, not the rows'
+  // subclients words, which would make every wave wait for its loads to decide.
   int64_t e[R];
-  bool any_explicit = false;
-#pragma unroll
-  for (int k = 0; k < R; ++k) any_explicit |= sub_explicit(sr[k]);
 #pragma unroll
   for (int k = 0; k < R; ++k) e[k] = rs.follow_exp;
-  if (__any(any_explicit)) {
+  if (rs.any_expl) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
-      if (sub_explicit(sr[k])) e[k] = eb[(unsigned)(i < n ? i : n - 1)];
+      const int64_t x = eb[(unsigned)(i < n ? i : n - 1)];
+      if (sub_explicit(sr[k])) e[k] = x;
     }
   }
 #pragma unroll
@@ -201,23 +195,23 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
 }
 
 // One G-thread workgroup per resource (G = 256..1024, R <= 4 rows per thread).
-template <int G, int R, int BATCH = R>
+template <int G, int R>
 __global__ __launch_bounds__(G) void k_block(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nitems) return;
-  group_segment<G, R, BATCH>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
+  group_segment<G, R>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
 }
 
 // One wave per resource (n <= 64 R), four independent waves per workgroup: wave
 // reductions only (DPP, no barriers), four resources in flight per workgroup.
-template <int R, int BATCH = R>
+template <int R>
 __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                               int32_t* general_list, int32_t* general_count) {
   Lds<64> lds;  // unused by wave reductions
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nitems) return;
-  group_segment<64, R, BATCH>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
+  group_segment<64, R>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
 }
 
 // Sub-wave groups: G = 16 or 32 lanes own one resource of up to G*R rows (R rows
@@ -232,7 +226,7 @@ __global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __rest
   Lds<G> lds;  // unused by sub-wave reductions
   const int i = blockIdx.x * (256 / G) + (int)(threadIdx.x / G);
   if (i >= nitems) return;  // whole groups only: reductions never cross a group
-  group_segment<G, R, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
+  group_segment<G, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -279,7 +273,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   const int seg = first_seg + k;
   const Res rs = load_res(p, seg);
   int64_t e = rs.follow_exp;  // followers expire with their resource; explicit rows read theirs
-  if (__any(nrows > 0 && sub_explicit(sr)) && sub_explicit(sr)) e = p.expiry[myrow];
+  if (__any(nrows > 0 && rs.any_expl) && rs.any_expl && sub_explicit(sr)) e = p.expiry[myrow];
   if (sub_released(sr)) e = kReleased;
   const int lv = (valid && !(p.now > e)) ? 1 : 0;  // store.go:174
   int s = sub_value(sr);
@@ -406,6 +400,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   Res ors;
   ors.exp_out = shfl_any(rs.exp_out, olo & 63);
   ors.follow_exp = shfl_any(rs.follow_exp, olo & 63);
+  ors.any_expl = shfl_i(rs.any_expl, olo & 63);
   if (owner) {
     const int oseg = first_seg + lane;
     if (olo == ohi) {  // resource without rows
@@ -414,6 +409,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
       osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
       ors.exp_out = p.now + p.cfg[oseg].lease_len_ns;
       ors.follow_exp = p.agg[oseg].follow_exp;
+      ors.any_expl = p.agg[oseg].explicit_rows;
     }
     Clean oc{ocount, osh, osw};
     write_resource(p, oseg, ors, oc, 0.0);
@@ -485,7 +481,7 @@ struct ChunkRows {
 };
 // Pass A: every column of the chunk's rows (loads issued before any is consumed,
 // see group_segment), then liveness from the expiry encoding.
-__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, int64_t follow_exp) {
+__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, const Res& rs) {
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;
   const int32_t* __restrict__ sb = p.sub + ch.row0;
@@ -504,17 +500,14 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
   int64_t e[kLR];
-  bool any_explicit = false;
 #pragma unroll
-  for (int k = 0; k < kLR; ++k) {
-    e[k] = follow_exp;
-    any_explicit |= sub_explicit(sr[k]);
-  }
-  if (__any(any_explicit)) {
+  for (int k = 0; k < kLR; ++k) e[k] = rs.follow_exp;
+  if (rs.any_expl) {  // the resource's flag (see group_segment)
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
       const int i = k * 256 + threadIdx.x;
-      if (sub_explicit(sr[k])) e[k] = eb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+      const int64_t x = eb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+      if (sub_explicit(sr[k])) e[k] = x;
     }
   }
 #pragma unroll
@@ -562,7 +555,7 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
   const Chunk ch = chunks[blockIdx.x];
   const Res rs = load_res(p, ch.seg);
   ChunkRows rw;
-  load_chunk(p, ch, rw, rs.follow_exp);
+  load_chunk(p, ch, rw, rs);
   AggA a = zeroA();
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
@@ -1258,6 +1251,7 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
     s_wants[r] = wants[i];
     s_sub[r] = (int32_t)((uint32_t)sub[i] | kSubExplicit);  // in [0, kSubMax] (k_check_rows); expiry explicit
     s_exp[r] = expiry[i];
+    agg[seg].explicit_rows = 1;  // the tick reads this resource's expiry column again
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
@@ -1716,6 +1710,8 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     a.sum_has = sh;
     a.sum_wants = sw;
     a.follow_exp = rs_cfg.follow_exp;
+    a.explicit_rows = 1;  // the rows this tick writes carry explicit expiries
+    a.pad = 0;
     p.res[rr] = a;
   }
 
@@ -1752,29 +1748,17 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
 }
 
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
-                      bool hbm_stream, hipStream_t st) {
+                      hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const unsigned wg4 = (unsigned)((n + 3) / 4);
   switch (bin) {
     case 0: k_sub<16, 4><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 1: k_sub<32, 4><<<(unsigned)((n + 7) / 8), 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 2:
-      if (hbm_stream) k_wave<4, 2><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount);
-      else k_wave<4><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount);
-      break;
+    case 2: k_wave<4><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 3: k_block<256, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 4:
-      if (hbm_stream) k_block<256, 4, 2><<<n, 256, 0, st>>>(p, segs, n, glist, gcount);
-      else k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount);
-      break;
-    case 5:
-      if (hbm_stream) k_block<512, 4, 2><<<n, 512, 0, st>>>(p, segs, n, glist, gcount);
-      else k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount);
-      break;
-    case 6:
-      if (hbm_stream) k_block<1024, 4, 2><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
-      else k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount);
-      break;
+    case 4: k_block<256, 4><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 5: k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 6: k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount); break;
     case 7: k_sub<8, 2><<<(unsigned)((n + 31) / 32), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 8: k_sub<16, 2><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;

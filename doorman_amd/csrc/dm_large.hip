@@ -202,17 +202,14 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
       if (k == kFR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // two round trips of half the rows
     }
     int64_t e[kFR];
-    bool any_explicit = false;
 #pragma unroll
-    for (int k = 0; k < kFR; ++k) {
-      e[k] = rs.follow_exp;
-      any_explicit |= sub_explicit(sr[k]);
-    }
-    if (__any(any_explicit)) {
+    for (int k = 0; k < kFR; ++k) e[k] = rs.follow_exp;
+    if (rs.any_expl) {  // the resource's flag (dm_kernels.hip, group_segment)
 #pragma unroll
       for (int k = 0; k < kFR; ++k) {
         const int i = k * G + t;
-        if (sub_explicit(sr[k])) e[k] = eb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+        const int64_t x = eb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+        if (sub_explicit(sr[k])) e[k] = x;
       }
     }
 #pragma unroll

@@ -19,7 +19,7 @@
 namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
-                      bool hbm_stream, hipStream_t st);
+                      hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
@@ -678,7 +678,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     aw = sw.data();
   }
   std::vector<ResAgg> agg(R);
-  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], 0};
+  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], 0, 1, 0};  // loaded rows carry explicit expiries
   DM_HIP(c, upload(c->agg, agg.data(), (size_t)R, st), "upload running sums");
   build_plan(c);
   int rc = upload_plan(c);
@@ -840,14 +840,11 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                       [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
   }
-  // a store well beyond the Infinity Cache streams from HBM every tick: group
-  // kernels then keep half their row loads in flight (dm_kernels.hip, BATCH)
-  const bool hbm_stream = c->N * 48 > kStreamBytes;
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
     hipStream_t s = cls_stream(b);
-    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, hbm_stream, s); }),
+    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }),
            "group kernel");
   }
   if (!c->h_packs.empty())

@@ -1,6 +1,6 @@
 """Interleaved A/B timing of library builds in ONE process (cdna guide §5.4 rule 24).
 
-  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:fused] ...
+  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:fused|:inplace|:alternate] ...
 
 Every build gets its own context with the same snapshot; rounds alternate between
 builds; per build the per-launch kernel time (HIP events) and the tick wall time
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--workload", default="c1")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--per-kernel", action="store_true", help="median us per tick of every kernel class")
     args = ap.parse_args()
     snap = make_workload(args.workload, 0)
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
@@ -37,11 +38,12 @@ def main():
         e = Engine(0, os.path.abspath(path))
         if mode.startswith("fused"):
             e.set_large_path(fused=True)
+        e.wb_columns = mode if mode in ("inplace", "alternate") else "auto"
         e.load(snap)
         for _ in range(3):
-            e.apportion(W.NOW_NS, writeback=True)
+            e.apportion(W.NOW_NS, writeback=True, wb_columns=e.wb_columns)
         engines.append(e)
-    res = {p: {"tick_us": [], "kern_us": [], "plain_us": []} for p in args.libs}
+    res = {p: {"tick_us": [], "kern_us": [], "plain_us": [], "cls": {}} for p in args.libs}
     for _ in range(args.rounds):
         for p, e in zip(args.libs, engines):
             e.set_profiling(True)
@@ -49,7 +51,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+                e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True, wb_columns=e.wb_columns)
             e.sync()
             dt = time.perf_counter() - t0
             kt = e.kernel_times()
@@ -58,10 +60,12 @@ def main():
             torch.cuda.synchronize()  # the same ticks without per-kernel events
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+                e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True, wb_columns=e.wb_columns)
             e.sync()
             res[p]["plain_us"].append((time.perf_counter() - t0) / args.steps * 1e6)
             res[p]["kern_us"].append(sum(v[1] for v in kt.values()) / args.steps * 1e3)
+            for name, v in kt.items():
+                res[p]["cls"].setdefault(name, []).append(v[1] / args.steps * 1e3)
     alg = algorithmic_bytes(N, R)
     for p in args.libs:
         k = res[p]["kern_us"]
@@ -69,6 +73,8 @@ def main():
         print(f"{os.path.basename(p):34s} kernel med {statistics.median(k):8.2f} us min {min(k):8.2f} "
               f"({alg / min(k) / 1e3:7.1f} GB/s best) | tick med {statistics.median(t):8.2f} us | "
               f"unprofiled tick med {statistics.median(res[p]['plain_us']):8.2f} min {min(res[p]['plain_us']):8.2f} us")
+        if args.per_kernel:
+            print("    " + "  ".join(f"{n} {statistics.median(v):.1f}" for n, v in sorted(res[p]["cls"].items())))
     for e in engines:
         e.close()
 
