@@ -479,8 +479,10 @@ struct ChunkRows {
   unsigned valid, live;
   unsigned expl, rel;  // rows whose expiry is explicit / already marked released (dm_device.h)
 };
-// Pass A: every column of the chunk's rows (loads issued before any is consumed,
-// see group_segment), then liveness from the expiry encoding.
+// Pass A: wants and subclients of the chunk's rows (loads issued before any is
+// consumed, see group_segment), liveness from the expiry encoding, then has for
+// the rows Clean releases only (every row in recompute mode): the steady state
+// reads 12 of a lease's 20 bytes here (C2: 122 -> 73 MB per tick).
 __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, const Res& rs) {
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;
@@ -493,10 +495,9 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     const int i = k * 256 + threadIdx.x;
     const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
     r.w[k] = wb[u];
-    r.h[k] = hb[u];
     sr[k] = sb[u];
-    // two round trips of half the rows: with all 32 loads per lane in flight the
-    // vector-memory pipe backs up (64 % of wave time issue-stalled); C2 -3 %
+    r.h[k] = 0.0;
+    // two round trips of half the rows (C2 tick 163 -> 157 us, tools/ab.py)
     if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   }
   int64_t e[kLR];
@@ -519,6 +520,12 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     r.expl |= (sub_explicit(sr[k]) ? 1u : 0u) << k;
     r.rel |= (sub_released(sr[k]) ? 1u : 0u) << k;
     r.s[k] = sub_value(sr[k]);
+  }
+  const unsigned need_h = p.recompute ? r.valid : (r.valid & ~r.live);
+  if (__any(need_h != 0)) {
+#pragma unroll
+    for (int k = 0; k < kLR; ++k)
+      if (need_h >> k & 1) r.h[k] = hb[(unsigned)(k * 256 + threadIdx.x)];
   }
 }
 

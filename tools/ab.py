@@ -1,12 +1,13 @@
 """Interleaved A/B timing of library builds in ONE process (cdna guide §5.4 rule 24).
 
-  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:fused|:inplace|:alternate] ...
+  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:fused|:inplace|:alternate][@VAR=value,...] ...
 
 Every build gets its own context with the same snapshot; rounds alternate between
 builds; per build the per-launch kernel time (HIP events) and the tick wall time
 are reported as median and min over rounds.
 """
 import argparse
+import contextlib
 import os
 import statistics
 import sys
@@ -22,6 +23,21 @@ from doorman_amd import workloads as W  # noqa: E402
 from doorman_amd.engine import Engine  # noqa: E402
 
 
+@contextlib.contextmanager
+def env(values):
+    """Environment variables in force for one engine's calls (A/B knobs)."""
+    saved = {k: os.environ.get(k) for k in values}
+    os.environ.update(values)
+    try:
+        yield
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
@@ -34,38 +50,47 @@ def main():
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
     engines = []
     for p in args.libs:  # LIB.so:fused = the same build with the large-resource chain forced
-        path, _, mode = p.partition(":")
-        e = Engine(0, os.path.abspath(path))
+        spec, _, envs = p.partition("@")  # LIB[:mode][@VAR=value,...]: environment at the engine's creation
+        path, _, mode = spec.partition(":")
+        e_env = dict(kv.partition("=")[::2] for kv in filter(None, envs.split(",")))
+        with env(e_env):
+            e = Engine(0, os.path.abspath(path))
+        e.env = e_env  # also in force around its ticks (knobs read per launch)
         if mode.startswith("fused"):
             e.set_large_path(fused=True)
         e.wb_columns = mode if mode in ("inplace", "alternate") else "auto"
         e.load(snap)
-        for _ in range(3):
-            e.apportion(W.NOW_NS, writeback=True, wb_columns=e.wb_columns)
+        with env(e.env):
+            for _ in range(3):
+                e.apportion(W.NOW_NS, writeback=True, wb_columns=e.wb_columns)
         engines.append(e)
     res = {p: {"tick_us": [], "kern_us": [], "plain_us": [], "cls": {}} for p in args.libs}
+    def one_round(p, e):
+        e.set_profiling(True)
+        e.reset_kernel_times()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True, wb_columns=e.wb_columns)
+        e.sync()
+        dt = time.perf_counter() - t0
+        kt = e.kernel_times()
+        e.set_profiling(False)
+        res[p]["tick_us"].append(dt / args.steps * 1e6)
+        torch.cuda.synchronize()  # the same ticks without per-kernel events
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True, wb_columns=e.wb_columns)
+        e.sync()
+        res[p]["plain_us"].append((time.perf_counter() - t0) / args.steps * 1e6)
+        res[p]["kern_us"].append(sum(v[1] for v in kt.values()) / args.steps * 1e3)
+        for name, v in kt.items():
+            res[p]["cls"].setdefault(name, []).append(v[1] / args.steps * 1e3)
+
     for _ in range(args.rounds):
         for p, e in zip(args.libs, engines):
-            e.set_profiling(True)
-            e.reset_kernel_times()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True, wb_columns=e.wb_columns)
-            e.sync()
-            dt = time.perf_counter() - t0
-            kt = e.kernel_times()
-            e.set_profiling(False)
-            res[p]["tick_us"].append(dt / args.steps * 1e6)
-            torch.cuda.synchronize()  # the same ticks without per-kernel events
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True, wb_columns=e.wb_columns)
-            e.sync()
-            res[p]["plain_us"].append((time.perf_counter() - t0) / args.steps * 1e6)
-            res[p]["kern_us"].append(sum(v[1] for v in kt.values()) / args.steps * 1e3)
-            for name, v in kt.items():
-                res[p]["cls"].setdefault(name, []).append(v[1] / args.steps * 1e3)
+            with env(e.env):
+                one_round(p, e)
     alg = algorithmic_bytes(N, R)
     for p in args.libs:
         k = res[p]["kern_us"]
