@@ -60,6 +60,21 @@ __device__ __forceinline__ T shfl_any(const T& v, int lane) {
   return r;
 }
 
+// A value every lane holds identically (an LDS broadcast, a combine of readlanes),
+// moved to SGPRs: uniform values that stay in VGPRs through a kernel's later
+// passes cost a register per dword per lane and with it occupancy.
+template <typename T>
+__device__ __forceinline__ T uniform(const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "4-byte granular");
+  int src[sizeof(T) / 4], dst[sizeof(T) / 4];
+  __builtin_memcpy(src, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = __builtin_amdgcn_readfirstlane(src[i]);
+  T r;
+  __builtin_memcpy(&r, dst, sizeof(T));
+  return r;
+}
+
 // DPP lane permute of every dword of v (a VALU operand modifier: no LDS trip).
 template <int CTRL, typename T>
 __device__ __forceinline__ T dpp_any(const T& v) {
@@ -139,7 +154,7 @@ __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
       r = op(r, x);
     }
     if constexpr (REUSE) __syncthreads();
-    return r;
+    return uniform(r);
   }
 }
 
@@ -303,27 +318,42 @@ __device__ __forceinline__ bool sub_explicit(int32_t raw) { return raw < 0 && (u
 __device__ __forceinline__ int64_t row_expiry(const DevParams& p, int64_t row, int32_t raw, int64_t follow_exp) {
   return sub_released(raw) ? kReleased : (raw < 0 ? p.expiry[row] : follow_exp);
 }
-// Store a decided live row: its gets, and in a writeback tick it becomes a follower
-// (only an explicit row's subclients word changes); otherwise its expiry.
-__device__ __forceinline__ void put_live(const DevParams& p, int64_t row, double g, const Res& rs, int32_t raw) {
-  __builtin_nontemporal_store(g, p.out_gets + row);
+// Element i of a column from a wave-uniform base: a 32-bit byte offset, so the
+// access can take the scalar-base form (one offset VGPR shared by every column of
+// the same width instead of a 64-bit address per column and row).  i * sizeof(T)
+// must fit 32 bits (rows within one resource or chunk).
+template <typename T>
+__device__ __forceinline__ T* col_at(T* base, uint32_t i) {
+  return (T*)((char*)base + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+template <typename T>
+__device__ __forceinline__ const T* col_at(const T* base, uint32_t i) {
+  return (const T*)((const char*)base + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+
+// Store a decided live row (row0 + i; row0 wave-uniform where the caller can): its
+// gets, and in a writeback tick it becomes a follower (only an explicit row's
+// subclients word changes); otherwise its expiry.
+__device__ __forceinline__ void put_live(const DevParams& p, int64_t row0, uint32_t i, double g, const Res& rs,
+                                         int32_t raw) {
+  __builtin_nontemporal_store(g, col_at(p.out_gets + row0, i));
   if (p.writeback) {
-    if (raw < 0) p.out_sub[row] = raw & 0x7FFFFFFF;
+    if (raw < 0) *col_at(p.out_sub + row0, i) = raw & 0x7FFFFFFF;
   } else {
-    __builtin_nontemporal_store((int64_t)rs.exp_out, p.out_expiry + row);
+    __builtin_nontemporal_store((int64_t)rs.exp_out, col_at(p.out_expiry + row0, i));
   }
 }
 // Store a row Clean released: no lease; in a writeback tick the row is zeroed and
 // marked released (once: an already released row is left alone).
-__device__ __forceinline__ void put_released(const DevParams& p, int64_t row, int32_t raw) {
-  __builtin_nontemporal_store(0.0, p.out_gets + row);
+__device__ __forceinline__ void put_released(const DevParams& p, int64_t row0, uint32_t i, int32_t raw) {
+  __builtin_nontemporal_store(0.0, col_at(p.out_gets + row0, i));
   if (p.writeback) {
     if (!sub_released(raw)) {
-      p.out_wants[row] = 0.0;
-      p.out_sub[row] = (int32_t)kSubReleased;
+      *col_at(p.out_wants + row0, i) = 0.0;
+      *col_at(p.out_sub + row0, i) = (int32_t)kSubReleased;
     }
   } else {
-    __builtin_nontemporal_store((int64_t)kReleased, p.out_expiry + row);
+    __builtin_nontemporal_store((int64_t)kReleased, col_at(p.out_expiry + row0, i));
   }
 }
 

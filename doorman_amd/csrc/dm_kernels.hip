@@ -49,9 +49,9 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     const int i = k * G + t;
     const unsigned u = (unsigned)(i < n ? i : n - 1);
     // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
-    w[k] = wb[u];
-    h[k] = hb[u];
-    sr[k] = sb[u];
+    w[k] = *col_at(wb, u);
+    h[k] = *col_at(hb, u);
+    sr[k] = *col_at(sb, u);
   }
   const Res rs = load_res(p, seg);
   // Followers expire with their resource; only a resource whose rows may carry an
@@ -65,7 +65,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
-      const int64_t x = eb[(unsigned)(i < n ? i : n - 1)];
+      const int64_t x = *col_at(eb, (unsigned)(i < n ? i : n - 1));
       if (sub_explicit(sr[k])) e[k] = x;
     }
   }
@@ -168,7 +168,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      put_released(p, lo + u, sr[k]);
+      put_released(p, lo, u, sr[k]);
       continue;
     }
     double g;
@@ -186,7 +186,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     } else {
       g = fs_uniform_row(w[k], h[k], C, cl.sum_has, fu);
     }
-    put_live(p, lo + u, g, rs, sr[k]);
+    put_live(p, lo, u, g, rs, sr[k]);
     delta.v += g - h[k];
   }
 
@@ -379,9 +379,9 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   }
   if (valid) {
     if (lv)
-      put_live(p, row0 + lane, g, rs, sr);
+      put_live(p, row0, (uint32_t)lane, g, rs, sr);
     else
-      put_released(p, row0 + lane, sr);
+      put_released(p, row0, (uint32_t)lane, sr);
   }
   // per-resource results: lane k (< nseg) owns resource first_seg + k
   const bool owner = lane < nseg;
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     const unsigned u = (unsigned)(k * 256 + threadIdx.x);
     const double w = rw.w[k], h = rw.h[k];
     if (!(rw.live >> k & 1)) {  // released by Clean (the raw word for put_released: marked or not)
-      put_released(p, ch.row0 + u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
+      put_released(p, ch.row0, u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
       continue;
     }
     double g;
@@ -781,7 +781,7 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
       g = fs_uniform_row(w, h, C, st.cl.sum_has, fu);
     }
     // an explicit row becomes a follower (its subclients word without the flag)
-    put_live(p, ch.row0 + u, g, rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
+    put_live(p, ch.row0, u, g, rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
       const double w = p.wants[row], h = p.has[row];
       const long long s = sub_at(row);
       if (dead(row)) {
-        put_released(p, row, p.sub[row]);
+        put_released(p, row, 0u, p.sub[row]);
         continue;
       }
       double g, T = 0.0;

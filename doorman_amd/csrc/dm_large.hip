@@ -360,7 +360,7 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      put_released(p, ch.row0 + u, sr[k]);
+      put_released(p, ch.row0, u, sr[k]);
       continue;
     }
     double g;
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     } else {
       g = fs_uniform_row(w[k], h[k], C, st.cl.sum_has, fu);
     }
-    put_live(p, ch.row0 + u, g, rs, sr[k]);
+    put_live(p, ch.row0, u, g, rs, sr[k]);
     delta.v += g - h[k];
   }
   delta = group_reduce<G>(delta, OpSumD(), lds.d);
