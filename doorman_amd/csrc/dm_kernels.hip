@@ -159,6 +159,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     }
     cu = group_reduce<G, AggC, OpC, false>(cu, OpC(), lds.c);
     fu = make_fsu(eq, a.smin, b.x, b.i, cu);
+    if constexpr (G >= 64) fu = uniform(fu);  // one resource per wave or workgroup: SGPRs
   }
 
   // ---- map: decide and write every lease (store.go:153-167 Assign) ----
@@ -541,18 +542,27 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
   r.live = m & 0xFFu;
   r.expl = (m >> 8) & 0xFFu;
   r.rel = (m >> 16) & 0xFFu;
+  // every load issued before any is consumed (lanes past the chunk re-read its last
+  // row, see group_segment): loads inside a per-lane branch made the compiler wait
+  // for each row-block before issuing the next, eight memory latencies per chunk
+  const int n = ch.nrows;
+  int sr[kLR];
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
-    r.w[k] = 0.0;
-    r.h[k] = 0.0;
-    r.s[k] = 0;
-    if (i < ch.nrows) {
-      const unsigned u = (unsigned)i;
-      r.w[k] = wb[u];
-      if (with_has) r.h[k] = hb[u];
-      if (with_sub) r.s[k] = sub_value(sb[u]);
-      r.valid |= 1u << k;
+    const unsigned u = (unsigned)(i < n ? i : n - 1);
+    r.w[k] = *col_at(wb, u);
+    r.h[k] = with_has ? *col_at(hb, u) : 0.0;
+    sr[k] = with_sub ? *col_at(sb, u) : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    const bool v = k * 256 + (int)threadIdx.x < n;
+    r.valid |= (v ? 1u : 0u) << k;
+    r.s[k] = v ? sub_value(sr[k]) : 0;
+    if (!v) {
+      r.w[k] = 0.0;
+      r.h[k] = 0.0;
     }
   }
 }
@@ -743,7 +753,8 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   load_chunk_w(p, P, ch, rw, ps, true);  // rows in flight while the resource's partials are reduced
   const LargeSeg L = ls[ch.lseg];
   // pass A totals: left by pass B for ProportionalShare / FairShare
-  const SegState st = (ps || fs) ? seg_state_of(p, L.seg, seg_tot(P, ch.lseg)->a) : seg_state<256>(p, P, L, lds);
+  const SegState st =
+      uniform((ps || fs) ? seg_state_of(p, L.seg, seg_tot(P, ch.lseg)->a) : seg_state<256>(p, P, L, lds));
   if (st.general) return;
   const Res& rs = st.rs;
   const double C = rs.C;
@@ -755,7 +766,8 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     b = seg_tot(P, ch.lseg)->b;  // left by pass C
     c = seg_c<256>(P, L, lds);
   }
-  const FsU fu = make_fsu(eq, st.a.smin, b.x, b.i, c);
+  b = uniform(b);  // the resource's totals stay in SGPRs through the map
+  const FsU fu = uniform(make_fsu(eq, st.a.smin, b.x, b.i, c));  // SGPRs through the map
   SumD delta{0.0};
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {

@@ -526,6 +526,13 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
     for (int i = 0; i < kNumBins + 2 && sp[i] >= '0' && sp[i] < '0' + dm_ctx::kAux; ++i) c->class_stream[i] = sp[i] - '0';
+  if (const char* sk = getenv("DM_STREAM_SKEW")) {  // A/B probe: plain streams created (and kept) first
+    static std::vector<hipStream_t> skew;
+    for (int i = 0; i < atoi(sk); ++i) {
+      hipStream_t x = nullptr;
+      if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) == hipSuccess) skew.push_back(x);
+    }
+  }
   e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -533,8 +540,20 @@ int dm_create(int device, dm_ctx** out) {
     return DM_E_HIP;
   }
   c->stream = c->own_stream;
+  // The auxiliary streams are created with a full CU mask, which gives each its own
+  // hardware queue.  Plain streams share the process's GPU_MAX_HW_QUEUES (4) queues
+  // round robin with every other stream of the process (torch's included), so which
+  // work classes ended up serialised behind one queue depended on how many streams
+  // existed before: C2 tick 147-179 us by creation order, 147-151 us with the masks
+  // (tools/host_cost.py, one process per run).  DM_CUMASK=0 restores plain streams.
+  const bool cumask = !getenv("DM_CUMASK") || atoi(getenv("DM_CUMASK")) != 0;
+  int ncu = 0;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0u);
+  for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
   for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
-    e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
+    e = cumask ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mask.size(), mask.data())
+               : hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
