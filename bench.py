@@ -79,7 +79,7 @@ def make_workload(name: str, rank: int):
 # canonical layout moves 48 B (int64 subclients, expiry read and written per lease).
 LEASE_BYTES = 28
 SURVEY_LEASE_BYTES = 48
-RESOURCE_BYTES = 128  # config 48 B + running sums and follower expiry 40 B read, 40 B written
+RESOURCE_BYTES = 97  # config 32 B + running sums and follower expiry 32 B read and written + explicit flag 1 B
 
 
 def algorithmic_bytes(n_leases: int, n_resources: int) -> int:

@@ -140,26 +140,28 @@ constexpr uint32_t kUpdCount = 32u;  // packed values != set bits of the row mas
 constexpr uint32_t kUpdReject = kUpdRange | kUpdDup | kUpdSub | kUpdCount;
 
 // Per-resource configuration, AoS (one scalar burst per resource).
-struct ResCfg {
+struct ResCfg {  // what every tick reads: 32 B
   double capacity;          // ResourceTemplate.capacity
-  double safe_capacity;     // NaN = unset (resource.go:91)
-  int64_t lease_len_ns;     // Algorithm.lease_length * 1e9
   int64_t learning_end_ns;  // learningModeEndTime
   int64_t parent_expiry_ns; // Resource.expiryTime (INT64_MAX = nil)
+  int32_t lease_len_s;      // Algorithm.lease_length (seconds, < 2^31, checked at load)
   int32_t kind;             // pb.Algorithm.Kind
+};
+struct ResCold {  // what only the readers and the hierarchy touch: 16 B
+  double safe_capacity;     // NaN = unset (resource.go:91)
   int32_t refresh_s;        // Algorithm.refresh_interval (seconds; < 2^31, checked at load)
+  int32_t pad;
 };
 
 // The store's running sums (store.go:105-111) and the expiry of the resource's
 // follower rows (SetSafeCapacity's value is derived from count at read time).
-struct ResAgg {
+// Whether any row of the resource may carry an explicit expiry is a separate byte
+// per resource (DevParams::expl), written only when it changes.
+struct ResAgg {  // 32 B, read and written by every tick
   int64_t count;
   double sum_has;
   double sum_wants;
   int64_t follow_exp;
-  int32_t explicit_rows;  // 1: some row may carry an explicit expiry (loaded, upserted,
-                          // hierarchy-written); 0 after a writeback tick (every row follows)
-  int32_t pad;
 };
 
 struct DevParams {
@@ -177,6 +179,8 @@ struct DevParams {
   double* out_wants;  // writeback only: released rows zeroed (else nullptr)
   int32_t* out_sub;   // writeback only
   ResAgg* res;        // per-resource results (== agg in writeback mode)
+  uint8_t* expl;      // [R] 1: some row may carry an explicit expiry (loaded, upserted,
+                      // hierarchy-written); a writeback tick clears it (every row follows)
   int64_t now;
   int32_t recompute;
   int32_t writeback;  // rows become followers / released in the store; out_expiry unused
@@ -205,6 +209,8 @@ struct HierArgs {
   const double2* gathered;  // [G][R] {SumWants, Count as bits} (k_publish records)
   const uint32_t* status;   // [G] k_hier_validate flags; a flagged server requests nothing
   ResCfg* leaf_cfg;         // this server's leaf template
+  ResCold* leaf_cold;       // ... its safe capacity and refresh interval
+  const ResCold* root_cold; // the root's
   int64_t R;
   int G;
   int server;

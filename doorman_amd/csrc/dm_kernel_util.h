@@ -19,7 +19,7 @@ struct Res {
   double C;           // Resource.capacity() (resource.go:62-70)
   int64_t exp_out;    // now + lease_length (store.go:161)
   int64_t follow_exp; // the expiry of the resource's follower rows (dm_device.h)
-  int32_t any_expl;   // ResAgg::explicit_rows: wave-uniform, so no row's expiry load waits on its subclients word
+  int32_t any_expl;   // DevParams::expl: wave-uniform, so no row's expiry load waits on its subclients word
   // the store's running sums, loaded with the config so that no global load
   // waits behind the first reduction's barrier
   long long agg_count;
@@ -33,10 +33,10 @@ __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
   r.kind = c.kind;
   r.learning = c.learning_end_ns > p.now;  // resource.go:108 learningModeEndTime.After(now)
   r.C = (c.parent_expiry_ns < p.now) ? 0.0 : c.capacity;  // expiryTime.Before(now)
-  r.exp_out = p.now + c.lease_len_ns;
+  r.exp_out = p.now + (int64_t)c.lease_len_s * kNs;
   const ResAgg g = p.agg[seg];
   r.follow_exp = g.follow_exp;
-  r.any_expl = g.explicit_rows;
+  r.any_expl = p.expl[seg];
   if (!p.recompute) {
     r.agg_count = g.count;
     r.agg_has = g.sum_has;
@@ -305,9 +305,8 @@ __device__ __forceinline__ void write_resource(const DevParams& p, int seg, cons
   r.sum_wants = c.sum_wants;
   r.sum_has = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
   r.follow_exp = p.writeback ? rs.exp_out : rs.follow_exp;  // a writeback tick's leases follow exp_out
-  r.explicit_rows = p.writeback ? 0 : rs.any_expl;            // ... and none keeps an explicit expiry
-  r.pad = 0;
   p.res[seg] = r;
+  if (p.writeback && rs.any_expl) p.expl[seg] = 0;  // ... and none keeps an explicit expiry
 }
 
 // ---- the subclients column's expiry encoding (dm_device.h) ----

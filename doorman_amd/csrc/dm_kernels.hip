@@ -408,9 +408,9 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
       ocount = p.recompute ? 0 : p.agg[oseg].count;
       osh = p.recompute ? 0.0 : p.agg[oseg].sum_has;
       osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
-      ors.exp_out = p.now + p.cfg[oseg].lease_len_ns;
+      ors.exp_out = p.now + (int64_t)p.cfg[oseg].lease_len_s * kNs;
       ors.follow_exp = p.agg[oseg].follow_exp;
-      ors.any_expl = p.agg[oseg].explicit_rows;
+      ors.any_expl = p.expl[oseg];
     }
     Clean oc{ocount, osh, osw};
     write_resource(p, oseg, ors, oc, 0.0);
@@ -1253,7 +1253,7 @@ __global__ void k_clear_rows(int64_t n, const int64_t* __restrict__ rows, int64_
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
                          const int64_t* __restrict__ expiry, RowIndex ix, double* s_has, double* s_wants,
-                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags) {
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (*flags & kUpdReject) return;  // uniform over the grid
   const bool active = i < n;
@@ -1270,7 +1270,7 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
     s_wants[r] = wants[i];
     s_sub[r] = (int32_t)((uint32_t)sub[i] | kSubExplicit);  // in [0, kSubMax] (k_check_rows); expiry explicit
     s_exp[r] = expiry[i];
-    agg[seg].explicit_rows = 1;  // the tick reads this resource's expiry column again
+    expl[seg] = 1;  // the tick reads this resource's expiry column again
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
@@ -1729,28 +1729,29 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     a.sum_has = sh;
     a.sum_wants = sw;
     a.follow_exp = rs_cfg.follow_exp;
-    a.explicit_rows = 1;  // the rows this tick writes carry explicit expiries
-    a.pad = 0;
     p.res[rr] = a;
+    p.expl[rr] = 1;  // the rows this tick writes carry explicit expiries
   }
 
   // this server's new template for the resource (server.go:279-313)
   if (valid && g == ha.server && ha.status[g] == 0u) {
     ResCfg* c = ha.leaf_cfg + rr;
+    ResCold* cc = ha.leaf_cold + rr;
     if (req) {
       const ResCfg rc = p.cfg[rr];
+      const ResCold rcc = ha.root_cold[rr];
       const int64_t sec = exp_new >= 0 ? exp_new / kNs : -((-exp_new + kNs - 1) / kNs);  // time.Unix(sec, 0)
       c->capacity = gets;                                                  // :293
-      c->safe_capacity = __builtin_isnan(rc.safe_capacity) ? 0.0 : rc.safe_capacity;  // :294, :894
-      c->lease_len_ns = rc.lease_len_ns;                                   // :295 Algorithm
-      c->refresh_s = rc.refresh_s;
+      cc->safe_capacity = __builtin_isnan(rcc.safe_capacity) ? 0.0 : rcc.safe_capacity;  // :294, :894
+      c->lease_len_s = rc.lease_len_s;                                     // :295 Algorithm
+      cc->refresh_s = rcc.refresh_s;
       c->kind = rc.kind;
       c->parent_expiry_ns = sec * kNs;                                     // :287-288
     } else {  // the "*" default template (server.go:53-63, :305)
       c->capacity = 0.0;
-      c->safe_capacity = 0.0;
-      c->lease_len_ns = 20 * kNs;
-      c->refresh_s = 1;
+      cc->safe_capacity = 0.0;
+      c->lease_len_s = 20;
+      cc->refresh_s = 1;
       c->kind = 3;
       c->parent_expiry_ns = INT64_MAX;  // expiryTimes has no entry: nil
     }
@@ -1808,10 +1809,11 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
-                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                         hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, ix, s_has, s_wants, s_sub,
-                                                        s_exp, agg, flags);
+                                                        s_exp, agg, expl, flags);
   return hipGetLastError();
 }
 

@@ -29,7 +29,8 @@ hipError_t launch_large_fused(int G, const DevParams& p, const Chunk* chunks, co
 hipError_t large_fused_occupancy(int G, int* blocks_per_cu);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
-                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                         hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
                           int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
@@ -136,10 +137,12 @@ struct dm_ctx {
   DBuf<double> wants, has;
   DBuf<int32_t> sub;  // subclients, 4 B per lease on the device (the ABI carries int64)
   DBuf<int64_t> expiry;
-  // running sums (+ the last writeback tick's safe capacity), AoS
+  // running sums + the followers' expiry, AoS (32 B)
   DBuf<ResAgg> agg;
-  // config, AoS
+  DBuf<uint8_t> expl;  // per resource: rows may carry explicit expiries (DevParams::expl)
+  // config, AoS: what every tick reads (32 B), and the rest (safe capacity, refresh)
   DBuf<ResCfg> cfg;
+  DBuf<ResCold> cold;
   // outputs of a non-writeback tick
   DBuf<double> out_gets;
   DBuf<int64_t> out_expiry;
@@ -261,7 +264,7 @@ struct dm_ctx {
   }
   void free_all() {
     seg_off.release(); blk_seg.release(); wants.release(); has.release(); sub.release(); expiry.release();
-    agg.release(); cfg.release();
+    agg.release(); expl.release(); cfg.release(); cold.release();
     out_gets.release(); out_expiry.release(); res.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
     fchunks.release(); flarge.release(); f_ticket.release(); f_sync.release(); f_part.release(); f_tot.release();
@@ -525,7 +528,11 @@ int dm_create(int device, dm_ctx** out) {
   c->device = device;
   if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
-    for (int i = 0; i < kNumBins + 2 && sp[i] >= '0' && sp[i] < '0' + dm_ctx::kAux; ++i) c->class_stream[i] = sp[i] - '0';
+    for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
+      const int d = sp[i] >= 'a' ? sp[i] - 'a' + 10 : sp[i] - '0';
+      if (d < 0 || d >= dm_ctx::kAux) break;
+      c->class_stream[i] = d;
+    }
   if (const char* sk = getenv("DM_STREAM_SKEW")) {  // A/B probe: plain streams created (and kept) first
     static std::vector<hipStream_t> skew;
     for (int i = 0; i < atoi(sk); ++i) {
@@ -697,8 +704,10 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     aw = sw.data();
   }
   std::vector<ResAgg> agg(R);
-  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], 0, 1, 0};  // loaded rows carry explicit expiries
+  for (int64_t r = 0; r < R; ++r) agg[r] = ResAgg{ac[r], ah[r], aw[r], 0};
   DM_HIP(c, upload(c->agg, agg.data(), (size_t)R, st), "upload running sums");
+  const std::vector<uint8_t> expl((size_t)std::max<int64_t>(R, 1), 1);  // loaded rows carry explicit expiries
+  DM_HIP(c, upload(c->expl, expl.data(), expl.size(), st), "upload explicit flags");
   build_plan(c);
   int rc = upload_plan(c);
   if (rc) return rc;
@@ -722,8 +731,8 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   for (int64_t r = 0; r < R; ++r) {
     if (cfg->lease_length_s[r] < 0 || cfg->refresh_interval_s[r] < 0)
       return c->fail(DM_E_INVAL, "lease_length and refresh_interval must be >= 0 (server.go:384-434)");
-    if (cfg->refresh_interval_s[r] > INT32_MAX || cfg->lease_length_s[r] > INT64_MAX / kNs)
-      return c->fail(DM_E_INVAL, "refresh_interval must be < 2^31 s and lease_length < 2^63 ns");
+    if (cfg->refresh_interval_s[r] > INT32_MAX || cfg->lease_length_s[r] > INT32_MAX)
+      return c->fail(DM_E_INVAL, "refresh_interval and lease_length must be < 2^31 s");
   }
   for (int64_t r = 0; r < R; ++r)
     if (cfg->kind[r] < DM_NO_ALGORITHM || cfg->kind[r] > DM_FAIR_SHARE) {
@@ -734,10 +743,14 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   DM_HIP(c, hipStreamSynchronize(c->stream), "sync");
   hipStream_t st = c->stream;
   std::vector<ResCfg> rc(R);
-  for (int64_t r = 0; r < R; ++r)
-    rc[r] = ResCfg{cfg->capacity[r], cfg->safe_capacity[r], cfg->lease_length_s[r] * kNs, cfg->learning_end_ns[r],
-                   cfg->parent_expiry_ns[r], cfg->kind[r], (int32_t)cfg->refresh_interval_s[r]};
+  std::vector<ResCold> rcold(R);
+  for (int64_t r = 0; r < R; ++r) {
+    rc[r] = ResCfg{cfg->capacity[r], cfg->learning_end_ns[r], cfg->parent_expiry_ns[r],
+                   (int32_t)cfg->lease_length_s[r], cfg->kind[r]};
+    rcold[r] = ResCold{cfg->safe_capacity[r], (int32_t)cfg->refresh_interval_s[r], 0};
+  }
   DM_HIP(c, upload(c->cfg, rc.data(), (size_t)R, st), "upload config");
+  DM_HIP(c, upload(c->cold, rcold.data(), (size_t)R, st), "upload config");
   c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
   DM_HIP(c, hipStreamSynchronize(st), "config load");
   c->cfg_loaded = true;
@@ -764,6 +777,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   p.expiry = c->expiry.p;
   p.cfg = c->cfg.p;
   p.agg = c->agg.p;
+  p.expl = c->expl.p;
   // Every tick writes every row's lease (released rows included).  On a store
   // beyond the Infinity Cache a writeback tick writes its gets/expiry into the
   // alternate pair of columns and the pairs swap afterwards: separate output
@@ -938,6 +952,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   p.expiry = c->expiry.p;
   p.cfg = c->cfg.p;
   p.agg = c->agg.p;
+  p.expl = c->expl.p;
   p.now = now_ns;
   p.recompute = 0;
   const ReqArgs q{c->rq_rows.p, c->rq_has.p, c->rq_wants.p, c->rq_sub.p, c->rq_gets.p, c->rq_exp.p};
@@ -1022,8 +1037,8 @@ int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, in
     const auto& so = c->h_seg_off;
     const int64_t r0 = std::upper_bound(so.begin(), so.end(), off) - so.begin() - 1;
     const int64_t r1 = std::upper_bound(so.begin(), so.end(), off + n - 1) - so.begin() - 1;
-    std::vector<ResCfg> cf((size_t)(r1 - r0 + 1));
-    DM_HIP(c, download(cf.data(), (const ResCfg*)c->cfg.p, r0, r1 - r0 + 1, c->stream), "read config");
+    std::vector<ResCold> cf((size_t)(r1 - r0 + 1));
+    DM_HIP(c, download(cf.data(), (const ResCold*)c->cold.p, r0, r1 - r0 + 1, c->stream), "read config");
     DM_HIP(c, hipStreamSynchronize(c->stream), "read config");
     int64_t r = r0;
     for (int64_t i = 0; i < n; ++i) {
@@ -1044,16 +1059,18 @@ int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* 
   const bool wb = !c->have_result || c->last_writeback;
   std::vector<ResAgg> v(n > 0 ? n : 0);
   std::vector<ResCfg> cf(safe && n > 0 ? n : 0);
+  std::vector<ResCold> cc(safe && n > 0 ? n : 0);
   DM_HIP(c, download(v.data(), (const ResAgg*)(wb ? c->agg.p : c->res.p), r0, n, c->stream), "read resources");
   // the device config: a hierarchy exchange rewrites a leaf's templates (dm_hier_root_tick)
   if (safe) DM_HIP(c, download(cf.data(), (const ResCfg*)c->cfg.p, r0, n, c->stream), "read config");
+  if (safe) DM_HIP(c, download(cc.data(), (const ResCold*)c->cold.p, r0, n, c->stream), "read config");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read resources");
   for (int64_t i = 0; i < n; ++i) {
     if (count) count[i] = v[i].count;
     if (sum_has) sum_has[i] = v[i].sum_has;
     if (sum_wants) sum_wants[i] = v[i].sum_wants;
     // SetSafeCapacity (resource.go:81-96) after the tick's Clean: configured, or capacity / Count
-    if (safe) safe[i] = std::isnan(cf[i].safe_capacity) ? cf[i].capacity / (double)v[i].count : cf[i].safe_capacity;
+    if (safe) safe[i] = std::isnan(cc[i].safe_capacity) ? cf[i].capacity / (double)v[i].count : cc[i].safe_capacity;
   }
   return DM_OK;
 }
@@ -1066,16 +1083,18 @@ int dm_read_config(dm_ctx* c, int64_t r0, int64_t n, int32_t* kind, double* capa
   int rc = check_range(c, r0, n, c->R);
   if (rc) return rc;
   std::vector<ResCfg> v(n > 0 ? (size_t)n : 0);
+  std::vector<ResCold> vc(n > 0 ? (size_t)n : 0);
   DM_HIP(c, download(v.data(), (const ResCfg*)c->cfg.p, r0, n, c->stream), "read config");
+  DM_HIP(c, download(vc.data(), (const ResCold*)c->cold.p, r0, n, c->stream), "read config");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read config");
   for (int64_t i = 0; i < n; ++i) {
     if (kind) kind[i] = v[i].kind;
     if (capacity) capacity[i] = v[i].capacity;
-    if (lease_length_s) lease_length_s[i] = v[i].lease_len_ns / kNs;
-    if (refresh_interval_s) refresh_interval_s[i] = v[i].refresh_s;
+    if (lease_length_s) lease_length_s[i] = v[i].lease_len_s;
+    if (refresh_interval_s) refresh_interval_s[i] = vc[i].refresh_s;
     if (learning_end_ns) learning_end_ns[i] = v[i].learning_end_ns;
     if (parent_expiry_ns) parent_expiry_ns[i] = v[i].parent_expiry_ns;
-    if (safe_capacity) safe_capacity[i] = v[i].safe_capacity;
+    if (safe_capacity) safe_capacity[i] = vc[i].safe_capacity;
   }
   return DM_OK;
 }
@@ -1177,7 +1196,8 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   int rc = staged_check(c, n, cols, 5, true, true);
   if (rc) return rc;
   DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->row_index(),
-                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->upd_flags.p, c->stream),
+                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, c->upd_flags.p,
+                          c->stream),
          "upsert");
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
@@ -1359,7 +1379,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
            "check rows");
     DM_HIP(c, launch_carry_reject(F + 1, F + 2, st), "carry");
     DM_HIP(c, launch_upsert(nu, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->row_index(),
-                            c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, F + 2, st),
+                            c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, F + 2, st),
            "upsert");
     DM_HIP(c, launch_clear_rows(nu, c->st_rows.p, c->N, c->row_bits.p, st), "clear rows");
   }
@@ -1475,6 +1495,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   p.expiry = root->expiry.p;
   p.cfg = root->cfg.p;
   p.agg = root->agg.p;
+  p.expl = root->expl.p;
   p.out_gets = root->has.p;
   p.out_expiry = root->expiry.p;
   p.out_wants = root->wants.p;
@@ -1482,7 +1503,8 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   p.res = root->agg.p;
   p.now = now_ns;
   p.recompute = 0;  // the root's running sums, updated as the reference's Clean + Assigns
-  const HierArgs ha{(const double2*)gathered, status, leaf->cfg.p, root->R, n_servers, server};
+  const HierArgs ha{(const double2*)gathered, status, leaf->cfg.p, leaf->cold.p, root->cold.p,
+                    root->R, n_servers, server};
   DM_HIP(root, launch_hier_tick(p, ha, root->stream), "hierarchy root tick");
   if (!same) {  // the leaf's next tick after its new template
     DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");

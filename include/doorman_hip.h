@@ -97,8 +97,8 @@ typedef struct {
 typedef struct {
   const int32_t* kind;              /* DM_* algorithm kind */
   const double* capacity;           /* ResourceTemplate.capacity */
-  const int64_t* lease_length_s;    /* Algorithm.lease_length */
-  const int64_t* refresh_interval_s; /* Algorithm.refresh_interval */
+  const int64_t* lease_length_s;    /* Algorithm.lease_length, seconds in [0, 2^31) (DM_E_INVAL otherwise) */
+  const int64_t* refresh_interval_s; /* Algorithm.refresh_interval, seconds in [0, 2^31) */
   const int64_t* learning_end_ns;   /* learningModeEndTime; DM_NO_LEARNING = none */
   const int64_t* parent_expiry_ns;  /* parent lease expiry; DM_NO_PARENT_EXPIRY = nil */
   const double* safe_capacity;      /* ResourceTemplate.safe_capacity; NaN = unset */
