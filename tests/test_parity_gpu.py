@@ -716,3 +716,29 @@ def test_follower_expiry_encoding(eng, cols):
         g2, e2 = eng.leases_rows(rows)
         np.testing.assert_array_equal(e2, exp[rows])
         assert g2.tobytes() == gets[rows].tobytes()
+
+
+def test_config_limits_and_cold_fields_round_trip(eng):
+    """Lease length and refresh interval are int32 seconds on the device (the hot 32-B
+    config record and the cold record): values up to 2^31 - 1 round-trip through
+    dm_read_config / dm_read_leases, 2^31 is DM_E_INVAL, and the safe capacity read
+    back from the cold record is the configured one (or capacity / Count when unset)."""
+    from doorman_amd._lib import DM_E_INVAL, DmError
+    snap = W.make_snapshot([3, 2], np.ones(5), np.zeros(5), 1, NOW + W.NS, 1, 10.0)
+    snap["lease_length_s"] = np.array([2 ** 31 - 1, 7], np.int64)
+    snap["refresh_interval_s"] = np.array([2 ** 31 - 1, 3], np.int64)
+    snap["safe_capacity"] = np.array([np.nan, 4.5])
+    eng.load(snap)
+    cfg = eng.config()
+    assert cfg["lease_length_s"].tolist() == [2 ** 31 - 1, 7]
+    assert cfg["refresh_interval_s"].tolist() == [2 ** 31 - 1, 3]
+    eng.apportion(NOW, writeback=True)
+    res = eng.resources()
+    assert res["safe_capacity"][0] == 10.0 / 3 and res["safe_capacity"][1] == 4.5
+    gets, exp = eng.leases()
+    assert exp[:3].tolist() == [NOW + (2 ** 31 - 1) * W.NS] * 3 and exp[3:].tolist() == [NOW + 7 * W.NS] * 2
+    bad = dict(snap)
+    bad["lease_length_s"] = np.array([2 ** 31, 7], np.int64)
+    with pytest.raises(DmError) as e:
+        eng.load(bad)
+    assert e.value.code == DM_E_INVAL
