@@ -559,8 +559,12 @@ int dm_create(int device, dm_ctx** out) {
   std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0u);
   for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
   for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
-    e = cumask ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mask.size(), mask.data())
-               : hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
+    e = cumask && ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mask.size(), mask.data())
+                          : hipErrorNotSupported;
+    if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
+      (void)hipGetLastError();
+      e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
