@@ -76,8 +76,8 @@ enum KClass {
   KC_LARGE_FUSED,
   KC_COUNT
 };
-const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block256x2",
-                                     "block256x4",   "block512x4", "block1024x4", "sub8x2",    "sub16x2",
+const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
+                                     "block128x8",   "block512x4", "block1024x4", "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release", "large_fused"};
