@@ -95,8 +95,8 @@ def kernel_units(snap):
     sizes = np.diff(snap["seg_off"])
     units = {}
     edges = [("sub8x2", 9, 16), ("sub16x2", 17, 32), ("sub16x4", 33, 64), ("sub32x4", 65, 128),
-             ("wave64x4", 129, 256), ("block128x4", 257, 512), ("block128x8", 513, 1024), ("block512x4", 1025, 2048),
-             ("block1024x4", 2049, 4096)]
+             ("wave64x4", 129, 256), ("block128x4", 257, 512), ("block128x8", 513, 1024), ("block256x8", 1025, 2048),
+             ("block512x8", 2049, 4096)]
     small = sizes <= 8
     units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
     for name, lo, hi in edges:

@@ -32,7 +32,7 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 constexpr int kSmallMax = 8;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
-constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block512x4, block1024x4, sub8x2, sub16x2
+constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block256x8, block512x8, sub8x2, sub16x2
 // Lease-table footprint (48 B per lease) above which a tick is taken to stream
 // from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
 constexpr int64_t kStreamBytes = 1LL << 30;

@@ -195,14 +195,16 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   if (t == 0) write_resource(p, seg, rs, cl, delta.v);
 }
 
-// One G-thread workgroup per resource (G = 128..1024, R = 4 or 8 rows per thread).
+// One G-thread workgroup per resource (G = 128..512, R = 4 or 8 rows per thread).
 // 257-1024 rows run on 128 threads (2 waves) with 8 rows each, held to 5 waves per
 // SIMD (<= 96 VGPRs): 5 x 4 SIMDs x 64 lanes x 8 rows = 10240 rows in flight per CU
 // against 7168 for 256 threads x 4 rows at 7 waves per SIMD (65 VGPRs).  The tick is
 // bound by bytes in flight: C3 560-590 -> 490-500 us, C1 61 -> 55 us
 // (tools/ab.py, one box); 6 waves per SIMD spills (80 VGPRs + scratch: 2x slower).
+// 1025-2048 / 2049-4096 rows likewise on 256 x 8 (5 waves) / 512 x 8 (106 VGPRs, 4
+// waves) instead of 512 x 4 / 1024 x 4: C2's kernel time -5%, its tick -2%.
 template <int G, int R>
-__global__ __launch_bounds__(G, (G == 128 && R == 8) ? 5 : 1) void k_block(DevParams p, const WorkItem* __restrict__ items, int nitems,
+__global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevParams p, const WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nitems) return;
@@ -1782,8 +1784,8 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
     case 2: k_wave<4><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 3: k_block<128, 4><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
     case 4: k_block<128, 8><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 5: k_block<512, 4><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 6: k_block<1024, 4><<<n, 1024, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 5: k_block<256, 8><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 6: k_block<512, 8><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
     case 7: k_sub<8, 2><<<(unsigned)((n + 31) / 32), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 8: k_sub<16, 2><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;

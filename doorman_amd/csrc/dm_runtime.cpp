@@ -77,7 +77,7 @@ enum KClass {
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
-                                     "block128x8",   "block512x4", "block1024x4", "sub8x2",    "sub16x2",
+                                     "block128x8",   "block256x8", "block512x8",  "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release", "large_fused"};

@@ -15,8 +15,8 @@ from . import _lib
 from ._lib import check, lib
 from .workloads import CFG_FIELDS
 
-_BIN_NAMES = ("small_packs", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8", "block512x4",
-              "block1024x4", "sub8x2", "sub16x2", "large_resources", "large_chunks", "leases",
+_BIN_NAMES = ("small_packs", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8", "block256x8",
+              "block512x8", "sub8x2", "sub16x2", "large_resources", "large_chunks", "leases",
               "large_fused", "fused_chunks", "fused_max_chunks", "fused_capacity")
 
 
