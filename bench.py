@@ -102,6 +102,8 @@ def kernel_units(snap):
     for name, lo, hi in edges:
         m = (sizes >= lo) & (sizes <= hi)
         units[name] = (int(sizes[m].sum()), int(m.sum()))
+    m = (sizes >= 9) & (sizes <= 256)  # the sub-wave bins in one launch (k_subs)
+    units["subs_merged"] = (int(sizes[m].sum()), int(m.sum()))
     big = sizes > 4096
     for name in ("large_fused", "large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
         units[name] = (int(sizes[big].sum()), int(big.sum()))

@@ -52,6 +52,15 @@ struct WorkItem {  // one resource of a size bin: no dependent load before its r
   int64_t lo;
 };
 
+// The sub-wave bins of one tick for k_subs, in launch order: 8x2 (9-16 rows),
+// 16x2 (17-32), 16x4 (33-64), 32x4 (65-128), 64x4 (129-256); blocks[k] workgroups
+// of 256 threads each (256 / G resources per workgroup).
+struct SubBins {
+  const WorkItem* items[5];
+  int32_t n[5];
+  int32_t blocks[5];
+};
+
 struct Chunk {  // kChunkRows rows of one large resource
   int32_t seg;
   int32_t lseg;  // index into the large-resource table

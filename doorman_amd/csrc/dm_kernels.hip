@@ -237,6 +237,32 @@ __global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __rest
   group_segment<G, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
+// The sub-wave bins in one launch (DM_MERGE_SUBS): the workgroups of each bin
+// follow one another in blockIdx order, so the class stream runs them without a
+// kernel boundary (drain + ramp) between bins.  Register use is the largest bin's.
+template <int G, int R>
+__device__ __forceinline__ void sub_part(const DevParams& p, const WorkItem* __restrict__ items, int nitems, int blk,
+                                         int32_t* general_list, int32_t* general_count) {
+  Lds<G> lds;  // unused by sub-wave and wave reductions
+  const int i = blk * (256 / G) + (int)(threadIdx.x / G);
+  if (i >= nitems) return;
+  group_segment<G, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
+}
+
+__global__ __launch_bounds__(256, 5) void k_subs(DevParams p, SubBins sb, int32_t* general_list,
+                                              int32_t* general_count) {
+  int b = blockIdx.x;
+  if (b < sb.blocks[0]) return sub_part<8, 2>(p, sb.items[0], sb.n[0], b, general_list, general_count);
+  b -= sb.blocks[0];
+  if (b < sb.blocks[1]) return sub_part<16, 2>(p, sb.items[1], sb.n[1], b, general_list, general_count);
+  b -= sb.blocks[1];
+  if (b < sb.blocks[2]) return sub_part<16, 4>(p, sb.items[2], sb.n[2], b, general_list, general_count);
+  b -= sb.blocks[2];
+  if (b < sb.blocks[3]) return sub_part<32, 4>(p, sb.items[3], sb.n[3], b, general_list, general_count);
+  b -= sb.blocks[3];
+  if (b < sb.blocks[4]) return sub_part<64, 4>(p, sb.items[4], sb.n[4], b, general_list, general_count);
+}
+
 // --------------------------------------------------------------------------
 // Wave-packed small resources (n <= kSmallMax): one wave covers a run of whole
 // resources; every lane evaluates its own client literally, looping over its
@@ -1790,6 +1816,14 @@ hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, 
     case 8: k_sub<16, 2><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st) {
+  unsigned blocks = 0;
+  for (int k = 0; k < 5; ++k) blocks += (unsigned)sb.blocks[k];
+  if (blocks == 0) return hipSuccess;
+  k_subs<<<blocks, 256, 0, st>>>(p, sb, glist, gcount);
   return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@ namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
+hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
@@ -74,13 +75,14 @@ enum KClass {
   KC_UPSERT,
   KC_RELEASE,
   KC_LARGE_FUSED,
+  KC_SUBS,
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
                                      "block128x8",   "block256x8", "block512x8",  "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
-                                     "store_release", "large_fused"};
+                                     "store_release", "large_fused", "subs_merged"};
 
 template <typename T>
 struct DBuf {
@@ -177,6 +179,9 @@ struct dm_ctx {
   DBuf<LargeSeg> large;
   // one-launch large path (dm_large.hip): its own chunking (fused_G * kFusedRows rows)
   int large_mode = DM_LARGE_CHAIN;
+  // the sub-wave bins in one launch (k_subs; DM_MERGE_SUBS=0: one launch per bin):
+  // C2 tick 144-145 -> 138 us (tools/ab.py, both orders, one box)
+  bool merge_subs = true;
   int fused_G = 512;
   bool fused_ok = false;       // every large resource within the co-residency bound
   int64_t fused_max_chunks = 0, fused_cap = 0;
@@ -526,6 +531,7 @@ int dm_create(int device, dm_ctx** out) {
   }
   dm_ctx* c = new dm_ctx();
   c->device = device;
+  if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
   if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
     for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
@@ -877,9 +883,29 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                       [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
   }
+  // the sub-wave bins (8x2, 16x2, 16x4, 32x4, 64x4) in one launch on bin 0's stream
+  static constexpr int kSubBins[5] = {7, 8, 0, 1, 2}, kSubG[5] = {8, 16, 16, 32, 64};
+  const bool merge_subs = c->merge_subs;
+  if (merge_subs) {
+    SubBins sb{};
+    int nonempty = 0;
+    for (int k = 0; k < 5; ++k) {
+      const int b = kSubBins[k], n = (int)c->h_bins[b].size();
+      const int per = 256 / kSubG[k];
+      sb.items[k] = c->bins[b].p;
+      sb.n[k] = n;
+      sb.blocks[k] = (n + per - 1) / per;
+      nonempty += n > 0;
+    }
+    if (nonempty > 0) {
+      hipStream_t s = cls_stream(0);
+      DM_HIP(c, timed(KC_SUBS, s, [&] { return launch_subs(p, sb, gl, gc, s); }), "sub-wave kernel");
+    }
+  }
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
+    if (merge_subs && (b == 7 || b == 8 || b <= 2)) continue;
     hipStream_t s = cls_stream(b);
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }),
            "group kernel");
