@@ -78,16 +78,27 @@ def make_workload(name: str, rank: int):
 # expiry is read or written per lease.  SURVEY.md section 8(d)'s
 # canonical layout moves 48 B (int64 subclients, expiry read and written per lease).
 LEASE_BYTES = 28
+DENSE_LEASE_BYTES = 24  # a dense resource's rows (one subclient count, every row a live follower): no subclients read
 SURVEY_LEASE_BYTES = 48
 RESOURCE_BYTES = 97  # config 32 B + running sums and follower expiry 32 B read and written + explicit flag 1 B
 
 
-def algorithmic_bytes(n_leases: int, n_resources: int) -> int:
+def algorithmic_bytes(n_leases: int, n_resources: int, dense_leases: float = 0) -> int:
     """Bytes a writeback tick must move with this store layout: per lease read wants,
-    has, subclients (int32: the boundary restricts them to [0, 2^31 - 1)), write gets;
+    has, subclients (int32: the boundary restricts them to [0, 2^31 - 1)), write gets
+    -- without the subclients read for the rows of dense resources (dm_store_stats);
     per resource the config record and the running sums in and out.  Re-reads are
     not counted."""
-    return LEASE_BYTES * n_leases + RESOURCE_BYTES * n_resources
+    return int(round(LEASE_BYTES * n_leases - (LEASE_BYTES - DENSE_LEASE_BYTES) * dense_leases
+                     + RESOURCE_BYTES * n_resources))
+
+
+def dense_fraction(eng, snap) -> float:
+    """Share of the rows of resources with 257..1024 rows (the 128-thread group
+    kernels, the only ones that keep the dense state) that sit in dense resources."""
+    sizes = np.diff(snap["seg_off"])
+    group = int(sizes[(sizes >= 257) & (sizes <= 1024)].sum())
+    return eng.store_stats()["dense_leases"] / group if group else 0.0
 
 
 def kernel_units(snap):
@@ -337,7 +348,9 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
     if single:  # one kernel per tick: HIP events around the timed region itself
         avg_s = run["stream_ms"] / steps / 1e3
     leases_k, res_k = kernel_units(snap).get(name, (N, R))
-    alg = algorithmic_bytes(leases_k, res_k)
+    group_kernel = name in ("block128x4", "block128x8")
+    dense_k = run.get("dense_frac", 0.0) * leases_k if group_kernel else 0.0
+    alg = algorithmic_bytes(leases_k, res_k, dense_k)
     achieved = alg / avg_s / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
@@ -352,8 +365,11 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
             "traffic_source": f"profiles/pmc_{workload}.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, calibrated)",
             "algorithmic_bytes_per_launch": alg,
             "bytes_model": (f"{LEASE_BYTES} B per lease (read wants, has, int32 subclients; write gets: granted "
-                            f"leases follow their resource's expiry) + {RESOURCE_BYTES} B per resource; the "
-                            f"canonical layout of SURVEY.md 8(d) moves {SURVEY_LEASE_BYTES} B per lease"),
+                            f"leases follow their resource's expiry), {DENSE_LEASE_BYTES} B for the rows of dense "
+                            f"resources (every row a live follower with one subclient count: no subclients read) "
+                            f"+ {RESOURCE_BYTES} B per resource; the canonical layout of SURVEY.md 8(d) moves "
+                            f"{SURVEY_LEASE_BYTES} B per lease"),
+            "dense_lease_share": round(dense_k / leases_k, 4) if leases_k else 0.0,
             "survey_layout_equivalent_GBs": round((SURVEY_LEASE_BYTES * leases_k + 64 * res_k) / avg_s / 1e9, 1),
             "avg_launch_us": round(avg_s * 1e6, 2),
             "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
@@ -463,6 +479,7 @@ def main():
         step = lambda: ht.tick(now, asynchronous=True)  # noqa: E731
 
     run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4")
+    run["dense_frac"] = dense_fraction(eng, snap)
     t = torch.tensor([run["elapsed"]], dtype=torch.float64, device=red_dev)
     n = torch.tensor([N], dtype=torch.float64, device=red_dev)
     if world > 1:
@@ -483,6 +500,7 @@ def main():
         e1.load(snap1)
         st1 = lambda: e1.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
         r1 = timed_steps(torch, e1, st1, args.steps, args.warmup, sync_ranks)
+        r1["dense_frac"] = dense_fraction(e1, snap1)
         n1 = len(snap1["wants"])
         extra["c1"] = {"workload": WORKLOADS["c1"], "value": n1 * args.steps / r1["elapsed"], "unit": "leases/s",
                        "ms_per_step": r1["elapsed"] / args.steps * 1e3,
@@ -494,7 +512,9 @@ def main():
         cpu = cpu_baseline(snap, now, args.cpu_budget)
 
     if rank == 0:
-        tick_bytes = algorithmic_bytes(N, R)
+        sizes = np.diff(snap["seg_off"])
+        group_leases = int(sizes[(sizes >= 257) & (sizes <= 1024)].sum())
+        tick_bytes = algorithmic_bytes(N, R, run["dense_frac"] * group_leases)
         line = {
             "metric": METRIC,
             "value": n_total * args.steps / t_max,

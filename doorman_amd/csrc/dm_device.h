@@ -48,7 +48,8 @@ struct Pack {  // a run of consecutive small resources covering <= 64 rows
 
 struct WorkItem {  // one resource of a size bin: no dependent load before its rows
   int32_t seg;
-  int32_t n;
+  int32_t n;   // rows (<= 4096) in bits 0-15; bits 16-23: the dense hint written by
+               // writeback ticks (s0 > 0 when expl[seg] == s0 + 1, below), else 0
   int64_t lo;
 };
 
@@ -56,7 +57,7 @@ struct WorkItem {  // one resource of a size bin: no dependent load before its r
 // 16x2 (17-32), 16x4 (33-64), 32x4 (65-128), 64x4 (129-256); blocks[k] workgroups
 // of 256 threads each (256 / G resources per workgroup).
 struct SubBins {
-  const WorkItem* items[5];
+  WorkItem* items[5];
   int32_t n[5];
   int32_t blocks[5];
 };
@@ -188,8 +189,13 @@ struct DevParams {
   double* out_wants;  // writeback only: released rows zeroed (else nullptr)
   int32_t* out_sub;   // writeback only
   ResAgg* res;        // per-resource results (== agg in writeback mode)
-  uint8_t* expl;      // [R] 1: some row may carry an explicit expiry (loaded, upserted,
-                      // hierarchy-written); a writeback tick clears it (every row follows)
+  uint8_t* expl;      // [R] per-resource row state: 1: some row may carry an explicit
+                      // expiry (loaded, upserted, hierarchy-written); 0: every row follows
+                      // its resource or is released; s0 + 1 in [2, 255] ("dense"): every
+                      // row is a live follower with subclients == s0, so a tick need not
+                      // read the subclients column (set by writeback ticks of the
+                      // 128-thread group kernels, 257-1024 rows; upserts set 1, releases
+                      // reset it to 0)
   int64_t now;
   int32_t recompute;
   int32_t writeback;  // rows become followers / released in the store; out_expiry unused

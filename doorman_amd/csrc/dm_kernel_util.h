@@ -19,13 +19,17 @@ struct Res {
   double C;           // Resource.capacity() (resource.go:62-70)
   int64_t exp_out;    // now + lease_length (store.go:161)
   int64_t follow_exp; // the expiry of the resource's follower rows (dm_device.h)
-  int32_t any_expl;   // DevParams::expl: wave-uniform, so no row's expiry load waits on its subclients word
+  int32_t xstate;     // DevParams::expl (dm_device.h): 1 = rows may carry explicit expiries (wave-uniform,
+                      // so no row's expiry load waits on its subclients word); s0 + 1 >= 2 = dense
   // the store's running sums, loaded with the config so that no global load
   // waits behind the first reduction's barrier
   long long agg_count;
   double agg_has;
   double agg_wants;
 };
+
+__device__ __forceinline__ bool any_explicit(const Res& r) { return r.xstate == 1; }
+__device__ __forceinline__ int dense_subclients(const Res& r) { return r.xstate >= 2 ? r.xstate - 1 : 0; }
 
 __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
   Res r;
@@ -36,7 +40,7 @@ __device__ __forceinline__ Res load_res(const DevParams& p, int seg) {
   r.exp_out = p.now + (int64_t)c.lease_len_s * kNs;
   const ResAgg g = p.agg[seg];
   r.follow_exp = g.follow_exp;
-  r.any_expl = p.expl[seg];
+  r.xstate = p.expl[seg];
   if (!p.recompute) {
     r.agg_count = g.count;
     r.agg_has = g.sum_has;
@@ -265,6 +269,14 @@ struct SumD {
 struct OpSumD {
   __device__ SumD operator()(SumD a, SumD b) const { return SumD{a.v + b.v}; }
 };
+struct SumDN {  // the Assign delta plus the live rows (group kernels with the dense state)
+  double v;
+  int n;
+  int pad;
+};
+struct OpSumDN {
+  __device__ SumDN operator()(SumDN a, SumDN b) const { return SumDN{a.v + b.v, a.n + b.n, 0}; }
+};
 
 template <int G>
 struct Lds {  // one slot per wave (unused by groups of one wave or less)
@@ -275,6 +287,7 @@ struct Lds {  // one slot per wave (unused by groups of one wave or less)
   AggC c[W];
   TMin t[W];
   SumD d[W];
+  SumDN dn[W];
 };
 
 // Cleaned store sums from pass A (store.go:169-181 applied to the snapshot).
@@ -298,15 +311,21 @@ __device__ __forceinline__ Clean clean_from(const DevParams& p, const Res& rs, c
   return c;
 }
 
+// dense_next (group kernels only): s0 > 0 when after this writeback tick every row of
+// the resource is a live follower with subclients s0 (the expl byte becomes s0 + 1).
 __device__ __forceinline__ void write_resource(const DevParams& p, int seg, const Res& rs, const Clean& c,
-                                               double delta) {
+                                               double delta, int dense_next = 0) {
   ResAgg r;
   r.count = c.count;
   r.sum_wants = c.sum_wants;
   r.sum_has = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
   r.follow_exp = p.writeback ? rs.exp_out : rs.follow_exp;  // a writeback tick's leases follow exp_out
   p.res[seg] = r;
-  if (p.writeback && rs.any_expl) p.expl[seg] = 0;  // ... and none keeps an explicit expiry
+  if (p.writeback) {  // ... and none keeps an explicit expiry
+    const int had = rs.xstate;
+    const int want = dense_next ? dense_next + 1 : 0;
+    if (had != want) p.expl[seg] = (uint8_t)want;
+  }
 }
 
 // ---- the subclients column's expiry encoding (dm_device.h) ----

@@ -25,11 +25,12 @@ namespace dm {
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
 template <int G, int R>
-__device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, int t, Lds<G>& lds,
-                                              int32_t* general_list, int32_t* general_count) {
+__device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, WorkItem* item, int t,
+                                              Lds<G>& lds, int32_t* general_list, int32_t* general_count) {
+  constexpr bool kDense = G == 128;  // the dense-subclients path (below)
   const int seg = wi.seg;
   const int64_t lo = wi.lo;
-  const int n = wi.n;
+  const int n = kDense ? wi.n & 0xFFFF : wi.n;
   // wave-uniform bases + 32-bit per-lane offsets: one VGPR addresses every column
   const double* __restrict__ wb = p.wants + lo;
   const double* __restrict__ hb = p.has + lo;
@@ -44,16 +45,43 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // re-read row n-1 (same cache line, n >= 1 in every bin) instead of branching
   // around the load, which made the compiler wait on each row's expiry before
   // issuing the next row (R serial memory latencies per workgroup).
+  // A dense resource (every row a live follower with the same subclients s0, the
+  // state its last writeback tick left: dm_device.h) is not read from the
+  // subclients column: 24 B per lease instead of 28.  The work item carries the
+  // state as a hint (no dependent load before the rows); the resource's own byte,
+  // loaded with its record, confirms it, and a stale hint (an upsert or release
+  // since that tick) reads the column after all.  Only the 128-thread blocks
+  // (257-1024 rows) take this path: in the other group kernels the extra branch
+  // costs registers they do not have (spills at 5 waves per SIMD; C2 +3.5 %).
+  const int hint = kDense ? wi.n >> 16 : 0;
+  if (!hint) {
 #pragma unroll
-  for (int k = 0; k < R; ++k) {
-    const int i = k * G + t;
-    const unsigned u = (unsigned)(i < n ? i : n - 1);
-    // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
-    w[k] = *col_at(wb, u);
-    h[k] = *col_at(hb, u);
-    sr[k] = *col_at(sb, u);
+    for (int k = 0; k < R; ++k) {
+      const int i = k * G + t;
+      const unsigned u = (unsigned)(i < n ? i : n - 1);
+      // plain loads: non-temporal loads measured 3-4% slower (tools/ab.py, C1 and C3)
+      w[k] = *col_at(wb, u);
+      h[k] = *col_at(hb, u);
+      sr[k] = *col_at(sb, u);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = k * G + t;
+      const unsigned u = (unsigned)(i < n ? i : n - 1);
+      w[k] = *col_at(wb, u);
+      h[k] = *col_at(hb, u);
+      sr[k] = hint;
+    }
   }
   const Res rs = load_res(p, seg);
+  if (hint && dense_subclients(rs) != hint) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = k * G + t;
+      sr[k] = *col_at(sb, (unsigned)(i < n ? i : n - 1));
+    }
+  }
   // Followers expire with their resource; only a resource whose rows may carry an
   // explicit expiry (loaded / upserted by the host, none after a writeback tick)
   // reads the 8-B expiry column.  The test is the resource's flag, not the rows'
@@ -61,7 +89,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   int64_t e[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) e[k] = rs.follow_exp;
-  if (rs.any_expl) {
+  if (any_explicit(rs)) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -115,7 +143,10 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     // heterogeneous subclients (GetServerCapacity, server.go:850-879) or NaN wants:
     // one round-2 threshold per distinct subclient count.  Rare (the hierarchy's
     // root level), so the whole resource goes to k_general, untouched here.
-    if (t == 0) general_list[atomicAdd(general_count, 1)] = seg;
+    if (t == 0) {
+      general_list[atomicAdd(general_count, 1)] = seg;
+      if (p.writeback && hint) item->n = n;  // k_general's writeback clears the byte
+    }
     return;
   }
 
@@ -191,8 +222,23 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     delta.v += g - h[k];
   }
 
-  delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
-  if (t == 0) write_resource(p, seg, rs, cl, delta.v);
+  int nlive = 0;  // live rows of the resource (the dense state needs all n)
+  if constexpr (kDense) {
+    SumDN dl{delta.v, __builtin_popcount(live), 0};
+    dl = group_reduce<G, SumDN, OpSumDN, false>(dl, OpSumDN(), lds.dn);
+    delta.v = dl.v;
+    nlive = dl.n;
+  } else {
+    delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
+  }
+  if (t == 0) {
+    // after a writeback tick every live row follows the resource; all n rows live
+    // with one subclient count s0 (1..254) makes the resource dense
+    const int dn =
+        (kDense && p.writeback && nlive == n && a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
+    write_resource(p, seg, rs, cl, delta.v, dn);
+    if (p.writeback && hint != dn) item->n = n | dn << 16;
+  }
 }
 
 // One G-thread workgroup per resource (G = 128..512, R = 4 or 8 rows per thread).
@@ -204,22 +250,22 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
 // 1025-2048 / 2049-4096 rows likewise on 256 x 8 (5 waves) / 512 x 8 (106 VGPRs, 4
 // waves) instead of 512 x 4 / 1024 x 4: C2's kernel time -5%, its tick -2%.
 template <int G, int R>
-__global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevParams p, const WorkItem* __restrict__ items, int nitems,
+__global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevParams p, WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nitems) return;
-  group_segment<G, R>(p, items[blockIdx.x], threadIdx.x, lds, general_list, general_count);
+  group_segment<G, R>(p, items[blockIdx.x], items + blockIdx.x, threadIdx.x, lds, general_list, general_count);
 }
 
 // One wave per resource (n <= 64 R), four independent waves per workgroup: wave
 // reductions only (DPP, no barriers), four resources in flight per workgroup.
 template <int R>
-__global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __restrict__ items, int nitems,
+__global__ __launch_bounds__(256) void k_wave(DevParams p, WorkItem* __restrict__ items, int nitems,
                                               int32_t* general_list, int32_t* general_count) {
   Lds<64> lds;  // unused by wave reductions
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nitems) return;
-  group_segment<64, R>(p, items[i], threadIdx.x & 63, lds, general_list, general_count);
+  group_segment<64, R>(p, items[i], items + i, threadIdx.x & 63, lds, general_list, general_count);
 }
 
 // Sub-wave groups: G = 16 or 32 lanes own one resource of up to G*R rows (R rows
@@ -229,24 +275,24 @@ __global__ __launch_bounds__(256) void k_wave(DevParams p, const WorkItem* __res
 // per pass set, 4 DPP steps each): narrow groups with several rows per lane share
 // every DPP step among 64 / G resources.
 template <int G, int R = 1>
-__global__ __launch_bounds__(256) void k_sub(DevParams p, const WorkItem* __restrict__ items, int nitems,
+__global__ __launch_bounds__(256) void k_sub(DevParams p, WorkItem* __restrict__ items, int nitems,
                                              int32_t* general_list, int32_t* general_count) {
   Lds<G> lds;  // unused by sub-wave reductions
   const int i = blockIdx.x * (256 / G) + (int)(threadIdx.x / G);
   if (i >= nitems) return;  // whole groups only: reductions never cross a group
-  group_segment<G, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
+  group_segment<G, R>(p, items[i], items + i, threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
 // The sub-wave bins in one launch (DM_MERGE_SUBS): the workgroups of each bin
 // follow one another in blockIdx order, so the class stream runs them without a
 // kernel boundary (drain + ramp) between bins.  Register use is the largest bin's.
 template <int G, int R>
-__device__ __forceinline__ void sub_part(const DevParams& p, const WorkItem* __restrict__ items, int nitems, int blk,
+__device__ __forceinline__ void sub_part(const DevParams& p, WorkItem* __restrict__ items, int nitems, int blk,
                                          int32_t* general_list, int32_t* general_count) {
   Lds<G> lds;  // unused by sub-wave and wave reductions
   const int i = blk * (256 / G) + (int)(threadIdx.x / G);
   if (i >= nitems) return;
-  group_segment<G, R>(p, items[i], threadIdx.x & (G - 1), lds, general_list, general_count);
+  group_segment<G, R>(p, items[i], items + i, threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
 __global__ __launch_bounds__(256, 5) void k_subs(DevParams p, SubBins sb, int32_t* general_list,
@@ -307,7 +353,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   const int seg = first_seg + k;
   const Res rs = load_res(p, seg);
   int64_t e = rs.follow_exp;  // followers expire with their resource; explicit rows read theirs
-  if (__any(nrows > 0 && rs.any_expl) && rs.any_expl && sub_explicit(sr)) e = p.expiry[myrow];
+  if (__any(nrows > 0 && any_explicit(rs)) && any_explicit(rs) && sub_explicit(sr)) e = p.expiry[myrow];
   if (sub_released(sr)) e = kReleased;
   const int lv = (valid && !(p.now > e)) ? 1 : 0;  // store.go:174
   int s = sub_value(sr);
@@ -434,7 +480,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
   Res ors;
   ors.exp_out = shfl_any(rs.exp_out, olo & 63);
   ors.follow_exp = shfl_any(rs.follow_exp, olo & 63);
-  ors.any_expl = shfl_i(rs.any_expl, olo & 63);
+  ors.xstate = shfl_i(rs.xstate, olo & 63);
   if (owner) {
     const int oseg = first_seg + lane;
     if (olo == ohi) {  // resource without rows
@@ -443,7 +489,7 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
       osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
       ors.exp_out = p.now + (int64_t)p.cfg[oseg].lease_len_s * kNs;
       ors.follow_exp = p.agg[oseg].follow_exp;
-      ors.any_expl = p.expl[oseg];
+      ors.xstate = p.expl[oseg];
     }
     Clean oc{ocount, osh, osw};
     write_resource(p, oseg, ors, oc, 0.0);
@@ -537,7 +583,7 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   int64_t e[kLR];
 #pragma unroll
   for (int k = 0; k < kLR; ++k) e[k] = rs.follow_exp;
-  if (rs.any_expl) {  // the resource's flag (see group_segment)
+  if (any_explicit(rs)) {  // the resource's flag (see group_segment)
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
       const int i = k * 256 + threadIdx.x;
@@ -1309,7 +1355,7 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
 }
 
 __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex ix, double* s_has, double* s_wants,
-                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags) {
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (*flags & kUpdReject) return;  // uniform over the grid
   const bool active = i < n;
@@ -1326,6 +1372,7 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex 
     s_wants[r] = 0.0;
     s_sub[r] = (int32_t)kSubReleased;
     s_exp[r] = kReleased;
+    if (expl[seg] >= 2) expl[seg] = 0;  // no longer dense: the next tick reads the subclients column
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
@@ -1800,7 +1847,7 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
+hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const unsigned wg4 = (unsigned)((n + 3) / 4);
@@ -1859,9 +1906,10 @@ hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, cons
 }
 
 hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
-                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                          hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, ix, s_has, s_wants, s_sub, s_exp, agg, flags);
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, ix, s_has, s_wants, s_sub, s_exp, agg, expl, flags);
   return hipGetLastError();
 }
 

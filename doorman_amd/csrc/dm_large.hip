@@ -204,7 +204,7 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     int64_t e[kFR];
 #pragma unroll
     for (int k = 0; k < kFR; ++k) e[k] = rs.follow_exp;
-    if (rs.any_expl) {  // the resource's flag (dm_kernels.hip, group_segment)
+    if (any_explicit(rs)) {  // the resource's flag (dm_kernels.hip, group_segment)
 #pragma unroll
       for (int k = 0; k < kFR; ++k) {
         const int i = k * G + t;

@@ -18,7 +18,7 @@
 
 namespace dm {
 hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
-hipError_t launch_bin(int bin, const DevParams& p, const WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
+hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
@@ -33,7 +33,8 @@ hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, cons
                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
                          hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
-                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, const uint32_t* flags, hipStream_t st);
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                          hipStream_t st);
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
                              const int64_t* sub, uint32_t* flags, hipStream_t st);
 hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st);
@@ -1311,7 +1312,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   int rc = staged_check(c, n, cols, 1, false, false);
   if (rc) return rc;
   DM_HIP(c, launch_release(n, c->st_rows.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p,
-                           c->agg.p, c->upd_flags.p, c->stream),
+                           c->agg.p, c->expl.p, c->upd_flags.p, c->stream),
          "release");
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
@@ -1396,7 +1397,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     DM_HIP(c, launch_check_rows(nr, c->st_rel.p, c->N, c->row_bits.p, nullptr, nullptr, F + 1, st), "check rows");
     DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
     DM_HIP(c, launch_release(nr, c->st_rel.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
-                             F + 1, st),
+                             c->expl.p, F + 1, st),
            "release");
     DM_HIP(c, launch_clear_rows(nr, c->st_rel.p, c->N, c->row_bits.p, st), "clear rows");
   } else {
@@ -1605,6 +1606,27 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   const int n = 8 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
+}
+
+int dm_store_stats(dm_ctx* c, int64_t* out, int max) {
+  DM_ENTER(c);
+  if (!out || max < 0) return c->fail(DM_E_INVAL, "bad output buffer");
+  if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  std::vector<uint8_t> ex((size_t)c->R);
+  DM_HIP(c, download(ex.data(), (const uint8_t*)c->expl.p, 0, c->R, c->stream), "read row states");
+  DM_HIP(c, hipStreamSynchronize(c->stream), "read row states");
+  int64_t v[4] = {0, 0, 0, 0};
+  for (int64_t r = 0; r < c->R; ++r) {
+    if (ex[(size_t)r] >= 2) {
+      v[0] += 1;
+      v[1] += c->h_seg_off[r + 1] - c->h_seg_off[r];
+    } else if (ex[(size_t)r] == 1) {
+      v[2] += 1;
+    }
+  }
+  v[3] = c->R;
+  for (int i = 0; i < 4 && i < max; ++i) out[i] = v[i];
+  return 4;
 }
 
 }  // extern "C"

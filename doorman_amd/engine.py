@@ -277,6 +277,14 @@ class Engine:
         n = self._chk(self._L.dm_plan_info(self._ctx, arr, 32))
         return {_BIN_NAMES[i]: int(arr[i]) for i in range(min(n, len(_BIN_NAMES)))}
 
+    def store_stats(self) -> dict:
+        """dm_store_stats: dense resources (read at 24 B per lease) and their rows,
+        resources that may hold explicit expiries, resources."""
+        arr = (ctypes.c_int64 * 4)()
+        self._chk(self._L.dm_store_stats(self._ctx, arr, 4))
+        return {"dense_resources": int(arr[0]), "dense_leases": int(arr[1]), "explicit_resources": int(arr[2]),
+                "resources": int(arr[3])}
+
 
 def device_count() -> int:
     n = ctypes.c_int()

@@ -295,6 +295,10 @@ int dm_reset_kernel_times(dm_ctx* ctx);
  * the one-launch large path, its chunks, the most chunks of one resource and the
  * device's resident-workgroup bound */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
+/* row-state summary of the device store (synchronous): dense resources (every row a
+ * live follower with one subclient count: a tick reads 24 B per lease, not 28),
+ * their rows, resources that may hold explicit expiries, resources; returns 4 */
+int dm_store_stats(dm_ctx* ctx, int64_t* out, int max);
 
 /* ---- round-oriented GetCapacity dispatch (dm_server.cpp) ----
  *

@@ -762,3 +762,64 @@ def test_config_limits_and_cold_fields_round_trip(eng):
     with pytest.raises(DmError) as e:
         eng.load(bad)
     assert e.value.code == DM_E_INVAL
+
+
+@pytest.mark.parametrize("cols", ["inplace", "alternate"])
+def test_dense_subclients_state(eng, cols):
+    """A writeback tick marks a group-kernel resource dense when every row is a live
+    follower with one subclient count; the next ticks skip its subclients column.
+    Releases, upserts (other subclient counts, explicit expiries) and lapsed
+    followers end the state, wants refreshes keep it; every tick matches the oracle
+    on a host copy, and dm_store_stats counts the dense resources."""
+    rng = np.random.default_rng(5150)
+    sizes = np.array([12, 30, 60, 100, 200, 400, 900, 1000, 1500, 3000, 5, 0, 9000, 20, 700])
+    snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=0.0, learning_frac=0.0,
+                               parent_expired_frac=0.0)
+    snap["lease_length_s"] = np.full(len(sizes), 20, np.int64)
+    group = (sizes >= 257) & (sizes <= 1024)  # the 128-thread group kernels keep the state
+    eng.load(snap)
+    assert eng.store_stats()["dense_resources"] == 0  # loaded rows carry explicit expiries
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    off = np.asarray(snap["seg_off"])
+    N = len(host["wants"])
+    for rnd, dt in enumerate([0, 5, 10, 15, 20, 25, 70]):
+        now = NOW + dt * W.NS
+        if rnd == 2:  # releases: those resources stop being dense
+            rows = np.array([off[1] + 3, off[6] + 10, off[8] + 1])
+            eng.release(rows)
+            host["has"][rows], host["wants"][rows], host["subclients"][rows] = 0.0, 0.0, 0
+            host["expiry_ns"][rows] = W.RELEASED
+            W.add_store_sums(host)
+        if rnd == 3:  # wants refreshes keep the state
+            rows = np.sort(rng.choice(N, N // 10, replace=False))
+            nw = rng.uniform(0.0, 2.0, len(rows))
+            eng.update_wants(rows, nw)
+            host["wants"][rows] = np.where(host["expiry_ns"][rows] == W.RELEASED, host["wants"][rows], nw)
+            W.add_store_sums(host)
+        if rnd == 4:  # upserts with another subclient count: explicit rows, non-uniform resources
+            rows = np.array([off[2] + 5, off[7] + 2, off[9] + 7, off[1] + 3])
+            ne = now + 100 * W.NS
+            eng.upsert(rows, np.zeros(4), np.ones(4), np.full(4, 3, np.int64), np.full(4, ne))
+            host["wants"][rows], host["has"][rows], host["subclients"][rows], host["expiry_ns"][rows] = 1.0, 0.0, 3, ne
+            W.add_store_sums(host)
+        eng.apportion(now, writeback=True, wb_columns=cols)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now)
+        assert_leases_match(host, gets, exp, ref, f"tick {rnd}")
+        live = ref["expiry_ns"] != W.RELEASED
+        host["has"] = np.where(live, ref["gets"], 0.0)
+        host["wants"] = np.where(live, host["wants"], 0.0)
+        host["subclients"] = np.where(live, host["subclients"], 0)
+        host["expiry_ns"] = ref["expiry_ns"].copy()
+        W.add_store_sums(host)
+        st = eng.read_store()
+        np.testing.assert_array_equal(st["subclients"], host["subclients"], err_msg=f"tick {rnd}")
+        np.testing.assert_array_equal(st["expiry_ns"], host["expiry_ns"], err_msg=f"tick {rnd}")
+        # expected dense resources: 257-1024 rows, every row live with one subclient count >= 1
+        want = 0
+        for r in np.flatnonzero(group):
+            s = host["subclients"][off[r]:off[r + 1]]
+            lv = host["expiry_ns"][off[r]:off[r + 1]] != W.RELEASED
+            want += int(lv.all() and s.min() == s.max() and 1 <= s[0] <= 254)
+        assert eng.store_stats()["dense_resources"] == want, f"tick {rnd}"
+    assert eng.store_stats()["dense_resources"] == 0  # every follower lapsed at the last tick
