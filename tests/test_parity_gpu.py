@@ -263,6 +263,35 @@ def test_c1_full_size_sampled(eng, kind):
     _sample_check(eng, snap, np.sort(rng.choice(10_000, 48, replace=False)), f"C1 kind={kind}")
 
 
+def test_c1_writeback_ticks_dense_sampled(eng):
+    """The bench's tick sequence at configs[1] size: back-to-back writeback ticks (from
+    the second tick on every resource is dense, its subclients column not read);
+    sampled resources match the oracle replaying the same ticks on a host copy."""
+    snap = W.c1()
+    eng.load(snap)
+    rng = np.random.default_rng(8)
+    resources = np.sort(rng.choice(10_000, 48, replace=False))
+    host = W.subset(snap, resources)
+    so = snap["seg_off"]
+    rows = np.concatenate([np.arange(so[r], so[r + 1]) for r in resources])
+    for t in range(3):
+        now = NOW + t * W.NS
+        eng.apportion(now, writeback=True)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now)
+        assert_leases_match(host, gets[rows], exp[rows], ref, f"C1 writeback tick {t}")
+        live = ref["expiry_ns"] != W.RELEASED
+        host["has"] = np.where(live, ref["gets"], 0.0)
+        host["wants"] = np.where(live, host["wants"], 0.0)
+        host["subclients"] = np.where(live, host["subclients"], 0)
+        host["expiry_ns"] = ref["expiry_ns"].copy()
+        W.add_store_sums(host)
+        if t == 0:
+            assert eng.store_stats()["dense_resources"] == 10_000
+    res = eng.resources()
+    assert_resources_match(host, {k: v[resources] for k, v in res.items()}, O.apportion(host, now), "C1 final")
+
+
 def test_c2_zipf_full_size_sampled(eng):
     """configs[2]: 1M resources, Zipf 1..1M clients, mixed kinds, 5% learning."""
     snap = W.c2()
