@@ -24,9 +24,16 @@ namespace dm {
 // Resource-per-group kernel: G threads (a wave or a 256-thread workgroup) own
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
-template <int G, int R>
+// MODE (the 128-thread bins only): kMixed = one kernel for every item (hint or not),
+// kDenseOnly = items whose hint is set (k_block_dense: no subclients column at all;
+// a stale hint queues the item for k_block_rest and returns), kRest = queued items
+// (k_block_rest: the column is read, the hint rewritten).
+enum { kMixed = 0, kDenseOnly = 1, kRest = 2 };
+template <int G, int R, int MODE = kMixed>
 __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, WorkItem* item, int t,
-                                              Lds<G>& lds, int32_t* general_list, int32_t* general_count) {
+                                              Lds<G>& lds, int32_t* general_list, int32_t* general_count,
+                                              int32_t* queue = nullptr, int32_t* qcount = nullptr,
+                                              int32_t qidx = 0) {
   constexpr bool kDense = G == 128;  // the dense-subclients path (below)
   const int seg = wi.seg;
   const int64_t lo = wi.lo;
@@ -53,8 +60,8 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // since that tick) reads the column after all.  Only the 128-thread blocks
   // (257-1024 rows) take this path: in the other group kernels the extra branch
   // costs registers they do not have (spills at 5 waves per SIMD; C2 +3.5 %).
-  const int hint = kDense ? wi.n >> 16 : 0;
-  if (!hint) {
+  const int hint = (kDense && MODE != kRest) ? wi.n >> 16 : 0;
+  if (MODE != kDenseOnly && !hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -75,7 +82,12 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     }
   }
   const Res rs = load_res(p, seg);
-  if (hint && dense_subclients(rs) != hint) {
+  if constexpr (MODE == kDenseOnly) {
+    if (dense_subclients(rs) != hint) {  // stale hint: k_block_rest reads the column
+      if (t == 0) queue[atomicAdd(qcount, 1)] = qidx;
+      return;
+    }
+  } else if (hint && dense_subclients(rs) != hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -89,7 +101,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   int64_t e[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) e[k] = rs.follow_exp;
-  if (any_explicit(rs)) {
+  if (MODE != kDenseOnly && any_explicit(rs)) {  // a dense resource has no explicit rows
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -145,7 +157,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     // root level), so the whole resource goes to k_general, untouched here.
     if (t == 0) {
       general_list[atomicAdd(general_count, 1)] = seg;
-      if (p.writeback && hint) item->n = n;  // k_general's writeback clears the byte
+      if (p.writeback && (wi.n >> 16)) item->n = n;  // k_general's writeback clears the byte
     }
     return;
   }
@@ -237,7 +249,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     const int dn =
         (kDense && p.writeback && nlive == n && a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
     write_resource(p, seg, rs, cl, delta.v, dn);
-    if (p.writeback && hint != dn) item->n = n | dn << 16;
+    if (p.writeback && (wi.n >> 16) != dn) item->n = n | dn << 16;
   }
 }
 
@@ -255,6 +267,46 @@ __global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevPa
   __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nitems) return;
   group_segment<G, R>(p, items[blockIdx.x], items + blockIdx.x, threadIdx.x, lds, general_list, general_count);
+}
+
+// The 128-thread bins split by the dense hint (launch_bin_split): k_block_dense
+// decides the items whose hint is set without the subclients column (70 VGPRs: 7
+// waves per SIMD instead of 5, 14336 rows in flight per CU) and queues the others;
+// k_block_rest decides the queue with the mixed body, a fixed grid striding over
+// it.  qcnt is a two-slot ring: this tick's count in qcnt[par], and k_block_rest
+// clears qcnt[par ^ 1] for the next tick (stream order); host_count (host-mapped)
+// tells the host how many items went to the queue (its choice of split or mixed).
+template <int R>
+__global__ __launch_bounds__(128) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
+                                                     int32_t* queue, int32_t* qcnt, int par,
+                                                     int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<128> lds;
+  if ((int)blockIdx.x >= nitems) return;
+  const WorkItem wi = items[blockIdx.x];
+  if ((wi.n >> 16) == 0) {
+    if (threadIdx.x == 0) queue[atomicAdd(qcnt + par, 1)] = (int32_t)blockIdx.x;
+    return;
+  }
+  group_segment<128, R, kDenseOnly>(p, wi, items + blockIdx.x, threadIdx.x, lds, general_list, general_count, queue,
+                                    qcnt + par, (int32_t)blockIdx.x);
+}
+
+template <int R>
+__global__ __launch_bounds__(128) void k_block_rest(DevParams p, WorkItem* __restrict__ items,
+                                                                    const int32_t* __restrict__ queue, int32_t* qcnt,
+                                                                    int par, int32_t* host_count,
+                                                                    int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<128> lds;
+  const int count = qcnt[par];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    qcnt[par ^ 1] = 0;
+    if (host_count) __hip_atomic_store(host_count, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  for (int q = blockIdx.x; q < count; q += gridDim.x) {
+    const int idx = queue[q];
+    group_segment<128, R, kRest>(p, items[idx], items + idx, threadIdx.x, lds, general_list, general_count);
+    __syncthreads();  // the next item reuses the single-use LDS slots
+  }
 }
 
 // One wave per resource (n <= 64 R), four independent waves per workgroup: wave
@@ -1871,6 +1923,24 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
   for (int k = 0; k < 5; ++k) blocks += (unsigned)sb.blocks[k];
   if (blocks == 0) return hipSuccess;
   k_subs<<<blocks, 256, 0, st>>>(p, sb, glist, gcount);
+  return hipGetLastError();
+}
+
+// The 128-thread bins (3: 128 x 4, 4: 128 x 8) split by the dense hint.
+hipError_t launch_bin_split(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt,
+                            int par, int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned rg = (unsigned)std::max(1, std::min(n, rest_grid));
+  if (bin == 3) {
+    k_block_dense<4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
+    k_block_rest<4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
+  } else if (bin == 4) {
+    k_block_dense<8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
+    k_block_rest<8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -21,6 +21,9 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
 hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
+hipError_t launch_bin_split(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt,
+                            int par, int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount,
+                            hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
@@ -183,6 +186,17 @@ struct dm_ctx {
   // the sub-wave bins in one launch (k_subs; DM_MERGE_SUBS=0: one launch per bin):
   // C2 tick 144-145 -> 138 us (tools/ab.py, both orders, one box)
   bool merge_subs = true;
+  // The 128-thread bins (3, 4) split by the dense hint (k_block_dense + k_block_rest)
+  // on a tick that follows a writeback tick (only those set hints), unless the last
+  // split tick the host has heard of queued more than a quarter of the bin's items
+  // for k_block_rest (then every 64th tick tries again: C2's bins, whose resources
+  // keep released rows, run 21 % slower split).  DM_DENSE_SPLIT=0: never split.
+  bool dense_split = true;
+  DBuf<int32_t> dq_list[2], dq_cnt[2];
+  int dq_par[2] = {0, 0};
+  int dq_skip[2] = {0, 0};   // ticks in the one-kernel form since the split was last tried
+  int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
+  int32_t* d_dq = nullptr;
   int fused_G = 512;
   bool fused_ok = false;       // every large resource within the co-residency bound
   int64_t fused_max_chunks = 0, fused_cap = 0;
@@ -277,6 +291,13 @@ struct dm_ctx {
     if (h_ferr) (void)hipHostFree(h_ferr);
     h_ferr = nullptr;
     d_ferr = nullptr;
+    for (int i = 0; i < 2; ++i) {
+      dq_list[i].release();
+      dq_cnt[i].release();
+    }
+    if (h_dq) (void)hipHostFree(h_dq);
+    h_dq = nullptr;
+    d_dq = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
     pa_nan.release(); pa_live.release(); p_tot.release();
@@ -429,6 +450,19 @@ static int upload_plan(dm_ctx* c) {
     c->fused_ok = c->fused_max_chunks > 0 && 2 * c->fused_max_chunks <= c->fused_cap &&
                   c->fused_max_chunks <= c->fused_G;  // the last arriver loads one record per thread
   }
+  if (!c->h_dq) {
+    DM_HIP(c, hipHostMalloc((void**)&c->h_dq, 2 * sizeof(int32_t), hipHostMallocMapped), "dense split word");
+    DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_dq, c->h_dq, 0), "dense split word");
+  }
+  for (int i = 0; i < 2; ++i) {  // the dense split of bins 3 and 4: rest queues and their two-slot counters
+    __atomic_store_n(c->h_dq + i, 0, __ATOMIC_RELAXED);
+    c->dq_skip[i] = 0;
+    const size_t nb = std::max<size_t>(c->h_bins[3 + i].size(), 1);
+    DM_HIP(c, c->dq_list[i].ensure(nb), "dense split queue");
+    DM_HIP(c, c->dq_cnt[i].ensure(2), "dense split queue");
+    DM_HIP(c, hipMemsetAsync(c->dq_cnt[i].p, 0, 2 * sizeof(int32_t), st), "dense split queue");
+    c->dq_par[i] = 0;
+  }
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
   DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
@@ -533,6 +567,7 @@ int dm_create(int device, dm_ctx** out) {
   dm_ctx* c = new dm_ctx();
   c->device = device;
   if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
+  if (const char* ds = getenv("DM_DENSE_SPLIT")) c->dense_split = atoi(ds) != 0;
   if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
     for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
@@ -884,6 +919,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                       [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
   }
+  // the 128-thread bins split by the dense hint after a writeback tick (hints set)
+  const bool split_dense = c->have_result && c->last_writeback;
   // the sub-wave bins (8x2, 16x2, 16x4, 32x4, 64x4) in one launch on bin 0's stream
   static constexpr int kSubBins[5] = {7, 8, 0, 1, 2}, kSubG[5] = {8, 16, 16, 32, 64};
   const bool merge_subs = c->merge_subs;
@@ -908,6 +945,21 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     if (n == 0) continue;
     if (merge_subs && (b == 7 || b == 8 || b <= 2)) continue;
     hipStream_t s = cls_stream(b);
+    if ((b == 3 || b == 4) && c->dense_split && split_dense) {
+      // only a writeback tick sets hints, so the split form follows one
+      const int i = b - 3, par = c->dq_par[i];
+      const int64_t queued = __atomic_load_n(c->h_dq + i, __ATOMIC_RELAXED);
+      if (4 * queued <= n || ++c->dq_skip[i] >= 64) {
+        c->dq_skip[i] = 0;
+        DM_HIP(c, timed(KC_BIN0 + b, s, [&] {
+                 return launch_bin_split(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
+                                         2048, gl, gc, s);
+               }),
+               "group kernel (dense split)");
+        c->dq_par[i] ^= 1;
+        continue;
+      }
+    }
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }),
            "group kernel");
   }

@@ -793,13 +793,19 @@ def test_config_limits_and_cold_fields_round_trip(eng):
     assert e.value.code == DM_E_INVAL
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("cols", ["inplace", "alternate"])
-def test_dense_subclients_state(eng, cols):
+def test_dense_subclients_state(monkeypatch, cols, split):
     """A writeback tick marks a group-kernel resource dense when every row is a live
     follower with one subclient count; the next ticks skip its subclients column.
     Releases, upserts (other subclient counts, explicit expiries) and lapsed
     followers end the state, wants refreshes keep it; every tick matches the oracle
-    on a host copy, and dm_store_stats counts the dense resources."""
+    on a host copy, and dm_store_stats counts the dense resources.  split=1: after a
+    writeback tick the 128-thread bins run as k_block_dense + k_block_rest (stale
+    hints queued); split=0 (DM_DENSE_SPLIT=0): the one-kernel form."""
+    from doorman_amd.engine import Engine
+    monkeypatch.setenv("DM_DENSE_SPLIT", split)  # read when the context is created
+    eng = Engine(0)
     rng = np.random.default_rng(5150)
     sizes = np.array([12, 30, 60, 100, 200, 400, 900, 1000, 1500, 3000, 5, 0, 9000, 20, 700])
     snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=0.0, learning_frac=0.0,
@@ -852,3 +858,4 @@ def test_dense_subclients_state(eng, cols):
             want += int(lv.all() and s.min() == s.max() and 1 <= s[0] <= 254)
         assert eng.store_stats()["dense_resources"] == want, f"tick {rnd}"
     assert eng.store_stats()["dense_resources"] == 0  # every follower lapsed at the last tick
+    eng.close()

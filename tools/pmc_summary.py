@@ -17,6 +17,8 @@ import sys
 
 CLASS = [
     # template args <G, R[, BATCH]>: BATCH 2 is the HBM-streaming variant of the same bin
+    (r"k_block_dense<4>", "block128x4"), (r"k_block_dense<8>", "block128x8"),
+    (r"k_block_rest<4>", "block128x4_rest"), (r"k_block_rest<8>", "block128x8_rest"),
     (r"k_block<128, 4(, \d)?>", "block128x4"), (r"k_block<128, 8(, \d)?>", "block128x8"), (r"k_block<256, 2(, \d)?>", "block256x2"), (r"k_block<256, 4(, \d)?>", "block256x4"),
     (r"k_block<256, 8(, \d)?>", "block256x8"), (r"k_block<512, 8(, \d)?>", "block512x8"), (r"k_block<512, 4(, \d)?>", "block512x4"), (r"k_block<1024, 4(, \d)?>", "block1024x4"),
     (r"k_wave<4(, \d)?>", "wave64x4"), (r"k_sub<16, 4>", "sub16x4"), (r"k_sub<32, 4>", "sub32x4"),
@@ -91,6 +93,13 @@ def main(d, w):
         wv = write.get((c, "WRITE_SIZE"), 0.0)
         out[c] = {"fetch_kb": v, "write_kb": wv, "avg_us": stats.get(c, {}).get("avg_us"),
                   "hbm_bytes_per_launch": v * 1024 * read_cal + wv * 1024 * write_cal}
+    # a split bin (k_block_dense + k_block_rest, one launch each per tick): the
+    # class's bytes per tick include its rest kernel's
+    for c in [k for k in out if k.endswith("_rest")]:
+        base = c[: -len("_rest")]
+        if base in out:
+            out[base]["hbm_bytes_per_launch_dense_kernel"] = out[base]["hbm_bytes_per_launch"]
+            out[base]["hbm_bytes_per_launch"] += out[c]["hbm_bytes_per_launch"]
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
     with open(os.path.join(root, "profiles", f"pmc_{w}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
