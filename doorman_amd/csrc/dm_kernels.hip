@@ -273,7 +273,8 @@ __global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevPa
 // decides the items whose hint is set without the subclients column (70 VGPRs: 7
 // waves per SIMD instead of 5, 14336 rows in flight per CU) and queues the others;
 // k_block_rest decides the queue with the mixed body, a fixed grid striding over
-// it.  qcnt is a two-slot ring: this tick's count in qcnt[par], and k_block_rest
+// it (512 workgroups: the queue is short whenever the host picks this form, and
+// empty for a store of dense resources, where the launch costs ~4 us).  qcnt is a two-slot ring: this tick's count in qcnt[par], and k_block_rest
 // clears qcnt[par ^ 1] for the next tick (stream order); host_count (host-mapped)
 // tells the host how many items went to the queue (its choice of split or mixed).
 template <int R>

@@ -953,7 +953,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
         c->dq_skip[i] = 0;
         DM_HIP(c, timed(KC_BIN0 + b, s, [&] {
                  return launch_bin_split(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
-                                         2048, gl, gc, s);
+                                         512, gl, gc, s);
                }),
                "group kernel (dense split)");
         c->dq_par[i] ^= 1;
