@@ -263,10 +263,12 @@ def test_c1_full_size_sampled(eng, kind):
     _sample_check(eng, snap, np.sort(rng.choice(10_000, 48, replace=False)), f"C1 kind={kind}")
 
 
-def test_c1_writeback_ticks_dense_sampled(eng):
+@pytest.mark.parametrize("recompute", [False, True])
+def test_c1_writeback_ticks_dense_sampled(eng, recompute):
     """The bench's tick sequence at configs[1] size: back-to-back writeback ticks (from
     the second tick on every resource is dense, its subclients column not read);
-    sampled resources match the oracle replaying the same ticks on a host copy."""
+    sampled resources match the oracle replaying the same ticks on a host copy, with
+    the store's running sums or with sums rebuilt from the rows (DM_AGG_RECOMPUTE)."""
     snap = W.c1()
     eng.load(snap)
     rng = np.random.default_rng(8)
@@ -276,10 +278,10 @@ def test_c1_writeback_ticks_dense_sampled(eng):
     rows = np.concatenate([np.arange(so[r], so[r + 1]) for r in resources])
     for t in range(3):
         now = NOW + t * W.NS
-        eng.apportion(now, writeback=True)
+        eng.apportion(now, writeback=True, recompute=recompute)
         gets, exp = eng.leases()
         ref = O.apportion(host, now)
-        assert_leases_match(host, gets[rows], exp[rows], ref, f"C1 writeback tick {t}")
+        assert_leases_match(host, gets[rows], exp[rows], ref, f"C1 writeback tick {t} recompute={recompute}")
         live = ref["expiry_ns"] != W.RELEASED
         host["has"] = np.where(live, ref["gets"], 0.0)
         host["wants"] = np.where(live, host["wants"], 0.0)
