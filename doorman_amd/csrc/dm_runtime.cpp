@@ -154,6 +154,7 @@ struct dm_ctx {
   DBuf<int64_t> out_expiry;
   DBuf<ResAgg> res;
   bool last_writeback = false, have_result = false;
+  int64_t seg_uniform = 0;  // rows per resource when every resource has the same count, else 0
   // A forked tick's work classes run on the auxiliary streams.  Normally they are
   // joined back into the context stream at the end of the tick; with DM_DEFER_JOIN
   // the join waits for the next library call that needs it (each cross-queue hop
@@ -705,6 +706,13 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   c->R = R;
   c->N = N;
   c->h_seg_off.assign(s->seg_off, s->seg_off + R + 1);
+  c->seg_uniform = 0;  // every resource the same number of rows (a hierarchy root store: G)
+  if (R > 0) {
+    const int64_t g = s->seg_off[1] - s->seg_off[0];
+    bool same = g > 0 && s->seg_off[0] == 0;
+    for (int64_t r = 1; r < R && same; ++r) same = s->seg_off[r + 1] - s->seg_off[r] == g;
+    c->seg_uniform = same ? g : 0;
+  }
   hipStream_t st = c->stream;
   DM_HIP(c, upload(c->seg_off, s->seg_off, (size_t)R + 1, st), "upload seg_off");
   {  // RowIndex: resource of the first row of every 2^kRowBlkShift-row block
@@ -1529,11 +1537,8 @@ int dm_publish_totals(dm_ctx* c, void* dst) {
   return DM_OK;
 }
 
-static bool root_layout_ok(dm_ctx* c, int G) {
-  if (G <= 0 || G > kHierMaxServers || c->R <= 0 || c->N != c->R * (int64_t)G) return false;
-  for (int64_t r = 0; r <= c->R; ++r)
-    if (c->h_seg_off[r] != r * (int64_t)G) return false;
-  return true;
+static bool root_layout_ok(dm_ctx* c, int G) {  // checked at load (seg_uniform), not per round
+  return G > 0 && G <= kHierMaxServers && c->R > 0 && c->N == c->R * (int64_t)G && c->seg_uniform == G;
 }
 
 // One exchange round of the hierarchy (server.go:227-323 -> :822-901): validate
