@@ -97,8 +97,11 @@ def exchange_all(L, roots, leaves, gathered, G, now):
         e.sync()
 
 
+@pytest.mark.parametrize("clients", [0, 600])
 @pytest.mark.parametrize("G", [1, 2, 3, 8, 20])
-def test_hierarchy_rounds_match_the_reference_model(G):
+def test_hierarchy_rounds_match_the_reference_model(G, clients):
+    """clients = 0: 3-119 clients per leaf resource; 600: every leaf resource on the
+    128-thread kernels, dense (and split) from its second writeback tick."""
     import torch
     from doorman_amd import _lib
     from doorman_amd.engine import Engine
@@ -109,7 +112,8 @@ def test_hierarchy_rounds_match_the_reference_model(G):
     rcfg = root_config(R, rng)
     leaves, tpl = [], []
     for g in range(G):
-        s = W.uniform(R, int(rng.integers(3, 120)), kind=W.FAIR_SHARE, seed=10 * G + g, capacity=1000.0)
+        s = W.uniform(R, clients or int(rng.integers(3, 120)), kind=W.FAIR_SHARE, seed=10 * G + g,
+                      capacity=1000.0)
         s["wants"] *= rng.uniform(0.2, 3.0)  # servers differ in appetite
         W.add_store_sums(s)
         cfg = M.default_config(R, np.where(rng.random(R) < 0.1, NOW + 2 * W.NS, W.INT64_MIN))
@@ -152,6 +156,9 @@ def test_hierarchy_rounds_match_the_reference_model(G):
             so = pre[g]["seg_off"]
             refresh_row = np.repeat(tpl[g]["refresh_interval_s"], np.diff(so))
             np.testing.assert_array_equal(ref_s[live], refresh_row[live])  # the root's refresh interval
+            if clients and t < 3:  # every leaf resource dense after a writeback tick until the
+                # last round, where the 20-s default template's followers lapse
+                assert leaves[g].store_stats()["dense_resources"] == R, f"G={G} round {t} leaf {g}"
     for e in leaves + roots:
         e.close()
 
