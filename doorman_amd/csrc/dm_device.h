@@ -129,6 +129,7 @@ struct FusedState {
   uint32_t* err;     // host-mapped word: a bounded wait gave up (residency bound violated)
   int32_t nchunks;
   uint32_t epoch;    // launch number, never 0: the value a phase's flag takes when its totals are out
+  uint32_t spin_limit;  // polls (s_sleep 8 each) before a wait gives up
 };
 
 // row -> resource lookup for store updates: seg_off plus, for every block of
@@ -201,11 +202,14 @@ struct DevParams {
   int32_t writeback;  // rows become followers / released in the store; out_expiry unused
 };
 
-// dm_decide: one resource and its requests [qlo, qhi) (sorted by row)
+// dm_decide: one resource and its requests [qlo, qhi) in the caller's order; the
+// resource's rows are copied to scratch rows [scr, scr + n) that take each
+// decision's Assign before the next request is decided
 struct ReqItem {
   int32_t seg;
   int32_t pad;
   int64_t qlo, qhi;
+  int64_t scr;
 };
 struct ReqArgs {
   const int64_t* rows;  // the row the request's lease is written to (its client's row, or a free row)
@@ -214,6 +218,10 @@ struct ReqArgs {
   const int64_t* sub;
   double* gets;
   int64_t* expiry;
+  // the round's working copy of the requested resources' rows (store.Assign target)
+  double* sc_has;
+  double* sc_wants;
+  int32_t* sc_sub;  // subclients of a live row, -1 for a row absent after Clean
 };
 
 // dm_hier_root_tick: one exchange round of the hierarchy's root (k_hier_tick)

@@ -1673,19 +1673,27 @@ __global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ ga
   if (f) atomicOr(&status[i / R], f);
 }
 
-// One exchange round of the root, decided literally: every requesting server's
-// request {has 0 (the intermediate never fills Has, server.go:244,873), wants
-// SumWants_g, subclients Count_g} is decided by Resource.Decide against the root
-// store as it was before the round (resource.go:100-113: Clean, then Learn or
-// the algorithm, algorithm.go:95-302 with the request's own values), then all of
-// the round's leases are assigned (store.go:153-167).  Servers that do not
-// request keep their root lease until Clean expires it.  The running sums follow
-// the reference's own update sequence -- Clean's releases in row order, then one
-// Assign per request in server order -- so they equal a sequential replay of the
-// round bit for bit.
+// One exchange round of the root.  The requests of the servers that ask for a
+// resource -- {has 0 (the intermediate never fills Has, server.go:244,873), wants
+// SumWants_g, subclients Count_g} -- are decided by Resource.Decide one after
+// another in server order, as the root's res.mu serialises the GetServerCapacity
+// calls (resource.go:103-104): Clean once (resource.go:106, store.go:169-181;
+// nothing else expires within the round), then per request Learn or the algorithm
+// (algorithm.go:95-302, with the request's own values for its server) against
+// the store as the Assigns of the earlier requests left it, then its Assign
+// (store.go:153-167: the row and the running sums).  So the root never grants
+// more than the reference would: a FairShare resource with capacity C and G
+// servers that each want C grants C, 0, ... in the first round, not G x C.
+// Servers that do not request keep their root lease until Clean expires it.  The
+// running sums follow the reference's update sequence -- Clean's releases in row
+// order, then one Assign per request in server order -- bit for bit.
 //
-// G <= 64 servers: a wave holds 64/G whole resources, one lane per server row;
-// every lane loops over its resource's rows by shuffles (O(G) per request).
+// G <= 64 servers: a wave holds 64 / P whole resources (P = G rounded up to a
+// power of two), one lane per server row.  For each server q in order, the lanes
+// of a resource walk its rows in row order by shuffles for the decision's loops
+// over store.Map (round 1, round 2, ProportionalShare's extra capacity / need:
+// the sums of a sequential Map, bit for bit the oracle's); lane q then takes the
+// Assign.  O(G) per decision, G decisions per resource.
 // The lane of `ha.server` then loads that server's template for each resource
 // exactly as performRequests + LoadConfig do (server.go:279-313,
 // resource.go:117-125): a requested resource takes the root's grant as capacity,
@@ -1696,13 +1704,15 @@ __global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ ga
 // 1 s, no parent expiry).  learningModeEndTime is kept (set once, resource.go:163).
 __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   const int G = ha.G;
-  const int per = 64 / G;  // resources per wave
+  const int P = G <= 1 ? 1 : 1 << (32 - __builtin_clz((unsigned)(G - 1)));
+  const int per = 64 / P;  // resources per wave
   const int lane = threadIdx.x & 63;
-  const int rl = lane / G, g = lane - rl * G;
-  const int64_t r = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * per + rl;
-  if (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * per >= ha.R) return;  // whole waves only
-  const bool valid = rl < per && r < ha.R;
-  const int64_t rr = valid ? r : 0;
+  const int rl = lane / P, g = lane - rl * P;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r = wave * per + rl;
+  if (wave * per >= ha.R) return;  // whole waves only
+  const bool valid = g < G && r < ha.R;
+  const int64_t rr = r < ha.R ? r : 0;
   const int64_t row = rr * G + (valid ? g : 0);
   double w = 0.0, h = 0.0, rw = 0.0;
   int s = 0, rs = 0;
@@ -1721,11 +1731,10 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     rs = req ? (int)__double_as_longlong(v.y) : 0;
   }
   const bool released = e == kReleased;
-  const bool live = valid && !released && !(p.now > e);     // present after Clean (store.go:174)
-  const bool expired = valid && !released && (p.now > e);   // released by this round's Clean
-  const int base = rl * G;                                  // first lane of this resource
-  const int sl = live ? s : ~s;                             // subclients + live bit (s >= 0)
-  auto src = [&](int q) { const int j = base + q; return j < 64 ? j : 63; };
+  bool live = valid && !released && !(p.now > e);          // present after Clean (store.go:174)
+  const bool expired = valid && !released && (p.now > e);  // released by this round's Clean
+  const int base = rl * P;                                 // first lane of this resource
+  auto src = [&](int q) { return base + q; };
 
   // Clean on the running sums, in row order (store.go:169-181 -> :142-151)
   long long count = rs_cfg.agg_count;
@@ -1742,97 +1751,125 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       }
     }
   }
+  if (!live) {  // this row is absent from the store the round starts with
+    h = 0.0;
+    w = 0.0;
+    s = 0;
+  }
 
-  // Decide (algorithm.go) for this lane's request against the cleaned store
   const double C = rs_cfg.C;
-  const double old_h = live ? h : 0.0;  // store.Get: the zero Lease when absent
-  const int old_s = live ? s : 0;
   const bool ps = !rs_cfg.learning && rs_cfg.kind == 2;
-  double gets = 0.0;
-  double eq = 0.0, ds = 0.0, avail = 0.0;
-  bool loop1 = false;
-  if (req) {
-    if (rs_cfg.learning) {
-      gets = 0.0;  // Learn: the request's Has (never filled by an intermediate)
-    } else if (rs_cfg.kind == 0) {
-      gets = rw;
-    } else if (rs_cfg.kind == 1) {
-      gets = minF(C, rw);
-    } else if (ps) {
-      const long long cnt = count + (live ? 0 : rs);  // :217-225
-      eq = C / (double)cnt;                            // :229
-      ds = eq * (double)rs;                            // :233 equalSharePerClient
-      avail = C - sh + old_h;                          // :239 unusedCapacity
-      if (sw <= C || rw <= ds) gets = minF(rw, avail);  // :245
-      else loop1 = true;
-    } else {
-      const long long cnt = count - old_s + rs;  // :115
-      avail = C - sh + old_h;                    // :120
-      eq = C / (double)cnt;                      // :123
-      ds = eq * (double)rs;                      // :126
-      if (rw <= ds) gets = minF(rw, avail);      // :131
-      else loop1 = true;
-    }
-  }
-  double x = 0.0, y = 0.0;
-  long long wx = rs;  // FairShare wantExtra starts at the request's subclients (:148)
-  if (__any(loop1)) {
-    for (int q = 0; q < G; ++q) {
-      const double wj = shfl_d(w, src(q));
-      const int sj = shfl_i(sl, src(q));
-      if (!loop1 || sj < 0) continue;  // absent rows are not in the store's Map
-      if (ps) {  // store.Map with this client's own request values (:259-279)
-        const double wv = (q == g) ? rw : wj;
-        const int sv = (q == g) ? rs : sj;
-        const double esp = eq * (double)sv;  // :273
-        if (wv < esp)
-          x += esp - wv;  // :275
-        else
-          y += wv - esp;  // :277
-      } else if (q != g) {  // FairShare round 1, this client skipped (:156-171)
-        const double d = (double)sj * eq;  // :160
-        if (wj < d)
-          x += d - wj;  // :164
-        else if (wj > d)
-          wx += sj;  // :168
+  const int rq = req ? 1 : 0;
+  double my_gets = 0.0;
+  for (int q = 0; q < G; ++q) {
+    const int rq_q = shfl_i(rq, src(q));
+    if (!__any(rq_q)) continue;  // no resource of this wave has server q's request
+    const double rw_q = shfl_d(rw, src(q));
+    const int rs_q = shfl_i(rs, src(q));
+    const int live_q = shfl_i(live ? 1 : 0, src(q));
+    const double old_h = shfl_d(h, src(q)), old_w = shfl_d(w, src(q));  // store.Get: zero when absent
+    const int old_s = shfl_i(s, src(q));
+    // Decide (algorithm.go) for server q's request against the store as it is now
+    double gets = 0.0, eq = 0.0, ds = 0.0, avail = 0.0;
+    bool loop1 = false;
+    if (rq_q) {
+      if (rs_cfg.learning) {
+        gets = 0.0;  // Learn: the request's Has (never filled by an intermediate)
+      } else if (rs_cfg.kind == 0) {
+        gets = rw_q;
+      } else if (rs_cfg.kind == 1) {
+        gets = minF(C, rw_q);
+      } else if (ps) {
+        const long long cnt = count + (live_q ? 0 : rs_q);  // :217-225
+        eq = C / (double)cnt;                               // :229
+        ds = eq * (double)rs_q;                             // :233 equalSharePerClient
+        avail = C - sh + old_h;                             // :239 unusedCapacity
+        if (sw <= C || rw_q <= ds) gets = minF(rw_q, avail);  // :245
+        else loop1 = true;
+      } else {
+        const long long cnt = count - old_s + rs_q;  // :115
+        avail = C - sh + old_h;                      // :120
+        eq = C / (double)cnt;                        // :123
+        ds = eq * (double)rs_q;                      // :126
+        if (rw_q <= ds) gets = minF(rw_q, avail);    // :131
+        else loop1 = true;
       }
     }
-  }
-  bool loop2 = false;
-  double dE = 0.0, T = 0.0;
-  if (loop1) {
-    if (ps) {
-      gets = minF(ds + (rw - ds) * (x / y), avail);  // :283,290
-    } else {
-      dE = (x / (double)wx) * (double)rs;  // :175
-      if (rw < ds + dE) gets = minF(rw, avail);  // :179
-      else {
-        T = dE + ds;  // :197 deservedExtra + deservedShare
-        loop2 = true;
+    if (__any(loop1)) {
+      // store.Map over the rows in row order (absent rows are not in the map)
+      const int sl = live ? s : ~s;  // subclients + live bit (s >= 0)
+      double x = 0.0, y = 0.0;
+      long long wx = rs_q;  // FairShare wantExtra starts at the request's subclients (:148)
+      for (int j = 0; j < G; ++j) {
+        const double wj = shfl_d(w, src(j));
+        const int sj = shfl_i(sl, src(j));
+        if (!loop1 || sj < 0) continue;
+        if (ps) {  // with server q's own request values for its row (:259-279)
+          const double wv = (j == q) ? rw_q : wj;
+          const int sv = (j == q) ? rs_q : sj;
+          const double esp = eq * (double)sv;  // :273
+          if (wv < esp)
+            x += esp - wv;  // :275
+          else
+            y += wv - esp;  // :277
+        } else if (j != q) {  // FairShare round 1, the requesting server skipped (:156-171)
+          const double d = (double)sj * eq;  // :160
+          if (wj < d)
+            x += d - wj;  // :164
+          else if (wj > d)
+            wx += sj;  // :168
+        }
+      }
+      bool loop2 = false;
+      double dE = 0.0, T = 0.0;
+      if (loop1) {
+        if (ps) {
+          gets = minF(ds + (rw_q - ds) * (x / y), avail);  // :283,290
+        } else {
+          dE = (x / (double)wx) * (double)rs_q;  // :175
+          if (rw_q < ds + dE) gets = minF(rw_q, avail);  // :179
+          else {
+            T = dE + ds;  // :197 deservedExtra + deservedShare
+            loop2 = true;
+          }
+        }
+      }
+      if (__any(loop2)) {
+        double ee = 0.0;
+        long long wee = rs_q;  // :189
+        for (int j = 0; j < G; ++j) {
+          const double wj = shfl_d(w, src(j));
+          const int sj = shfl_i(sl, src(j));
+          if (!loop2 || sj < 0 || j == q) continue;
+          if (!(wj > (double)sj * eq)) continue;  // wantExtraClients (:165-169)
+          if (wj < T)
+            ee += T - wj;  // :197-198
+          else if (wj > T)
+            wee += sj;  // :199-200
+        }
+        if (loop2) gets = minF(ds + dE + (ee / (double)wee) * (double)rs_q, avail);  // :203-204
       }
     }
-  }
-  if (__any(loop2)) {
-    double ee = 0.0;
-    long long wee = rs;  // :189
-    for (int q = 0; q < G; ++q) {
-      const double wj = shfl_d(w, src(q));
-      const int sj = shfl_i(sl, src(q));
-      if (!loop2 || sj < 0 || q == g) continue;
-      if (!(wj > (double)sj * eq)) continue;  // wantExtraClients (:165-169)
-      if (wj < T)
-        ee += T - wj;  // :197-198
-      else if (wj > T)
-        wee += sj;  // :199-200
+    // Assign (store.go:153-167): the running sums, and server q's row
+    if (rq_q) {
+      sh += gets - old_h;
+      sw += rw_q - old_w;
+      count += rs_q - old_s;
+      if (g == q) {
+        h = gets;
+        w = rw_q;
+        s = rs_q;
+        live = true;
+        my_gets = gets;
+      }
     }
-    if (loop2) gets = minF(ds + dE + (ee / (double)wee) * (double)rs, avail);  // :203-204
   }
 
-  // Assign the round's leases (store.go:153-167) and the running sums, in server order
+  // the round's rows: the requests' leases, and the rows this round's Clean released
   const int64_t exp_new = rs_cfg.exp_out;
   if (valid) {
     if (req) {  // the root store is written in place (out_* alias its columns)
-      p.out_gets[row] = gets;
+      p.out_gets[row] = my_gets;
       p.out_wants[row] = rw;
       p.out_sub[row] = (int32_t)((uint32_t)rs | kSubExplicit);
       p.out_expiry[row] = exp_new;
@@ -1841,19 +1878,6 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       p.out_wants[row] = 0.0;
       p.out_sub[row] = (int32_t)kSubReleased;
       p.out_expiry[row] = kReleased;
-    }
-  }
-  const int rq = req ? 1 : 0;
-  for (int q = 0; q < G; ++q) {
-    const int rj = shfl_i(rq, src(q));
-    const double gj = shfl_d(gets, src(q)), rwj = shfl_d(rw, src(q));
-    const int rsj = shfl_i(rs, src(q));
-    const double ohj = shfl_d(old_h, src(q)), owj = shfl_d(live ? w : 0.0, src(q));
-    const int osj = shfl_i(old_s, src(q));
-    if (rj) {
-      sh += gj - ohj;
-      sw += rwj - owj;
-      count += rsj - osj;
     }
   }
   if (valid && g == 0) {
@@ -1874,7 +1898,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       const ResCfg rc = p.cfg[rr];
       const ResCold rcc = ha.root_cold[rr];
       const int64_t sec = exp_new >= 0 ? exp_new / kNs : -((-exp_new + kNs - 1) / kNs);  // time.Unix(sec, 0)
-      c->capacity = gets;                                                  // :293
+      c->capacity = my_gets;                                               // :293
       cc->safe_capacity = __builtin_isnan(rcc.safe_capacity) ? 0.0 : rcc.safe_capacity;  // :294, :894
       c->lease_len_s = rc.lease_len_s;                                     // :295 Algorithm
       cc->refresh_s = rcc.refresh_s;
@@ -2054,7 +2078,9 @@ hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t
 
 hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st) {
   if (ha.R <= 0) return hipSuccess;
-  const int64_t per = 64 / ha.G;
+  int P = 1;
+  while (P < ha.G) P <<= 1;
+  const int64_t per = 64 / P;
   const int64_t waves = (ha.R + per - 1) / per;
   k_hier_tick<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(p, ha);
   return hipGetLastError();

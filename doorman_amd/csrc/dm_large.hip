@@ -31,7 +31,10 @@
 // this kernel only when every large resource has at most half that many chunks
 // and at most G (one record per thread of the last arriver; dm_runtime.cpp); every
 // wait is bounded and a wait that gives up sets a host-visible error word (the tick
-// then reports DM_E_HIP) instead of hanging.
+// then reports DM_E_HIP) instead of hanging.  A chunk whose wait gave up writes
+// nothing after it, but other chunks may already have written their leases, so
+// after such a writeback tick the host treats the store as lost until it is
+// loaded again (dm_runtime.cpp, check_fused).
 #include <hip/hip_runtime.h>
 
 #include "dm_kernel_util.h"
@@ -39,7 +42,6 @@
 namespace dm {
 
 constexpr int kFR = kFusedRows;  // rows per thread held in VGPRs
-constexpr uint32_t kSpinLimit = 1u << 21;  // x s_sleep 8 (~512 clocks): ~0.4 s, far beyond any real wait
 
 __device__ __forceinline__ uint64_t bits(double d) { return __builtin_bit_cast(uint64_t, d); }
 __device__ __forceinline__ uint64_t bits(long long i) { return (uint64_t)i; }
@@ -86,16 +88,17 @@ __device__ __forceinline__ AggC load_c(const uint64_t* r) { return AggC{dbl(ld_w
 
 __device__ __forceinline__ int flag_at(int phase) { return 32 + phase * kFusedFlagCopies * 32; }
 
-// Bounded poll of one flag word by one lane.
-__device__ __forceinline__ void wait_flag(uint32_t* flag, uint32_t epoch, uint32_t* err) {
+// Bounded poll of one flag word by one lane; false when it gave up.
+__device__ __forceinline__ bool wait_flag(uint32_t* flag, uint32_t epoch, uint32_t limit, uint32_t* err) {
   for (uint32_t spins = 0; __hip_atomic_load((gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;
        ++spins) {
-    if (spins > kSpinLimit) {
+    if (spins >= limit) {
       __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
+      return false;
     }
     __builtin_amdgcn_s_sleep(8);
   }
+  return true;
 }
 
 // Last arriver, wave 0: publish the totals record (lane 0 stored it), then every
@@ -133,8 +136,10 @@ __device__ __forceinline__ AggC all_reduce_c(const FusedState& F, const LargeSeg
 // One exchange of a phase: lane 0 has stored this chunk's record; returns (to every
 // thread) after the resource's totals words [w0, w1) are in xt.  The last arriver
 // reduces and publishes them (reduce(), then its flag); the others poll the flag.
+// Returns false (uniformly) when the poll gave up: the chunk must then write
+// nothing more (the host reports the tick as failed and the store as unusable).
 template <int G, typename Reduce>
-__device__ __forceinline__ void exchange(uint32_t* ctr, uint32_t* flags, int ci, const FusedState& F, int nch,
+__device__ __forceinline__ bool exchange(uint32_t* ctr, uint32_t* flags, int ci, const FusedState& F, int nch,
                                          uint64_t* trec, uint64_t* xt, uint32_t* xl, int w0, int w1, Reduce reduce) {
   if (threadIdx.x < 64) {
     const bool last = arrive_last(ctr, nch);
@@ -145,12 +150,13 @@ __device__ __forceinline__ void exchange(uint32_t* ctr, uint32_t* flags, int ci,
     reduce();  // every thread; lane 0 stores the totals words write-through
     if (threadIdx.x < 64) publish_flag(flags, F.epoch);
   } else if (threadIdx.x == 0) {
-    wait_flag(flags + (ci % kFusedFlagCopies) * 32, F.epoch, F.err);
+    if (!wait_flag(flags + (ci % kFusedFlagCopies) * 32, F.epoch, F.spin_limit, F.err)) *xl = 2u;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: loads stay below the poll
   }
   if (threadIdx.x == 0)
     for (int i = w0; i < w1; ++i) xt[i] = ld_wt(trec + i);
   __syncthreads();
+  return *xl != 2u;
 }
 
 __device__ __forceinline__ AggA xt_a(const uint64_t* xt) {
@@ -282,15 +288,16 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
   SegState st;
   AggB tb{0.0, 0.0, 0};
   if (need_tot) {
-    exchange<G>(sy + 0, sy + flag_at(0), ci, F, nch, trec, xt, &xl[0], 0, 11, [&] {  // pass-A (and speculative B) totals
-      const AggA ta = all_reduce_a<G>(p, F, L, lds);
-      const AggB sb2 = spec ? all_reduce_b<G>(F, L, lds) : AggB{0.0, 0.0, 0};
-      if (t == 0) {
-        store_a(trec, ta);
-        store_b(trec, sb2);
-        if (seg_state_of(p, ch.seg, ta).general) general_list[atomicAdd(general_count, 1)] = ch.seg;  // k_general
-      }
-    });
+    if (!exchange<G>(sy + 0, sy + flag_at(0), ci, F, nch, trec, xt, &xl[0], 0, 11, [&] {  // pass-A (and speculative B) totals
+          const AggA ta = all_reduce_a<G>(p, F, L, lds);
+          const AggB sb2 = spec ? all_reduce_b<G>(F, L, lds) : AggB{0.0, 0.0, 0};
+          if (t == 0) {
+            store_a(trec, ta);
+            store_b(trec, sb2);
+            if (seg_state_of(p, ch.seg, ta).general) general_list[atomicAdd(general_count, 1)] = ch.seg;  // k_general
+          }
+        }))
+      return;
     st = seg_state_of(p, ch.seg, xt_a(xt));
     tb = AggB{dbl(xt[8]), dbl(xt[9]), (long long)xt[10]};
     if (st.general) return;  // heterogeneous-subclient FairShare: k_general decides the resource
@@ -320,10 +327,11 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     }
     bb = group_reduce<G>(bb, OpB(), lds.b);
     if (t == 0) store_b(prec, bb);
-    exchange<G>(sy + 1, sy + flag_at(1), ci, F, nch, trec, xt, &xl[1], 8, 11, [&] {
-      const AggB x = all_reduce_b<G>(F, L, lds);
-      if (t == 0) store_b(trec, x);
-    });
+    if (!exchange<G>(sy + 1, sy + flag_at(1), ci, F, nch, trec, xt, &xl[1], 8, 11, [&] {
+          const AggB x = all_reduce_b<G>(F, L, lds);
+          if (t == 0) store_b(trec, x);
+        }))
+      return;
     tb = AggB{dbl(xt[8]), dbl(xt[9]), (long long)xt[10]};
   }
 
@@ -345,10 +353,11 @@ __global__ __launch_bounds__(G, 1024 / G) void k_large_fused(DevParams p, const 
     }
     c = group_reduce<G>(c, OpC(), lds.c);
     if (t == 0) store_c(prec, c);
-    exchange<G>(sy + 2, sy + flag_at(2), ci, F, nch, trec, xt, &xl[2], 11, 13, [&] {
-      const AggC x = all_reduce_c<G>(F, L, lds);
-      if (t == 0) store_c(trec, x);
-    });
+    if (!exchange<G>(sy + 2, sy + flag_at(2), ci, F, nch, trec, xt, &xl[2], 11, 13, [&] {
+          const AggC x = all_reduce_c<G>(F, L, lds);
+          if (t == 0) store_c(trec, x);
+        }))
+      return;
     tc = AggC{dbl(xt[11]), (long long)xt[12]};
   }
 

@@ -133,6 +133,7 @@ struct dm_ctx {
 
   int64_t R = 0, N = 0;
   bool store_loaded = false, cfg_loaded = false;
+  bool store_lost = false;  // a failed fused writeback tick wrote part of the store (check_fused)
   std::vector<int64_t> h_seg_off;
   std::vector<int64_t> h_refresh_s;
 
@@ -202,6 +203,7 @@ struct dm_ctx {
   bool fused_ok = false;       // every large resource within the co-residency bound
   int64_t fused_max_chunks = 0, fused_cap = 0;
   uint32_t fused_epoch = 0;
+  uint32_t fused_spin_limit = 1u << 21;  // x s_sleep 8 (~512 clocks): ~0.4 s, far beyond any real wait
   std::vector<Chunk> h_fchunks;
   std::vector<LargeSeg> h_flarge;
   DBuf<Chunk> fchunks;
@@ -235,10 +237,12 @@ struct dm_ctx {
   hipEvent_t ev_bat[3] = {};
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
-  // dm_decide: a round's requests (sorted by row), per-resource work items, results
+  // dm_decide: a round's requests (grouped by resource), per-resource work items, results
   DBuf<int64_t> rq_rows, rq_sub, rq_exp;
   DBuf<double> rq_has, rq_wants, rq_gets;
   DBuf<ReqItem> rq_items;
+  DBuf<double> rq_sc_has, rq_sc_wants;  // the round's working copy of the requested resources' rows
+  DBuf<int32_t> rq_sc_sub;
   // dm_hier_root_tick: per-server rejection flags, two rounds' worth (round r uses
   // words [(r & 1) * kHierMaxServers, +G)); each round zeroes the next round's words
   DBuf<uint32_t> hier_status;
@@ -310,7 +314,7 @@ struct dm_ctx {
     h_bat_flags = nullptr;
     row_bits.release(); upd_flags.release(); hier_status.release();
     rq_rows.release(); rq_sub.release(); rq_exp.release(); rq_has.release(); rq_wants.release(); rq_gets.release();
-    rq_items.release();
+    rq_items.release(); rq_sc_has.release(); rq_sc_wants.release(); rq_sc_sub.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
   }
@@ -518,9 +522,19 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
 // A wait of the one-launch large path gave up (its co-residency bound was
 // violated, e.g. by other processes' launches on the same device): the tick's
 // large-resource results are not valid.
+// A fused tick whose in-launch hand-off gave up: its leases are invalid, and a
+// writeback tick may have written part of the store (chunks that got their totals
+// wrote their rows), so the store is unusable until the next dm_store_load.
 static int check_fused(dm_ctx* c) {
   if (c->h_ferr && __atomic_load_n(c->h_ferr, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(c->h_ferr, 0u, __ATOMIC_RELEASE);
+    c->have_result = false;  // the tick's leases are invalid
+    if (c->last_writeback) {
+      c->store_lost = true;
+      return c->fail(DM_E_HIP, "large-resource hand-off timed out (too few resident workgroups) in a writeback "
+                               "tick: the store is partly written and must be reloaded (dm_store_load); use "
+                               "dm_set_large_path(ctx, DM_LARGE_CHAIN)");
+    }
     return c->fail(DM_E_HIP, "large-resource hand-off timed out (too few resident workgroups); the tick's leases "
                              "are invalid -- retry with dm_set_large_path(ctx, DM_LARGE_CHAIN)");
   }
@@ -576,13 +590,8 @@ int dm_create(int device, dm_ctx** out) {
       if (d < 0 || d >= dm_ctx::kAux) break;
       c->class_stream[i] = d;
     }
-  if (const char* sk = getenv("DM_STREAM_SKEW")) {  // A/B probe: plain streams created (and kept) first
-    static std::vector<hipStream_t> skew;
-    for (int i = 0; i < atoi(sk); ++i) {
-      hipStream_t x = nullptr;
-      if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) == hipSuccess) skew.push_back(x);
-    }
-  }
+  // test hook: a tiny bound makes the fused path's waits give up (tests/test_large_gpu.py)
+  if (const char* sl = getenv("DM_FUSED_SPIN_LIMIT")) c->fused_spin_limit = (uint32_t)strtoul(sl, nullptr, 10);
   e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -772,6 +781,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     c->all_sub_one = s->subclients[i] == 1 || s->expiry_ns[i] == DM_RELEASED;
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
+  c->store_lost = false;
   c->have_result = false;
   if (c->cfg_loaded && (int64_t)c->h_refresh_s.size() != R) c->cfg_loaded = false;
   return DM_OK;
@@ -813,6 +823,7 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
 
 static int ready(dm_ctx* c) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!c->cfg_loaded || (int64_t)c->h_refresh_s.size() != c->R)
     return c->fail(DM_E_STATE, "no configuration loaded for the store's resources");
   return DM_OK;
@@ -916,7 +927,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (nch > 0 && c->use_fused()) {
     c->fused_epoch = c->fused_epoch + 1 == 0 ? 1 : c->fused_epoch + 1;
     const FusedState F{c->f_ticket.p, c->f_sync.p, c->f_part.p, c->f_tot.p, c->d_ferr,
-                       (int32_t)c->h_fchunks.size(), c->fused_epoch};
+                       (int32_t)c->h_fchunks.size(), c->fused_epoch, c->fused_spin_limit};
     DM_HIP(c, timed(KC_LARGE_FUSED, s_large,
                     [&] { return launch_large_fused(c->fused_G, p, c->fchunks.p, c->flarge.p, F, gl, gc, s_large); }),
            "large-resource kernel");
@@ -996,9 +1007,11 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   return DM_OK;
 }
 
-// A round of requests, each decided by Resource.Decide against the store as it is
-// (dm_round.hip).  Requests are sorted by row on the host so that each resource's
-// requests are one contiguous range; one workgroup per resource with requests.
+// A round of requests, each decided by Resource.Decide in the caller's order and
+// seeing the Assigns of the requests before it on the same resource
+// (dm_round.hip).  Requests are ordered by resource on the host (stable: a
+// resource's requests keep the caller's order); one workgroup per resource with
+// requests, over a scratch copy of its rows.
 int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const double* has, const double* wants,
               const int64_t* subclients, double* gets, int64_t* expiry_ns) {
   DM_ENTER(c);
@@ -1007,24 +1020,30 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !subclients || !gets || !expiry_ns)))
     return c->fail(DM_E_INVAL, "bad requests");
   if (n == 0) return DM_OK;
+  std::vector<int64_t> seg_of((size_t)n);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t r = rows[k];
+    if (r < 0 || r >= c->N) return c->fail(DM_E_RANGE, "request row out of range");
+    if (subclients[k] < 0 || subclients[k] > kSubMax) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-2]");
+    seg_of[(size_t)k] = std::upper_bound(c->h_seg_off.begin(), c->h_seg_off.end(), r) - c->h_seg_off.begin() - 1;
+  }
   std::vector<int64_t> order((size_t)n);
   for (int64_t i = 0; i < n; ++i) order[(size_t)i] = i;
-  std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return rows[a] < rows[b]; });
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return seg_of[(size_t)a] < seg_of[(size_t)b]; });
   std::vector<int64_t> srows((size_t)n), ssub((size_t)n);
   std::vector<double> shas((size_t)n), swants((size_t)n);
   std::vector<ReqItem> items;
-  int64_t seg = 0;
+  int64_t scratch = 0;
   for (int64_t i = 0; i < n; ++i) {
-    const int64_t k = order[(size_t)i], r = rows[k];
-    if (r < 0 || r >= c->N) return c->fail(DM_E_RANGE, "request row out of range");
-    if (i > 0 && r == srows[(size_t)i - 1]) return c->fail(DM_E_INVAL, "one request per row");
-    if (subclients[k] < 0 || subclients[k] > kSubMax) return c->fail(DM_E_INVAL, "subclients must be in [0, 2^31-2]");
-    srows[(size_t)i] = r;
+    const int64_t k = order[(size_t)i], seg = seg_of[(size_t)k];
+    srows[(size_t)i] = rows[k];
     shas[(size_t)i] = has[k];
     swants[(size_t)i] = wants[k];
     ssub[(size_t)i] = subclients[k];
-    while (c->h_seg_off[seg + 1] <= r) ++seg;
-    if (items.empty() || items.back().seg != (int32_t)seg) items.push_back(ReqItem{(int32_t)seg, 0, i, i});
+    if (items.empty() || items.back().seg != (int32_t)seg) {
+      items.push_back(ReqItem{(int32_t)seg, 0, i, i, scratch});
+      scratch += c->h_seg_off[seg + 1] - c->h_seg_off[seg];
+    }
     items.back().qhi = i + 1;
   }
   hipStream_t st = c->stream;
@@ -1035,6 +1054,9 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   DM_HIP(c, upload(c->rq_items, items.data(), items.size(), st), "stage requests");
   DM_HIP(c, c->rq_gets.ensure((size_t)n), "request results");
   DM_HIP(c, c->rq_exp.ensure((size_t)n), "request results");
+  DM_HIP(c, c->rq_sc_has.ensure((size_t)std::max<int64_t>(scratch, 1)), "request scratch");
+  DM_HIP(c, c->rq_sc_wants.ensure((size_t)std::max<int64_t>(scratch, 1)), "request scratch");
+  DM_HIP(c, c->rq_sc_sub.ensure((size_t)std::max<int64_t>(scratch, 1)), "request scratch");
   DevParams p{};
   p.seg_off = c->seg_off.p;
   p.wants = c->wants.p;
@@ -1046,7 +1068,8 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   p.expl = c->expl.p;
   p.now = now_ns;
   p.recompute = 0;
-  const ReqArgs q{c->rq_rows.p, c->rq_has.p, c->rq_wants.p, c->rq_sub.p, c->rq_gets.p, c->rq_exp.p};
+  const ReqArgs q{c->rq_rows.p, c->rq_has.p,     c->rq_wants.p,    c->rq_sub.p,   c->rq_gets.p,
+                  c->rq_exp.p,  c->rq_sc_has.p,  c->rq_sc_wants.p, c->rq_sc_sub.p};
   DM_HIP(c, launch_decide(p, c->rq_items.p, (int)items.size(), q, st), "decide requests");
   DM_HIP(c, download(shas.data(), (const double*)c->rq_gets.p, 0, n, st), "read decisions");
   DM_HIP(c, download(ssub.data(), (const int64_t*)c->rq_exp.p, 0, n, st), "read decisions");
@@ -1193,6 +1216,7 @@ int dm_read_config(dm_ctx* c, int64_t r0, int64_t n, int32_t* kind, double* capa
 int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants, int64_t* sub, int64_t* exp) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
   DM_HIP(c, download(has, (const double*)c->has.p, off, n, c->stream), "read has");
@@ -1275,6 +1299,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
                     const int64_t* sub, const int64_t* exp) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
@@ -1303,6 +1328,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
 int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
@@ -1328,6 +1354,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
                                const double* wants) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (first_row < 0 || (first_row & 63) || nwords < 0 || n < 0 || (nwords > 0 && !mask) || (n > 0 && !wants))
     return c->fail(DM_E_INVAL, "bad masked update (first_row must be a multiple of 64)");
   if (nwords == 0) return n == 0 ? DM_OK : c->fail(DM_E_INVAL, "packed values without a mask");
@@ -1365,6 +1392,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
 int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
@@ -1389,6 +1417,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
 int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!b) return c->fail(DM_E_INVAL, "null batch");
   const int64_t nw = b->wants_nwords, nm = b->wants_n, nr = b->release_n, nu = b->upsert_n;
   if (nw < 0 || nm < 0 || nr < 0 || nu < 0) return c->fail(DM_E_INVAL, "negative batch sizes");
@@ -1532,6 +1561,7 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
 int dm_publish_totals(dm_ctx* c, void* dst) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
   DM_HIP(c, launch_publish(c->R, c->agg.p, dst, c->stream), "publish");
   return DM_OK;
@@ -1669,6 +1699,7 @@ int dm_store_stats(dm_ctx* c, int64_t* out, int max) {
   DM_ENTER(c);
   if (!out || max < 0) return c->fail(DM_E_INVAL, "bad output buffer");
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   std::vector<uint8_t> ex((size_t)c->R);
   DM_HIP(c, download(ex.data(), (const uint8_t*)c->expl.p, 0, c->R, c->stream), "read row states");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read row states");

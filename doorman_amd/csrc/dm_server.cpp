@@ -9,13 +9,15 @@
 //   1. Clean (store.go:169-181): leases whose expiry passed are released and
 //      their clients forgotten; ReleaseCapacity (server.go:668-714) likewise.
 //   2. New clients take a free row (no lease: store.HasClient is false for them).
-//   3. dm_decide runs Resource.Decide for every request of the round against
-//      the store as it was before the round -- the request's own has (Learn),
-//      wants and subclients for its client, the stored rows for everyone else
-//      (algorithm.go:115,148,157,223-225,263-269) -- and the leases are then
-//      assigned (dm_store_upsert, store.go:153-167: sums += new - old, expiry =
-//      now + length).  A round of one request is exactly the reference's
-//      GetCapacity; a round of many is each request's Decide on the same store.
+//   3. dm_decide runs Resource.Decide for every request of the round in queue
+//      order -- the request's own has (Learn), wants and subclients for its
+//      client, the stored rows for everyone else (algorithm.go:115,148,157,
+//      223-225,263-269) -- and each decision's Assign is seen by the requests
+//      after it on the same resource, as res.mu serialises the reference's
+//      GetCapacity calls (resource.go:103-104).  The round's final leases are
+//      then written to the store (dm_store_upsert, store.go:153-167: sums +=
+//      new - old, expiry = now + length).  A round is exactly the reference
+//      serving its requests one after another in queue order.
 //
 // Clients that did not ask this round keep their leases (and count in the
 // sums) until they expire.  The host keeps the client -> row maps, the rows'
@@ -281,12 +283,12 @@ int dm_server_tick(dm_server* s, int64_t now) {
       return rc;
     }
   }
-  // 2. one request per row (the last one wins); a new client takes a free row,
-  //    which holds no lease (store.HasClient false for the decision)
-  std::vector<int64_t> ticket_row(reqs.size());
-  std::unordered_map<int64_t, size_t> row_req;  // row -> index into the round's requests
-  std::vector<int64_t> rows, u_sub;
-  std::vector<double> u_has, u_wants;
+  // 2. every request in queue order; a new client takes a free row, which holds no
+  //    lease (store.HasClient false for its first decision)
+  const int64_t nq = (int64_t)reqs.size();
+  std::vector<int64_t> q_row((size_t)nq), q_sub((size_t)nq);
+  std::vector<double> q_has((size_t)nq), q_wants((size_t)nq);
+  std::unordered_map<int64_t, size_t> row_last;  // row -> the last request on it
   struct Fresh {
     int64_t res, row;
     std::string client;
@@ -306,19 +308,11 @@ int dm_server_tick(dm_server* s, int64_t now) {
     } else {
       row = c->second;
     }
-    ticket_row[k] = row;
-    auto ins = row_req.emplace(row, rows.size());
-    if (ins.second) {
-      rows.push_back(row);
-      u_has.push_back(q.has);
-      u_wants.push_back(q.wants);
-      u_sub.push_back(q.sub);
-    } else {
-      const size_t j = ins.first->second;
-      u_has[j] = q.has;
-      u_wants[j] = q.wants;
-      u_sub[j] = q.sub;
-    }
+    q_row[k] = row;
+    q_has[k] = q.has;
+    q_wants[k] = q.wants;
+    q_sub[k] = q.sub;
+    row_last[row] = k;
   }
   auto rollback = [&](int code) {  // new clients never got a lease: forget them
     for (const Fresh& f : fresh) {
@@ -328,21 +322,33 @@ int dm_server_tick(dm_server* s, int64_t now) {
     }
     return s->ctx_fail(code);
   };
-  if (rows.empty()) return DM_OK;
-  const int64_t n = (int64_t)rows.size();
-  // 3. decide every request against the store as it was before the round
-  //    (Resource.Decide per request), then Assign the leases (store.go:153-167)
-  std::vector<double> gets(n);
-  std::vector<int64_t> exp(n);
-  if ((rc = dm_decide(s->ctx, now, n, rows.data(), u_has.data(), u_wants.data(), u_sub.data(), gets.data(),
+  if (nq == 0) return DM_OK;
+  // 3. Resource.Decide for every request in queue order, each seeing the Assigns of
+  //    the requests before it on its resource (res.mu serialises them,
+  //    resource.go:103-104); then the round's final leases go into the store
+  //    (store.go:153-167), one Assign per row with its last request's values
+  std::vector<double> gets((size_t)nq);
+  std::vector<int64_t> exp((size_t)nq);
+  if ((rc = dm_decide(s->ctx, now, nq, q_row.data(), q_has.data(), q_wants.data(), q_sub.data(), gets.data(),
                       exp.data())))
     return rollback(rc);
-  if ((rc = dm_store_upsert(s->ctx, n, rows.data(), gets.data(), u_wants.data(), u_sub.data(), exp.data())))
+  std::vector<int64_t> rows, u_sub, u_exp;
+  std::vector<double> u_gets, u_wants;
+  for (int64_t k = 0; k < nq; ++k) {
+    if (row_last[q_row[k]] != (size_t)k) continue;
+    rows.push_back(q_row[k]);
+    u_gets.push_back(gets[k]);
+    u_wants.push_back(q_wants[k]);
+    u_sub.push_back(q_sub[k]);
+    u_exp.push_back(exp[k]);
+  }
+  const int64_t n = (int64_t)rows.size();
+  if ((rc = dm_store_upsert(s->ctx, n, rows.data(), u_gets.data(), u_wants.data(), u_sub.data(), u_exp.data())))
     return rollback(rc);
   for (int64_t j = 0; j < n; ++j) {
-    s->has[rows[j]] = gets[j];
-    s->expiry[rows[j]] = exp[j];
-    s->heap.push({exp[j], rows[j]});
+    s->has[rows[j]] = u_gets[j];
+    s->expiry[rows[j]] = u_exp[j];
+    s->heap.push({u_exp[j], rows[j]});
   }
   // SetSafeCapacity (resource.go:81-96) after the round's Assigns
   int64_t rlo = s->R, rhi = -1;
@@ -355,12 +361,11 @@ int dm_server_tick(dm_server* s, int64_t now) {
     return s->ctx_fail(rc);
   s->results.assign(reqs.size(), Out{});
   for (size_t k = 0; k < reqs.size(); ++k) {
-    const size_t j = row_req[ticket_row[k]];
     const int64_t r = reqs[k].res;
     Out& o = s->results[k];
-    o.capacity = gets[j];
+    o.capacity = gets[k];
     // Lease.Expiry.Unix() (server.go:789): seconds, rounded toward -inf
-    o.expiry_s = exp[j] >= 0 ? exp[j] / 1000000000LL : -((-exp[j] + 999999999LL) / 1000000000LL);
+    o.expiry_s = exp[k] >= 0 ? exp[k] / 1000000000LL : -((-exp[k] + 999999999LL) / 1000000000LL);
     o.refresh_s = s->refresh_s[r];  // int64(RefreshInterval.Seconds())
     const double safe = s->safe_capacity[r];
     o.safe = std::isnan(safe) ? s->capacity[r] / (double)count[(size_t)(r - rlo)] : safe;

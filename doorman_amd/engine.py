@@ -204,9 +204,10 @@ class Engine:
         self._chk(self._L.dm_apportion(self._ctx, int(now_ns), flags))
 
     def decide(self, now_ns: int, rows, has, wants, subclients):
-        """dm_decide: Resource.Decide for each request of a round against the store as it
-        is (rows[k] = the client's row, or a free row of its resource for a new client);
-        returns (gets, expiry_ns).  The store is not changed."""
+        """dm_decide: Resource.Decide for each request of a round, in order, each seeing
+        the Assigns of the requests before it on its resource (rows[k] = the client's
+        row, or a free row of its resource for a new client; a row may repeat);
+        returns (gets, expiry_ns).  The device store is not changed."""
         rows = _c(rows, np.int64)
         a = [_c(has, np.float64), _c(wants, np.float64), _c(subclients, np.int64)]
         gets, exp = np.empty(len(rows)), np.empty(len(rows), np.int64)

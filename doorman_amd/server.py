@@ -2,10 +2,11 @@
 (dm_server_* in include/doorman_hip.h, doorman_amd/csrc/dm_server.cpp).
 
 Mirrors the reference server's request path (go/server/doorman/server.go:668-817,
-resource.go:100-113): a round's ResourceRequests are queued, then decided together
-round by round (dm_decide: each request against the store as it was before the
-round, then the Assigns); each ticket gets the lease GetCapacity would put in its
-response (capacity, expiry_time in unix seconds, refresh_interval, safe_capacity).
+resource.go:100-113): a round's ResourceRequests are queued, then decided by one
+dm_server_tick in queue order (dm_decide: each request sees the Assigns of the
+requests before it on its resource, as res.mu serialises the reference's calls);
+each ticket gets the lease GetCapacity would put in its response (capacity,
+expiry_time in unix seconds, refresh_interval, safe_capacity).
 """
 from __future__ import annotations
 

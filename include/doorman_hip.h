@@ -196,13 +196,17 @@ int dm_apportion(dm_ctx* ctx, int64_t now_ns, uint32_t flags);
 /* A round of individual requests (Resource.Decide, resource.go:100-113, for each):
  * request k is for the client whose lease lives in row rows[k] -- its existing row,
  * or a free (released) row of the resource it asks for, which makes it a new client
- * (store.HasClient false, algorithm.go:223-225).  Every request is decided against
- * the store as it is (after a Clean at now_ns, which is not written back), with the
- * request's own has (Learn), wants and subclients for its client and the stored
- * rows for everyone else (algorithm.go:115,126,148,157,263-269).  gets[k] and
- * expiry_ns[k] (now + lease length) are the leases; the store is not changed --
- * Assign them with dm_store_upsert.  Rows unique; subclients in [0, 2^31 - 1).
- * Synchronous. */
+ * (store.HasClient false, algorithm.go:223-225).  After a Clean at now_ns (not
+ * written back), the requests are decided in the order given, as res.mu serialises
+ * the reference's calls (resource.go:103-104): each with the request's own has
+ * (Learn), wants and subclients for its client and the rows for everyone else
+ * (algorithm.go:115,126,148,157,263-269), and each decision's Assign (store.go:
+ * 153-167: the row and the running sums) is seen by the later requests on the same
+ * resource -- so a round's grants stay within the capacity exactly as the
+ * reference's.  A row may be requested more than once (a client's later request
+ * sees its earlier one).  gets[k] and expiry_ns[k] (now + lease length) are the
+ * leases; the device store is not changed -- Assign the final ones with
+ * dm_store_upsert.  Subclients in [0, 2^31 - 1).  Synchronous. */
 int dm_decide(dm_ctx* ctx, int64_t now_ns, int64_t n, const int64_t* rows, const double* has, const double* wants,
               const int64_t* subclients, double* gets, int64_t* expiry_ns);
 
@@ -313,11 +317,11 @@ int dm_store_stats(dm_ctx* ctx, int64_t* out, int max);
  *
  * Requests queued during a round are decided together by dm_server_tick: the
  * store first drops expired leases (Clean, store.go:169-181) and released
- * clients (store.go:142-151); then every request is decided by Resource.Decide
- * against the store as it was before the round (dm_decide: the request's own has,
- * wants and subclients for its client, new clients absent from the store), and
- * the round's leases are assigned (store.go:153-167).  A round of one request is
- * the reference's GetCapacity exactly.  Clients that did not ask keep their
+ * clients (store.go:142-151); then every request is decided by Resource.Decide in
+ * queue order, each seeing the Assigns (store.go:153-167) of the requests before it
+ * on its resource (dm_decide: the request's own has, wants and subclients for its
+ * client, new clients absent from the store until their first Assign).  A round is
+ * the reference's GetCapacity calls served one after another in queue order.  Clients that did not ask keep their
  * leases, which expire unless refreshed.  A round that fails leaves no leases
  * (dm_server_lease then reports an error for its tickets) and forgets the new
  * clients it had placed.  Resources are configured up front (the outcome of

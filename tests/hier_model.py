@@ -7,8 +7,9 @@ Restated from the reference itself, not from the kernels:
   * the root's GetServerCapacity   server.go:822-901: bands summed (:850-879), a band
         with num_clients < 1 fails the whole RPC with InvalidArgument (:863-866);
         each request decided by Resource.Decide (resource.go:100-113) -- here the
-        oracle's literal restatement, one private store copy per request (the
-        round's snapshot semantics) -- and assigned (store.go:153-167)
+        oracle's literal restatement -- and assigned (store.go:153-167), one after
+        another in server order as the root's res.mu serialises the calls
+        (resource.go:103-104): each request sees the Assigns before it
   * the intermediate's reload      server.go:279-313 + Server.LoadConfig (:187-218)
         + Resource.LoadConfig (resource.go:117-125): capacity = the grant, expiry
         time = time.Unix(gets.expiry_time, 0), the root's Algorithm and
@@ -49,18 +50,15 @@ class Root:
 
     def round(self, now: int, requests):
         """requests[g]: None (server g sent nothing / its RPC failed) or {r: (wants, subclients)}.
-        Returns {(g, r): Lease} for every request, all decided against the stores as they
-        were before the round, then assigned."""
+        Returns {(g, r): Lease} for every request, decided and assigned in server order
+        (Decide ends with store.Assign, algorithm.go:71-300)."""
         out = {}
         for r in range(self.R):
             st = self.stores[r]
-            st.clean(now)  # every private copy's Decide starts with the same Clean
-            reqs = [(g, *requests[g][r]) for g in range(self.G) if requests[g] is not None and r in requests[g]]
-            leases = [O.decide(st.clone(), self.tab[r], g, 0.0, w, s, now) for g, w, s in reqs]
-            lease_s, refresh_s = int(self.tab[r]["lease_length_s"]), int(self.tab[r]["refresh_interval_s"])
-            for (g, w, s), l in zip(reqs, leases):
-                st.assign(g, lease_s, refresh_s, l.has, w, s, now)
-                out[(g, r)] = l
+            for g in range(self.G):
+                if requests[g] is not None and r in requests[g]:
+                    w, s = requests[g][r]
+                    out[(g, r)] = O.decide(st, self.tab[r], g, 0.0, w, s, now)
         return out
 
     def rows(self) -> dict:

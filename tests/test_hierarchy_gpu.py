@@ -6,7 +6,9 @@ G servers each publish their store totals, run the root's round on their own
 copy of the root store (as every rank of a node does) and load their new
 templates, then tick their leaf store.  Per round:
   * every root copy equals the model's root stores bit for bit (rows and running
-    sums: the kernel decides each request literally in the reference's order);
+    sums: the kernel decides the servers' requests one after another in server
+    order, each seeing the Assigns before it, as the root's res.mu serialises
+    GetServerCapacity calls, and walks the rows in the oracle's order);
   * every leaf's configuration equals the model's templates bit for bit (grant,
     parent expiry in Unix seconds, the root's algorithm and safe capacity, or the
     "*" default for resources it did not request; learning end kept);
@@ -160,6 +162,50 @@ def test_hierarchy_rounds_match_the_reference_model(G, clients):
                 # last round, where the 20-s default template's followers lapse
                 assert leaves[g].store_stats()["dense_resources"] == R, f"G={G} round {t} leaf {g}"
     for e in leaves + roots:
+        e.close()
+
+
+@pytest.mark.parametrize("G", [2, 4, 8, 64])
+def test_root_round_grants_stay_within_capacity(G):
+    """G servers that each want more than a resource's capacity.  The
+    root decides their requests one after another (resource.go:103-104), so on the
+    first exchange FairShare grants C, 0, 0, ... and ProportionalShare the same
+    (not G x C); later rounds share it out as the sequential model does.  Every
+    round: Σ_g grants <= C per resource, the root rows equal the model's bit for
+    bit and each leaf template's capacity is its grant."""
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    L = _lib.lib()
+    R = 37
+    kind = np.where(np.arange(R) % 2 == 0, W.FAIR_SHARE, W.PROPORTIONAL_SHARE).astype(np.int32)
+    rcfg = {"kind": kind, "capacity": np.full(R, 100.0), "lease_length_s": np.full(R, 30, np.int64),
+            "refresh_interval_s": np.full(R, 5, np.int64), "learning_end_ns": np.full(R, W.INT64_MIN, np.int64),
+            "parent_expiry_ns": np.full(R, W.INT64_MAX, np.int64), "safe_capacity": np.full(R, np.nan)}
+    roots = [root_engine(rcfg, G)]
+    leaf = Engine(0)
+    leaf.load(M.with_config(W.uniform(R, 20, kind=W.FAIR_SHARE, seed=1), M.default_config(R)))
+    model = M.Root(rcfg, G)
+    rng = np.random.default_rng(G)
+    gathered = torch.zeros((G * R, 2), dtype=torch.float64, device="cuda")
+    for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 10 * W.NS]):
+        sw = rng.uniform(100.0, 300.0, (G, R))  # every server wants more than C
+        cnt = rng.integers(1, 40, (G, R)).astype(np.int64)
+        rec = np.stack([sw.reshape(-1), cnt.reshape(-1).view(np.float64)], axis=1)
+        gathered.copy_(torch.from_numpy(rec))
+        resp = model.round(now, [M.server_request(sw[g], cnt[g]) for g in range(G)])
+        _lib.check(L.dm_hier_root_tick(roots[0]._ctx, gathered.data_ptr(), G, now, leaf._ctx, 0), roots[0]._ctx)
+        roots[0].sync()
+        leaf.sync()
+        assert_root_equal(roots[0], model, f"G={G} round {t}")
+        grants = np.array([[resp[(g, r)].has for r in range(R)] for g in range(G)])
+        assert np.all(grants.sum(axis=0) <= 100.0 * (1 + 1e-12)), (t, grants.sum(axis=0).max())
+        if t == 0:
+            np.testing.assert_array_equal(grants[0], np.full(R, 100.0))
+            assert np.all(grants[1:] == 0.0)
+        np.testing.assert_array_equal(leaf.config()["capacity"], grants[0])
+    for e in roots + [leaf]:
         e.close()
 
 

@@ -189,3 +189,52 @@ def test_large_resources_at_c2(pair, which):
     e = max_err(sub, gets[rows], ref)
     print(f"C2 large resources ({which}): max |got-ref|/max(|ref|, C_r/n_r) = {e:.3e} (bar 1e-9)")
     assert e <= 1e-9
+
+
+def test_fused_wait_that_gives_up_loses_the_store_until_reload():
+    """a fused-path wait that gives up (forced here with a zero spin bound,
+    DM_FUSED_SPIN_LIMIT) fails the tick with DM_E_HIP, and the chunk stops before
+    any further store write.  Chunks that did get their totals may have written
+    their rows, so after a failed writeback tick every call that needs the store
+    reports DM_E_STATE until the store is loaded again; the reloaded store then
+    ticks exactly as the chain does.  A failed tick without writeback keeps the
+    store."""
+    from doorman_amd._lib import DM_E_HIP, DM_E_STATE
+    from doorman_amd._lib import DmError as DoormanError
+    rng = np.random.default_rng(77)
+    snap = snapshot_with_sizes(rng, np.array([60000, 70000, 50000, 45000], dtype=np.int64), hetero=False)
+    os.environ["DM_FUSED_SPIN_LIMIT"] = "0"
+    try:
+        eng = _engine(fused=True)
+    finally:
+        os.environ.pop("DM_FUSED_SPIN_LIMIT")
+    chain = _engine()
+    try:
+        eng.load(snap)
+        before = eng.read_store()
+        try:
+            eng.apportion(NOW)  # no writeback: the store must survive a failure
+            failed = False
+        except DoormanError as e:
+            assert e.code == DM_E_HIP
+            failed = True
+        after = eng.read_store()
+        for k in before:
+            assert before[k].tobytes() == after[k].tobytes(), k
+        assert failed, "a zero spin bound must make some chunk's wait give up"
+        if failed:
+            with pytest.raises(DoormanError) as e:
+                eng.apportion(NOW, writeback=True)
+            assert e.value.code == DM_E_HIP
+            for call in (lambda: eng.apportion(NOW), lambda: eng.read_store(), lambda: eng.leases()):
+                with pytest.raises(DoormanError) as e:
+                    call()
+                assert e.value.code == DM_E_STATE
+        eng.set_large_path(fused=False)
+        a = _tick(eng, snap, writeback=True)
+        b = _tick(chain, snap, writeback=True)
+        for x, y in zip(a[:2], b[:2]):
+            assert x.tobytes() == y.tobytes()
+    finally:
+        eng.close()
+        chain.close()
