@@ -4,16 +4,22 @@ One step = one apportionment tick over every lease of the rank's store: the
 device-resident snapshot is decided (Clean, learning mode, the resource's
 algorithm) and written back (DM_WRITEBACK), inputs already resident in HBM.
 With the hierarchy on (the default for the north-star workload c3), every step
-first runs the intermediate-server exchange (publish per-resource totals, one
-all-gather over RCCL, the root's apportionment, this server's grants).
+also runs the intermediate-server exchange (publish per-resource totals, one
+all-gather over RCCL, the root's apportionment, this server's grants), pipelined
+beside the next leaf tick (dm_hier_pipeline).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c1ps|c2|c3|c4] [--hier on|off|auto]
+                  [--layout auto|sharded|replicated]
+
+configs[3] (c3, the default): ONE 100M-lease snapshot (100k resources x 1k
+clients) sharded by resource id over the N GPUs (hierarchy.partition), each GPU
+the intermediate server of its range -- strong scaling, the whole node's leases
+per step are 100M at every N.  --layout replicated gives every GPU its own
+full-size store instead (weak scaling; reported under extra.weak_scaling at N > 1).
 
 --gpus N > 1 without a torch.distributed environment starts N ranks itself
 (python -m torch.distributed.run, one process per GPU, started before this
-process touches the GPU) and exits with their status.  Under torchrun each rank
-owns one GPU and its own store (weak scaling: a full C3-shaped store per GPU).
-Rank 0 prints one JSON line.
+process touches the GPU) and exits with their status.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -39,15 +45,24 @@ WORKLOADS = {
     "c1": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), FairShare, uniform wants",
     "c1ps": "C1 (BASELINE configs[1]): 10,000 resources x 1,000 clients per GPU (10M leases), ProportionalShare",
     "c2": "C2 (BASELINE configs[2]): 1M resources, Zipf 1..1M clients (13,970,034 leases), mixed kinds, 5% learning",
-    "c3": "C3 (BASELINE configs[3], north-star size): 100,000 resources x 1,000 clients = 100M leases per GPU, "
-          "FairShare",
+    "c3": "C3 (BASELINE configs[3], north-star size): 100,000 resources x 1,000 clients = 100M leases, FairShare",
     "c4": "C4 (BASELINE configs[4]) per GPU: 125M-lease device-resident store (1B over 8 GPUs), 125k resources x "
           "1k client slots, FS/PS mixed, 5% learning; every step = 5 s refresh tick: 10% wants updates and 1% "
           "departures + 1% new clients over PCIe, then the tick",
 }
 
 
-def make_workload(name: str, rank: int):
+C3_R, C3_CLIENTS = 100_000, 1_000
+
+
+def c3_bounds(world: int):
+    """configs[3]: the resource-id ranges of the node's GPUs (contiguous, balanced by
+    lease count: hierarchy.partition)."""
+    from doorman_amd.hierarchy import partition
+    return partition(np.full(C3_R, C3_CLIENTS), world)
+
+
+def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicated"):
     from doorman_amd import workloads as W
     if name == "c1":
         return W.c1(seed=1 + 1000 * rank, kind=W.FAIR_SHARE)
@@ -56,7 +71,10 @@ def make_workload(name: str, rank: int):
     if name == "c2":
         return W.c2(seed=2 + 1000 * rank)
     if name == "c3":
-        return W.uniform(100_000, 1_000, kind=W.FAIR_SHARE, seed=3 + 1000 * rank)
+        if layout == "sharded":  # this rank's range of the one 100M-lease snapshot
+            b = c3_bounds(world)
+            return W.uniform_range(C3_R, C3_CLIENTS, int(b[rank]), int(b[rank + 1]), kind=W.FAIR_SHARE, seed=3)
+        return W.uniform_range(C3_R, C3_CLIENTS, 0, C3_R, kind=W.FAIR_SHARE, seed=3 + 1000 * rank)
     if name == "c4":
         snap = W.uniform(125_000, 1_000, kind="mixed", seed=4 + 1000 * rank)
         rng = np.random.default_rng(40 + rank)
@@ -118,6 +136,10 @@ def kernel_units(snap):
     big = sizes > 4096
     for name in ("large_fused", "large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
         units[name] = (int(sizes[big].sum()), int(big.sum()))
+    for b in ("block128x4", "block128x8"):  # the split form's two kernels
+        units[b + "_dense"] = units[b]
+        units[b + "_rest"] = (0, 0)  # only what the dense kernel queued; counted with the dense kernel
+    units["hier_publish"] = (0, len(sizes))
     return units
 
 
@@ -293,7 +315,7 @@ def cpu_baseline(snap, now_ns, budget_s=12.0):
 # ---------------------------------------------------------------------------
 # timing
 # ---------------------------------------------------------------------------
-def timed_steps(torch, eng, step, steps, warmup, sync_ranks, extra_warm=True):
+def timed_steps(torch, eng, step, steps, warmup, sync_ranks, extra_warm=True, also=()):
     """W untimed warm-up steps, then more until ~0.3 s of ticks have run (the first
     milliseconds of back-to-back ticks run ~10% slow: C3 measured 843 us/tick after 3
     warm-up ticks, 765 after 30; the count is agreed over ranks), then K timed steps
@@ -326,13 +348,18 @@ def timed_steps(torch, eng, step, steps, warmup, sync_ranks, extra_warm=True):
     sync_ranks("barrier", None)
     elapsed = time.perf_counter() - t0
     stream_ms = ev0.elapsed_time(ev1)
-    eng.set_profiling(True)
-    eng.reset_kernel_times()
+    prof = [eng] + list(also)  # the exchange's root round runs on the root engine
+    for e in prof:
+        e.set_profiling(True)
+        e.reset_kernel_times()
     for _ in range(steps):
         step()
-    eng.sync()
-    ktimes = eng.kernel_times()
-    eng.set_profiling(False)
+    torch.cuda.synchronize()
+    ktimes = {}
+    for e in prof:
+        e.sync()
+        ktimes.update(e.kernel_times())
+        e.set_profiling(False)
     return {"elapsed": elapsed, "stream_ms": stream_ms, "ktimes": ktimes, "warm_run": max(warmup, 1) + extra}
 
 
@@ -348,7 +375,7 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
     if single:  # one kernel per tick: HIP events around the timed region itself
         avg_s = run["stream_ms"] / steps / 1e3
     leases_k, res_k = kernel_units(snap).get(name, (N, R))
-    group_kernel = name in ("block128x4", "block128x8")
+    group_kernel = name in ("block128x4", "block128x8", "block128x4_dense", "block128x8_dense")
     dense_k = run.get("dense_frac", 0.0) * leases_k if group_kernel else 0.0
     alg = algorithmic_bytes(leases_k, res_k, dense_k)
     achieved = alg / avg_s / 1e9
@@ -373,6 +400,8 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
             "survey_layout_equivalent_GBs": round((SURVEY_LEASE_BYTES * leases_k + 64 * res_k) / avg_s / 1e9, 1),
             "avg_launch_us": round(avg_s * 1e6, 2),
             "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
+            "kernel_time_share_note": "of the summed event time of every profiled kernel class of a step (the "
+                                      "exchange's publish and root round included; concurrent classes overlap)",
             "timed_region_stream_us_per_step": round(run["stream_ms"] * 1e3 / steps, 2),
             "duration_source": ("HIP event pair around the timed region on the kernel's stream (one kernel "
                                 "per tick)" if single else "HIP events around every launch, profiled region")}
@@ -405,9 +434,13 @@ def main():
                     help="nccl (= RCCL) on a node; gloo + --same-device rehearses N>1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
     ap.add_argument("--hier", default="auto", choices=["auto", "on", "off"],
-                    help="every step runs the intermediate-server exchange first (SURVEY.md §8e, configs[3]): "
-                         "publish totals, RCCL all-gather, root apportionment, take grants, then the leaf tick; "
-                         "auto = on for c3")
+                    help="every step also runs the intermediate-server exchange (SURVEY.md §8e, configs[3]): "
+                         "publish totals, RCCL all-gather, root apportionment, take grants; auto = on for c3")
+    ap.add_argument("--layout", default="auto", choices=["auto", "sharded", "replicated"],
+                    help="c3 over N GPUs: sharded = one 100M-lease snapshot split by resource id (configs[3], "
+                         "strong scaling; auto); replicated = a full store per GPU (weak scaling)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run each step's exchange before its leaf tick on one stream instead of beside the next tick")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -419,6 +452,9 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     hier = args.hier == "on" or (args.hier == "auto" and args.workload == "c3")
+    layout = args.layout if args.layout != "auto" else ("sharded" if args.workload == "c3" else "replicated")
+    if layout == "sharded" and args.workload != "c3":
+        raise SystemExit("--layout sharded is configs[3]'s layout (--workload c3)")
 
     import torch  # loaded first: libdoorman_hip then binds to torch's HIP runtime
     import torch.distributed as dist
@@ -449,47 +485,62 @@ def main():
     from doorman_amd import workloads as W
     from doorman_amd.engine import Engine
 
-    snap = make_workload(args.workload, rank)
-    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
-    eng = Engine(dev_index)
-    eng.load(snap)
-    now = W.NOW_NS
+    def gather(src, dst):
+        if world > 1 and not gloo:
+            dist.all_gather_into_tensor(dst, src)  # RCCL over xGMI
+        elif world > 1:  # rehearsal: through host memory
+            parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
+            dist.all_gather(parts, src.cpu())
+            dst.copy_(torch.cat(parts).to(dst.device))
+        else:
+            dst.copy_(src)
 
-    # back-to-back ticks: a forked tick's class streams join lazily (DM_DEFER_JOIN)
-    step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
-    root = None
-    if args.workload == "c4":
-        step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup)
-    if hier:
-        from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
-        root = Engine(dev_index)
-        root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world, lease_length_s=20))
-
-        def gather(src, dst):
-            if world > 1 and not gloo:
-                dist.all_gather_into_tensor(dst, src)  # RCCL over xGMI
-            elif world > 1:  # rehearsal: through host memory
-                parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
-                dist.all_gather(parts, src.cpu())
-                dst.copy_(torch.cat(parts).to(dst.device))
+    def measure(layout):
+        """Load this rank's store (and root copy), run the timed steps; returns the run,
+        the snapshot and the engines (closed by the caller)."""
+        snap = make_workload(args.workload, rank, world, layout)
+        R = len(snap["seg_off"]) - 1
+        eng = Engine(dev_index)
+        eng.load(snap)
+        now = W.NOW_NS
+        # back-to-back ticks: a forked tick's class streams join lazily (DM_DEFER_JOIN)
+        step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
+        root = ht = None
+        if args.workload == "c4":
+            step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup)
+        if hier:
+            from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
+            root = Engine(dev_index)
+            if layout == "sharded":  # the root of the whole snapshot: one row per resource (its owner's)
+                bounds = c3_bounds(world)
+                root.load(root_snapshot(C3_R, 1, W.FAIR_SHARE, 1000.0, lease_length_s=20))
+                ht = HierarchicalTick(torch, eng, root, C3_R, world, rank, gather, shard_lo=bounds,
+                                      pipelined=not args.no_pipeline)
             else:
-                dst.copy_(src)
+                root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world,
+                                        lease_length_s=20))
+                ht = HierarchicalTick(torch, eng, root, R, world, rank, gather, pipelined=not args.no_pipeline)
+            step = lambda: ht.tick(now, asynchronous=True)  # noqa: E731
+        run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4",
+                          also=[root] if root is not None else [])
+        run["dense_frac"] = dense_fraction(eng, snap)
+        if ht is not None:
+            ht.sync()
+            ht.check()  # any server whose request the root rejected (server.go:863-866) fails loudly
+        t = torch.tensor([run["elapsed"]], dtype=torch.float64, device=red_dev)
+        n = torch.tensor([len(snap["wants"])], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        run["t_max"], run["n_total"] = float(t.item()), float(n.item())
+        return run, snap, eng, root
 
-        ht = HierarchicalTick(torch, eng, root, R, world, rank, gather)
-        step = lambda: ht.tick(now, asynchronous=True)  # noqa: E731
-
-    run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4")
-    run["dense_frac"] = dense_fraction(eng, snap)
-    t = torch.tensor([run["elapsed"]], dtype=torch.float64, device=red_dev)
-    n = torch.tensor([N], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-    t_max, n_total = float(t.item()), float(n.item())
+    run, snap, eng, root = measure(layout)
+    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
+    t_max, n_total = run["t_max"], run["n_total"]
     roofline = roofline_of(args.workload, snap, run, args.steps,
                            single_kernel_tick=not hier and args.workload != "c4")
-    if hier:
-        ht.check()  # any server whose request the root rejected (server.go:863-866) fails loudly
+    now = W.NOW_NS
 
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra and args.workload == "c3":
@@ -510,6 +561,20 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(snap, now, args.cpu_budget)
+    eng.close()
+    if root is not None:
+        root.close()
+    if world > 1 and layout == "sharded" and not args.no_extra:
+        # weak scaling beside the configs[3] line: every GPU its own full 100M-lease store
+        rw, snapw, ew, rootw = measure("replicated")
+        extra["weak_scaling"] = {"layout": "replicated: a full 100k x 1k store per GPU, every GPU an intermediate "
+                                           "server of the same resources",
+                                 "value": rw["n_total"] * args.steps / rw["t_max"], "unit": "leases/s",
+                                 "leases_per_gpu": len(snapw["wants"]), "ms_per_step": rw["t_max"] / args.steps * 1e3,
+                                 "scaling": "weak"}
+        ew.close()
+        if rootw is not None:
+            rootw.close()
 
     if rank == 0:
         sizes = np.diff(snap["seg_off"])
@@ -525,16 +590,22 @@ def main():
             "warmup_steps_run": run["warm_run"],
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if layout == "sharded" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded numpy generators of SURVEY.md §8d)",
             "config": {"workload": WORKLOADS[args.workload] + (
-                           "; hierarchical: every GPU is an intermediate server of the same resources, all-gather "
-                           "of per-resource totals + root apportionment every step" if hier else ""),
-                       "resources_per_gpu": R, "leases_per_gpu": N,
-                       "parallelism": (f"intermediate-server hierarchy x{world} (all-gather 16 B x R per GPU)"
-                                       if hier else f"resource-sharded x{world} (no data-path collective)"),
+                           (f"; one snapshot sharded by resource id over {world} GPU(s) (contiguous ranges), each GPU "
+                            f"the intermediate server of its range" if layout == "sharded" else
+                            "; every GPU holds a full store and is an intermediate server of the same resources")
+                           + (f"; every step the exchange: publish per-resource totals, all-gather "
+                              f"{'(RCCL) ' if world > 1 and not gloo else ''}of {world} block(s), the root's round "
+                              f"over every resource on each GPU, this server's grants"
+                              + ("" if args.no_pipeline else ", pipelined beside the next leaf tick (one tick of "
+                                                             "lag, dm_hier_pipeline)") if hier else "")),
+                       "layout": layout, "resources_per_gpu": R, "leases_per_gpu": N, "leases_total": int(n_total),
+                       "parallelism": (f"intermediate-server hierarchy x{world}, {layout}" if hier
+                                       else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
             "dist": dist_info,
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
@@ -545,9 +616,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    eng.close()
-    if root is not None:
-        root.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -228,15 +228,25 @@ struct ReqArgs {
 constexpr int kHierMaxServers = 64;     // one lane per server row, whole resources per wave
 constexpr uint32_t kHierInvalid = 1u;    // a band with num_clients < 1: InvalidArgument (server.go:863-866)
 constexpr uint32_t kHierCountRange = 2u; // Count > kSubMax: beyond the root's 32-bit subclients column
+// A server's published block (dm_publish_totals): record 0 = {its request's
+// validation flags as u64 bits, 0}, record 1 + i = {SumWants, Count as bits} of the
+// i-th resource it holds; blocks sit `stride` records apart in the gathered buffer.
 struct HierArgs {
-  const double2* gathered;  // [G][R] {SumWants, Count as bits} (k_publish records)
-  const uint32_t* status;   // [G] k_hier_validate flags; a flagged server requests nothing
-  ResCfg* leaf_cfg;         // this server's leaf template
-  ResCold* leaf_cold;       // ... its safe capacity and refresh interval
-  const ResCold* root_cold; // the root's
+  const double2* gathered;  // [G][stride]
+  int64_t stride;
+  const int64_t* shard_lo;  // [G + 1] sharded layout (server g holds resources [lo[g], lo[g+1])); nullptr: replicated
+  uint32_t* status_out;     // [G] this round's flags, for dm_hier_status
+  ResCfg* leaf_cfg;         // where this server's new templates go (its leaf's, or a staged slot)
+  ResCold* leaf_cold;
+  const ResCfg* leaf_prev_cfg;   // the templates a rejected round keeps (== leaf_cfg when written in place)
+  const ResCold* leaf_prev_cold;
+  const ResCold* root_cold; // the root's safe capacity / refresh interval
   int64_t R;
-  int G;
+  int64_t leaf_lo;          // first resource of this server's leaf (0 when replicated)
+  int G;                    // servers
+  int K;                    // root rows per resource: G (replicated) or 1 (sharded: its owner's)
   int server;
+  int pad;
 };
 
 }  // namespace dm

@@ -1635,42 +1635,48 @@ __global__ void k_gather_leases(int64_t n, const int64_t* __restrict__ rows, con
   if (expiry) out_exp[i] = expiry[r];  // else resolved by k_resolve_rows
 }
 
-// server.go:242-253: {SumWants, Count} per resource, interleaved 16 B records.
-__global__ void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __restrict__ dst) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  double2 v;
-  v.x = agg[r].sum_wants;
-  v.y = __longlong_as_double(agg[r].count);
-  dst[r] = v;
-}
-
-// Intermediate-server hierarchy (server.go:227-323 on each intermediate ->
-// :822-901 on the root).  The root store holds R resources x G server rows
-// (resource r owns rows [r*G, r*G+G), server g = client g); `gathered` is the
-// all-gather of every server's k_publish records, [G][R] x 16 B.
-//
-// k_hier_validate: a server's GetServerCapacity carries one band per resource
-// whose SumWants > 0 (server.go:241-253); a band with num_clients < 1 makes the
-// root reject the whole RPC with InvalidArgument (server.go:863-866), so that
-// server requests nothing this round and keeps its configuration
-// (performRequests returns before LoadConfig, server.go:268-272).  A Count that
-// does not fit the root's 32-bit subclients column is rejected the same way
-// (kHierCountRange) instead of being clamped.
-// The status words are double-buffered by round: this round's words were zeroed by
-// the previous round's launch, and this launch zeroes the next round's (no memset).
-__global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ gathered, uint32_t* status,
-                                uint32_t* zero_next) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < G) zero_next[i] = 0;
-  if (i >= R * G) return;
-  const double2 v = gathered[i];
-  if (!(v.x > 0.0)) return;  // not requested (server.go:241)
-  const long long count = __double_as_longlong(v.y);
+// server.go:234-255: what an intermediate server sends upstream -- {SumWants, Count}
+// of every resource it holds (a band only when SumWants > 0, :241) -- plus the root's
+// validation of that request (:858-868), computed here once instead of by every
+// root copy: a band with Count < 1 fails the whole GetServerCapacity with
+// InvalidArgument (:863-866), and a Count beyond the root's 32-bit subclients
+// column is rejected the same way (kHierCountRange).  dst[1 + r] = the record of
+// resource r; dst[0] = {the flags of the whole request, 0}, written by the last
+// workgroup to arrive (sync[0] accumulates the workgroups' flags, sync[1] counts
+// them; both return to zero for the next launch).
+__global__ __launch_bounds__(256) void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __restrict__ dst,
+                                                 uint32_t* sync, int nblocks) {
+  __shared__ uint32_t wf[4];
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   uint32_t f = 0;
-  if (count < 1) f |= kHierInvalid;
-  if (count > kSubMax) f |= kHierCountRange;
-  if (f) atomicOr(&status[i / R], f);
+  if (r < R) {
+    const ResAgg a = agg[r];
+    double2 v;
+    v.x = a.sum_wants;
+    v.y = __longlong_as_double(a.count);
+    dst[1 + r] = v;
+    if (a.sum_wants > 0.0) {  // a band (server.go:241)
+      if (a.count < 1) f |= kHierInvalid;
+      if (a.count > kSubMax) f |= kHierCountRange;
+    }
+  }
+  const uint32_t w = (__ballot(f & kHierInvalid) ? kHierInvalid : 0u) | (__ballot(f & kHierCountRange) ? kHierCountRange : 0u);
+  if ((threadIdx.x & 63) == 0) wf[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0) {
+      const uint32_t all = wf[0] | wf[1] | wf[2] | wf[3];
+      if (all) (void)__hip_atomic_fetch_or((gu32*)sync, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (arrive_last(sync + 1, nblocks) && threadIdx.x == 0) {
+      const uint32_t flags = __hip_atomic_load((gu32*)sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double2 v;
+      v.x = __longlong_as_double((long long)flags);
+      v.y = 0.0;
+      dst[0] = v;
+    }
+  }
 }
 
 // One exchange round of the root.  The requests of the servers that ask for a
@@ -1688,36 +1694,62 @@ __global__ void k_hier_validate(int64_t R, int G, const double2* __restrict__ ga
 // running sums follow the reference's update sequence -- Clean's releases in row
 // order, then one Assign per request in server order -- bit for bit.
 //
-// G <= 64 servers: a wave holds 64 / P whole resources (P = G rounded up to a
-// power of two), one lane per server row.  For each server q in order, the lanes
-// of a resource walk its rows in row order by shuffles for the decision's loops
-// over store.Map (round 1, round 2, ProportionalShare's extra capacity / need:
-// the sums of a sequential Map, bit for bit the oracle's); lane q then takes the
-// Assign.  O(G) per decision, G decisions per resource.
-// The lane of `ha.server` then loads that server's template for each resource
-// exactly as performRequests + LoadConfig do (server.go:279-313,
+// Layouts (HierArgs): replicated -- every server holds every resource, the root
+// store has K = G rows per resource (row r*G + g = server g); sharded -- server g
+// holds resources [lo[g], lo[g+1]) (contiguous resource-id ranges),
+// so only the owner ever requests resource r and the root store has one row per
+// resource (K = 1).  A server whose published flags are set (a band with
+// num_clients < 1, server.go:863-866, or a Count beyond 2^31 - 2) requests nothing
+// this round.
+//
+// K <= 64 rows: a wave holds 64 / P whole resources (P = K rounded up to a power
+// of two), one lane per row.  For each row q in order, the lanes of a resource
+// walk its rows in row order by shuffles for the decision's loops over store.Map
+// (round 1, round 2, ProportionalShare's extra capacity / need: the sums of a
+// sequential Map, bit for bit the oracle's); lane q then takes the Assign.  O(K)
+// per decision, K decisions per resource.
+// The lane of `ha.server` then writes that server's template for each of its
+// resources exactly as performRequests + LoadConfig do (server.go:279-313,
 // resource.go:117-125): a requested resource takes the root's grant as capacity,
 // its expiry (Unix seconds) as the parent expiry, and the root's algorithm
 // (kind, lease length, refresh) and configured safe capacity (0 when unset,
 // server.go:894); a resource it did not request drops to the "*" default
 // template (server.go:53-63: capacity 0, safe 0, FAIR_SHARE, lease 20 s, refresh
-// 1 s, no parent expiry).  learningModeEndTime is kept (set once, resource.go:163).
+// 1 s, no parent expiry); a rejected round keeps the templates it had
+// (performRequests returns before LoadConfig, :268-272).  learningModeEndTime is
+// kept (set once, resource.go:163).
+__device__ __forceinline__ int hier_owner(const int64_t* lo, int G, int64_t r) {
+  int a = 0, b = G;  // lo[a] <= r < lo[b]
+  while (b - a > 1) {
+    const int m = (a + b) >> 1;
+    if (lo[m] <= r) a = m;
+    else b = m;
+  }
+  return a;
+}
+
 __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
-  const int G = ha.G;
-  const int P = G <= 1 ? 1 : 1 << (32 - __builtin_clz((unsigned)(G - 1)));
+  const int K = ha.K;
+  const int P = K <= 1 ? 1 : 1 << (32 - __builtin_clz((unsigned)(K - 1)));
   const int per = 64 / P;  // resources per wave
   const int lane = threadIdx.x & 63;
-  const int rl = lane / P, g = lane - rl * P;
+  const int rl = lane / P, g0 = lane - rl * P;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x < ha.G)  // the round's per-server flags (dm_hier_status)
+    ha.status_out[threadIdx.x] = (uint32_t)__double_as_longlong(ha.gathered[(int64_t)threadIdx.x * ha.stride].x);
   const int64_t r = wave * per + rl;
   if (wave * per >= ha.R) return;  // whole waves only
-  const bool valid = g < G && r < ha.R;
+  const bool valid = g0 < K && r < ha.R;
   const int64_t rr = r < ha.R ? r : 0;
-  const int64_t row = rr * G + (valid ? g : 0);
+  const int64_t row = rr * K + (valid ? g0 : 0);
+  // the server this row belongs to, and its record of the resource
+  const int g = ha.shard_lo ? hier_owner(ha.shard_lo, ha.G, rr) : g0;
+  const int64_t rec = ha.shard_lo ? rr - ha.shard_lo[g] : rr;
   double w = 0.0, h = 0.0, rw = 0.0;
   int s = 0, rs = 0;
   int64_t e = kReleased;
   bool req = false;
+  uint32_t flags = 0;
   const Res rs_cfg = load_res(p, (int)rr);
   if (valid) {
     w = p.wants[row];
@@ -1725,8 +1757,10 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     const int32_t raw = p.sub[row];  // expiry encoding (dm_device.h): root rows are explicit or released
     s = sub_value(raw);
     e = row_expiry(p, row, raw, rs_cfg.follow_exp);
-    const double2 v = ha.gathered[(int64_t)g * ha.R + rr];
-    req = ha.status[g] == 0u && v.x > 0.0;  // count in [1, kSubMax] when status is clear
+    const double2* blk = ha.gathered + (int64_t)g * ha.stride;
+    flags = (uint32_t)__double_as_longlong(blk[0].x);
+    const double2 v = blk[1 + rec];
+    req = flags == 0u && v.x > 0.0;  // count in [1, kSubMax] when the flags are clear
     rw = v.x;
     rs = req ? (int)__double_as_longlong(v.y) : 0;
   }
@@ -1741,7 +1775,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   double sh = rs_cfg.agg_has, sw = rs_cfg.agg_wants;
   const int xp = expired ? 1 : 0;
   if (__any(xp)) {
-    for (int q = 0; q < G; ++q) {
+    for (int q = 0; q < K; ++q) {
       const double hj = shfl_d(h, src(q)), wj = shfl_d(w, src(q));
       const int sj = shfl_i(s, src(q)), xj = shfl_i(xp, src(q));
       if (xj) {
@@ -1761,7 +1795,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   const bool ps = !rs_cfg.learning && rs_cfg.kind == 2;
   const int rq = req ? 1 : 0;
   double my_gets = 0.0;
-  for (int q = 0; q < G; ++q) {
+  for (int q = 0; q < K; ++q) {
     const int rq_q = shfl_i(rq, src(q));
     if (!__any(rq_q)) continue;  // no resource of this wave has server q's request
     const double rw_q = shfl_d(rw, src(q));
@@ -1800,7 +1834,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       const int sl = live ? s : ~s;  // subclients + live bit (s >= 0)
       double x = 0.0, y = 0.0;
       long long wx = rs_q;  // FairShare wantExtra starts at the request's subclients (:148)
-      for (int j = 0; j < G; ++j) {
+      for (int j = 0; j < K; ++j) {
         const double wj = shfl_d(w, src(j));
         const int sj = shfl_i(sl, src(j));
         if (!loop1 || sj < 0) continue;
@@ -1837,7 +1871,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       if (__any(loop2)) {
         double ee = 0.0;
         long long wee = rs_q;  // :189
-        for (int j = 0; j < G; ++j) {
+        for (int j = 0; j < K; ++j) {
           const double wj = shfl_d(w, src(j));
           const int sj = shfl_i(sl, src(j));
           if (!loop2 || sj < 0 || j == q) continue;
@@ -1855,7 +1889,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       sh += gets - old_h;
       sw += rw_q - old_w;
       count += rs_q - old_s;
-      if (g == q) {
+      if (g0 == q) {  // this lane is row q
         h = gets;
         w = rw_q;
         s = rs_q;
@@ -1880,7 +1914,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       p.out_expiry[row] = kReleased;
     }
   }
-  if (valid && g == 0) {
+  if (valid && g0 == 0) {  // the resource's first lane
     ResAgg a;
     a.count = count;
     a.sum_has = sh;
@@ -1891,26 +1925,45 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   }
 
   // this server's new template for the resource (server.go:279-313)
-  if (valid && g == ha.server && ha.status[g] == 0u) {
-    ResCfg* c = ha.leaf_cfg + rr;
-    ResCold* cc = ha.leaf_cold + rr;
-    if (req) {
+  if (valid && g == ha.server) {
+    const int64_t li = rr - ha.leaf_lo;  // the resource's index in this server's leaf
+    ResCfg* c = ha.leaf_cfg + li;
+    ResCold* cc = ha.leaf_cold + li;
+    const int64_t learn = ha.leaf_prev_cfg[li].learning_end_ns;  // kept (resource.go:163)
+    if (flags != 0u) {  // rejected: the templates stay (a staged slot takes a copy)
+      if (ha.leaf_prev_cfg != ha.leaf_cfg) {
+        *c = ha.leaf_prev_cfg[li];
+        *cc = ha.leaf_prev_cold[li];
+      }
+    } else if (req) {
       const ResCfg rc = p.cfg[rr];
       const ResCold rcc = ha.root_cold[rr];
       const int64_t sec = exp_new >= 0 ? exp_new / kNs : -((-exp_new + kNs - 1) / kNs);  // time.Unix(sec, 0)
-      c->capacity = my_gets;                                               // :293
-      cc->safe_capacity = __builtin_isnan(rcc.safe_capacity) ? 0.0 : rcc.safe_capacity;  // :294, :894
-      c->lease_len_s = rc.lease_len_s;                                     // :295 Algorithm
-      cc->refresh_s = rcc.refresh_s;
-      c->kind = rc.kind;
-      c->parent_expiry_ns = sec * kNs;                                     // :287-288
+      ResCfg t;
+      t.capacity = my_gets;               // :293
+      t.learning_end_ns = learn;
+      t.parent_expiry_ns = sec * kNs;     // :287-288
+      t.lease_len_s = rc.lease_len_s;     // :295 Algorithm
+      t.kind = rc.kind;
+      *c = t;
+      ResCold tc;
+      tc.safe_capacity = __builtin_isnan(rcc.safe_capacity) ? 0.0 : rcc.safe_capacity;  // :294, :894
+      tc.refresh_s = rcc.refresh_s;
+      tc.pad = 0;
+      *cc = tc;
     } else {  // the "*" default template (server.go:53-63, :305)
-      c->capacity = 0.0;
-      cc->safe_capacity = 0.0;
-      c->lease_len_s = 20;
-      cc->refresh_s = 1;
-      c->kind = 3;
-      c->parent_expiry_ns = INT64_MAX;  // expiryTimes has no entry: nil
+      ResCfg t;
+      t.capacity = 0.0;
+      t.learning_end_ns = learn;
+      t.parent_expiry_ns = INT64_MAX;  // expiryTimes has no entry: nil
+      t.lease_len_s = 20;
+      t.kind = 3;
+      *c = t;
+      ResCold tc;
+      tc.safe_capacity = 0.0;
+      tc.refresh_s = 1;
+      tc.pad = 0;
+      *cc = tc;
     }
   }
 }
@@ -1951,21 +2004,31 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
   return hipGetLastError();
 }
 
-// The 128-thread bins (3: 128 x 4, 4: 128 x 8) split by the dense hint.
-hipError_t launch_bin_split(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt,
-                            int par, int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount,
-                            hipStream_t st) {
+// The 128-thread bins (3: 128 x 4, 4: 128 x 8) split by the dense hint: the dense
+// kernel over every item, then the rest kernel over what it queued (two launches,
+// timed separately).
+hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
+                            int32_t* glist, int32_t* gcount, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (bin == 3)
+    k_block_dense<4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
+  else if (bin == 4)
+    k_block_dense<8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
+                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const unsigned rg = (unsigned)std::max(1, std::min(n, rest_grid));
-  if (bin == 3) {
-    k_block_dense<4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
+  if (bin == 3)
     k_block_rest<4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
-  } else if (bin == 4) {
-    k_block_dense<8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
+  else if (bin == 4)
     k_block_rest<8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
-  } else {
+  else
     return hipErrorInvalidValue;
-  }
   return hipGetLastError();
 }
 
@@ -2043,9 +2106,9 @@ hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t
   return hipGetLastError();
 }
 
-hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st) {
-  if (R <= 0) return hipSuccess;
-  k_publish<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(R, agg, (double2*)dst);
+hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, uint32_t* sync, hipStream_t st) {
+  const int nb = (int)std::max<int64_t>(1, (R + 255) / 256);
+  k_publish<<<(unsigned)nb, 256, 0, st>>>(R, agg, (double2*)dst, sync, nb);
   return hipGetLastError();
 }
 
@@ -2068,18 +2131,10 @@ hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, uint32_t* zero_next,
-                                hipStream_t st) {
-  if (R * G <= 0) return hipSuccess;
-  k_hier_validate<<<(unsigned)((R * G + 255) / 256), 256, 0, st>>>(R, G, (const double2*)gathered, status,
-                                                                      zero_next);
-  return hipGetLastError();
-}
-
 hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st) {
   if (ha.R <= 0) return hipSuccess;
   int P = 1;
-  while (P < ha.G) P <<= 1;
+  while (P < ha.K) P <<= 1;
   const int64_t per = 64 / P;
   const int64_t waves = (ha.R + per - 1) / per;
   k_hier_tick<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(p, ha);

@@ -21,9 +21,10 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
 hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
-hipError_t launch_bin_split(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt,
-                            int par, int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount,
-                            hipStream_t st);
+hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
+                            int32_t* glist, int32_t* gcount, hipStream_t st);
+hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
+                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
@@ -46,7 +47,7 @@ hipError_t launch_resolve_rows(int64_t n, const int64_t* rows, int64_t off, cons
                                hipStream_t st);
 hipError_t launch_gather_leases(int64_t n, const int64_t* rows, const double* gets, const int64_t* expiry,
                                double* out_gets, int64_t* out_exp, hipStream_t st);
-hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, hipStream_t st);
+hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, uint32_t* sync, hipStream_t st);
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
                                double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st);
 hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
@@ -55,8 +56,6 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
 hipError_t launch_decide(const DevParams& p, const ReqItem* items, int nitems, const ReqArgs& q, hipStream_t st);
-hipError_t launch_hier_validate(int64_t R, int G, const void* gathered, uint32_t* status, uint32_t* zero_next,
-                                hipStream_t st);
 hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st);
 }  // namespace dm
 
@@ -80,13 +79,21 @@ enum KClass {
   KC_RELEASE,
   KC_LARGE_FUSED,
   KC_SUBS,
+  KC_DENSE3,  // the 128-thread bins' split form: dense kernel, then the rest kernel
+  KC_DENSE4,
+  KC_REST3,
+  KC_REST4,
+  KC_PUBLISH,   // dm_publish_totals
+  KC_HIER_ROOT, // dm_hier_root_tick
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
                                      "block128x8",   "block256x8", "block512x8",  "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
-                                     "store_release", "large_fused", "subs_merged"};
+                                     "store_release", "large_fused", "subs_merged", "block128x4_dense",
+                                     "block128x8_dense", "block128x4_rest", "block128x8_rest", "hier_publish",
+                                     "hier_root"};
 
 template <typename T>
 struct DBuf {
@@ -243,12 +250,35 @@ struct dm_ctx {
   DBuf<ReqItem> rq_items;
   DBuf<double> rq_sc_has, rq_sc_wants;  // the round's working copy of the requested resources' rows
   DBuf<int32_t> rq_sc_sub;
-  // dm_hier_root_tick: per-server rejection flags, two rounds' worth (round r uses
-  // words [(r & 1) * kHierMaxServers, +G)); each round zeroes the next round's words
+  // dm_publish_totals: the workgroups' validation flags and their arrival counter
+  // (k_publish; both return to zero after each launch)
+  DBuf<uint32_t> pub_sync;
+  // root side of the hierarchy: the exchange's layout (dm_hier_layout) and the
+  // last round's per-server flags
+  int hier_G = 0;                    // 0: not configured (replicated, G from each call)
+  bool hier_sharded = false;
+  std::vector<int64_t> h_hier_lo;    // [G + 1] sharded bounds
+  DBuf<int64_t> hier_lo;
+  int64_t hier_stride = 0;
   DBuf<uint32_t> hier_status;
-  uint32_t hier_round = 0;
-  int hier_status_g = 0;  // G the buffer was last zeroed for
   int hier_servers = 0;
+  // leaf side: pipelined templates (dm_hier_pipeline).  An exchange stages this
+  // leaf's new templates in a free slot; the leaf's ticks take the staged templates
+  // of the exchanges enqueued before the previous tick (one tick of lag).
+  static constexpr int kTplSlots = 3;
+  bool tpl_pipe = false;
+  DBuf<ResCfg> tpl_cfg[kTplSlots];
+  DBuf<ResCold> tpl_cold[kTplSlots];
+  hipEvent_t ev_tpl_ready[kTplSlots] = {};  // root stream: the slot's templates are written
+  hipEvent_t ev_tpl_free[kTplSlots] = {};   // leaf stream: the ticks that read the slot are done
+  bool tpl_free_rec[kTplSlots] = {};        // ev_tpl_free holds a record
+  struct Staged {
+    int slot;
+    int64_t tag;  // leaf ticks issued before the exchange was enqueued
+  };
+  std::vector<Staged> tpl_pending;          // oldest first
+  std::vector<int> tpl_free_slots;
+  int64_t ticks_issued = 0;
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
   bool profiling = false;
@@ -273,6 +303,17 @@ struct dm_ctx {
     }
     hipEvent_t e = nullptr;
     (void)hipEventCreate(&e);
+    return e;
+  }
+  // HIP events around one launch on its stream while profiling is on (dm_kernel_times)
+  template <typename F>
+  hipError_t timed(int cls, hipStream_t s, F&& fn) {
+    if (!profiling) return fn();
+    ProfEvent pe{cls, take_event(), take_event()};
+    (void)hipEventRecord(pe.a, s);
+    hipError_t e = fn();
+    (void)hipEventRecord(pe.b, s);
+    pending.push_back(pe);
     return e;
   }
   void collect_profile() {
@@ -312,7 +353,11 @@ struct dm_ctx {
     bat_flags.release();
     if (h_bat_flags) (void)hipHostFree(h_bat_flags);
     h_bat_flags = nullptr;
-    row_bits.release(); upd_flags.release(); hier_status.release();
+    row_bits.release(); upd_flags.release(); hier_status.release(); hier_lo.release(); pub_sync.release();
+    for (int i = 0; i < kTplSlots; ++i) {
+      tpl_cfg[i].release();
+      tpl_cold[i].release();
+    }
     rq_rows.release(); rq_sub.release(); rq_exp.release(); rq_has.release(); rq_wants.release(); rq_gets.release();
     rq_items.release(); rq_sc_has.release(); rq_sc_wants.release(); rq_sc_sub.release();
     if (h_flags) (void)hipHostFree(h_flags);
@@ -546,7 +591,7 @@ static int check_fused(dm_ctx* c) {
 // ---------------------------------------------------------------------------
 extern "C" {
 
-const char* dm_version(void) { return "doorman-hip 0.2 (gfx950, abi 2)"; }
+const char* dm_version(void) { return "doorman-hip 0.3 (gfx950, abi 3)"; }
 
 int dm_device_count(int* out) {
   if (!out) return DM_E_INVAL;
@@ -622,6 +667,10 @@ int dm_create(int device, dm_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
+  for (int i = 0; i < dm_ctx::kTplSlots && e == hipSuccess; ++i) {
+    e = hipEventCreateWithFlags(&c->ev_tpl_ready[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_tpl_free[i], hipEventDisableTiming);
+  }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
@@ -656,6 +705,10 @@ void dm_destroy(dm_ctx* c) {
     (void)hipStreamDestroy(c->cpy);
   }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  for (int i = 0; i < dm_ctx::kTplSlots; ++i) {
+    if (c->ev_tpl_ready[i]) (void)hipEventDestroy(c->ev_tpl_ready[i]);
+    if (c->ev_tpl_free[i]) (void)hipEventDestroy(c->ev_tpl_free[i]);
+  }
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_bat)
@@ -813,6 +866,7 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
                    (int32_t)cfg->lease_length_s[r], cfg->kind[r]};
     rcold[r] = ResCold{cfg->safe_capacity[r], (int32_t)cfg->refresh_interval_s[r], 0};
   }
+  c->tpl_pending.clear();  // staged exchanges were computed for the old configuration
   DM_HIP(c, upload(c->cfg, rc.data(), (size_t)R, st), "upload config");
   DM_HIP(c, upload(c->cold, rcold.data(), (size_t)R, st), "upload config");
   c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
@@ -829,10 +883,34 @@ static int ready(dm_ctx* c) {
   return DM_OK;
 }
 
+// Pipelined hierarchy (dm_hier_pipeline): before a leaf tick, take the templates of
+// the exchanges enqueued before the previous tick (stream-ordered after their root
+// kernels); the slot they replace becomes free once the ticks that read it are done.
+static int commit_templates(dm_ctx* c) {
+  int take = -1;
+  size_t n = 0;
+  while (n < c->tpl_pending.size() && c->tpl_pending[n].tag < c->ticks_issued) take = c->tpl_pending[n++].slot;
+  for (size_t i = 0; i + 1 < n; ++i) c->tpl_free_slots.push_back(c->tpl_pending[i].slot);  // superseded
+  c->tpl_pending.erase(c->tpl_pending.begin(), c->tpl_pending.begin() + (ptrdiff_t)n);
+  if (take < 0) return DM_OK;
+  DM_HIP(c, c->join_aux(), "join");  // deferred class work also read the old templates
+  DM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_tpl_ready[take], 0), "staged templates");
+  c->main_dirty = true;  // the class streams fork after the wait
+  std::swap(c->cfg, c->tpl_cfg[take]);
+  std::swap(c->cold, c->tpl_cold[take]);
+  // the old templates (now in slot `take`) are free after the ticks already enqueued
+  DM_HIP(c, hipEventRecord(c->ev_tpl_free[take], c->stream), "template slot");
+  c->tpl_free_rec[take] = true;
+  c->tpl_free_slots.push_back(take);
+  return DM_OK;
+}
+
 int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   DM_CHECK_CTX(c);
   int rc = ready(c);
   if (rc) return rc;
+  if (c->tpl_pipe && (rc = commit_templates(c))) return rc;
+  c->ticks_issued += 1;
   const bool wb = flags & DM_WRITEBACK;
   DevParams p{};
   p.seg_off = c->seg_off.p;
@@ -888,15 +966,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p,
              c->pa_live.p, c->p_tot.p};
   hipStream_t st = c->stream;
-  auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t {
-    if (!c->profiling) return fn();
-    ProfEvent pe{cls, c->take_event(), c->take_event()};
-    (void)hipEventRecord(pe.a, s);
-    hipError_t e = fn();
-    (void)hipEventRecord(pe.b, s);
-    c->pending.push_back(pe);
-    return e;
-  };
+  auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t { return c->timed(cls, s, fn); };
   const int nch = (int)c->h_chunks.size();
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
@@ -970,9 +1040,17 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
       const int64_t queued = __atomic_load_n(c->h_dq + i, __ATOMIC_RELAXED);
       if (4 * queued <= n || ++c->dq_skip[i] >= 64) {
         c->dq_skip[i] = 0;
-        DM_HIP(c, timed(KC_BIN0 + b, s, [&] {
-                 return launch_bin_split(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
-                                         512, gl, gc, s);
+        // the rest kernel strides over whatever the dense kernel queues; its grid is
+        // only sized from the last split tick's queue (a hint: correctness never
+        // depends on it): an empty queue costs 16 workgroups that read one count
+        const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
+        DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
+                 return launch_bin_dense(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc, s);
+               }),
+               "group kernel (dense split)");
+        DM_HIP(c, timed(KC_REST3 + i, s, [&] {
+                 return launch_bin_rest(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
+                                        rest_grid, gl, gc, s);
                }),
                "group kernel (dense split)");
         c->dq_par[i] ^= 1;
@@ -1563,48 +1641,120 @@ int dm_publish_totals(dm_ctx* c, void* dst) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
-  DM_HIP(c, launch_publish(c->R, c->agg.p, dst, c->stream), "publish");
+  if (!c->pub_sync.p) {
+    DM_HIP(c, c->pub_sync.ensure(2), "publish state");
+    DM_HIP(c, hipMemsetAsync(c->pub_sync.p, 0, 2 * sizeof(uint32_t), c->stream), "publish state");
+  }
+  DM_HIP(c, c->timed(KC_PUBLISH, c->stream, [&] { return launch_publish(c->R, c->agg.p, dst, c->pub_sync.p, c->stream); }),
+         "publish");
   return DM_OK;
 }
 
-static bool root_layout_ok(dm_ctx* c, int G) {  // checked at load (seg_uniform), not per round
-  return G > 0 && G <= kHierMaxServers && c->R > 0 && c->N == c->R * (int64_t)G && c->seg_uniform == G;
+int dm_hier_layout(dm_ctx* root, int n_servers, const int64_t* shard_lo, int64_t stride) {
+  DM_ENTER(root);
+  if (n_servers <= 0 || n_servers > kHierMaxServers) return root->fail(DM_E_INVAL, "1..64 intermediate servers");
+  if (!root->store_loaded) return root->fail(DM_E_STATE, "load the root store first");
+  int64_t widest = root->R;
+  if (shard_lo) {
+    if (shard_lo[0] != 0 || shard_lo[n_servers] != root->R)
+      return root->fail(DM_E_INVAL, "shard bounds must run from 0 to the root's resource count");
+    widest = 0;
+    for (int g = 0; g < n_servers; ++g) {
+      if (shard_lo[g + 1] < shard_lo[g]) return root->fail(DM_E_INVAL, "shard bounds must be non-decreasing");
+      widest = std::max(widest, shard_lo[g + 1] - shard_lo[g]);
+    }
+  }
+  if (stride == 0) stride = 1 + widest;
+  if (stride < 1 + widest) return root->fail(DM_E_INVAL, "record stride below 1 + the largest shard");
+  root->hier_G = n_servers;
+  root->hier_sharded = shard_lo != nullptr;
+  root->hier_stride = stride;
+  if (shard_lo) {
+    root->h_hier_lo.assign(shard_lo, shard_lo + n_servers + 1);
+    DM_HIP(root, upload(root->hier_lo, root->h_hier_lo.data(), root->h_hier_lo.size(), root->stream), "shard bounds");
+  } else {
+    root->h_hier_lo.clear();
+  }
+  return DM_OK;
 }
 
-// One exchange round of the hierarchy (server.go:227-323 -> :822-901): validate
-// every server's request (k_hier_validate), decide the round on the root store
-// and load this server's template into the leaf (k_hier_tick).  Stream-ordered:
-// the all-gather that produced `gathered` must precede it on the root's stream.
+int dm_hier_pipeline(dm_ctx* leaf, int on) {
+  DM_ENTER(leaf);
+  if (!leaf->cfg_loaded) return leaf->fail(DM_E_STATE, "load the leaf's configuration first");
+  if (!on && leaf->tpl_pipe && !leaf->tpl_pending.empty()) {  // take the newest staged templates now
+    const int take = leaf->tpl_pending.back().slot;
+    DM_HIP(leaf, hipStreamWaitEvent(leaf->stream, leaf->ev_tpl_ready[take], 0), "staged templates");
+    std::swap(leaf->cfg, leaf->tpl_cfg[take]);
+    std::swap(leaf->cold, leaf->tpl_cold[take]);
+  }
+  leaf->tpl_pending.clear();
+  leaf->tpl_free_slots.clear();
+  for (int i = 0; i < dm_ctx::kTplSlots; ++i) {
+    leaf->tpl_free_slots.push_back(i);
+    leaf->tpl_free_rec[i] = false;
+  }
+  if (on) DM_HIP(leaf, hipStreamSynchronize(leaf->stream), "template slots");  // no tick still reads a slot
+  leaf->tpl_pipe = on != 0;
+  return DM_OK;
+}
+
+// One exchange round of the hierarchy (server.go:227-323 -> :822-901): decide the
+// round on the root store from every server's published block (the request and
+// its validation flags, dm_publish_totals) and write this server's templates into
+// its leaf -- in place, or into a staged slot the leaf takes one tick later
+// (dm_hier_pipeline).  Stream-ordered: the all-gather that produced `gathered`
+// must precede it on the root's stream.
 int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns, dm_ctx* leaf, int server) {
   DM_ENTER(root);
   if (!root->store_loaded || !root->cfg_loaded) return root->fail(DM_E_STATE, "root store / config not loaded");
   if (!gathered || !leaf) return root->fail(DM_E_INVAL, "null gathered buffer or leaf context");
   if (n_servers <= 0 || n_servers > kHierMaxServers)
     return root->fail(DM_E_INVAL, "1..64 intermediate servers per root store");
-  if (!root_layout_ok(root, n_servers))
-    return root->fail(DM_E_STATE, "root store must hold R resources x n_servers rows (resource r: rows r*G..r*G+G-1)");
+  if (root->hier_G != 0 && root->hier_G != n_servers)
+    return root->fail(DM_E_INVAL, "n_servers differs from the root's dm_hier_layout");
+  const bool sharded = root->hier_G != 0 && root->hier_sharded;
+  const int K = sharded ? 1 : n_servers;
+  // checked at load (seg_uniform), not per round
+  if (root->R <= 0 || root->N != root->R * (int64_t)K || root->seg_uniform != K)
+    return root->fail(DM_E_STATE, sharded ? "sharded root store must hold one row per resource"
+                                          : "root store must hold R resources x n_servers rows (resource r: rows "
+                                            "r*G..r*G+G-1)");
   if (server < 0 || server >= n_servers) return root->fail(DM_E_RANGE, "server index out of range");
   if (leaf->device != root->device) return root->fail(DM_E_INVAL, "root and leaf contexts must share a device");
-  if (!leaf->cfg_loaded || leaf->R != root->R) return root->fail(DM_E_STATE, "leaf must hold the same resources");
+  const int64_t leaf_lo = sharded ? root->h_hier_lo[server] : 0;
+  const int64_t leaf_R = sharded ? root->h_hier_lo[server + 1] - leaf_lo : root->R;
+  if (!leaf->cfg_loaded || leaf->R != leaf_R)
+    return root->fail(DM_E_STATE, "the leaf must hold exactly this server's resources");
+  const int64_t stride = root->hier_G != 0 ? root->hier_stride : 1 + root->R;
   DM_HIP(root, leaf->join_aux(), "join leaf streams");
   leaf->main_dirty = true;
-  DM_HIP(root, root->hier_status.ensure(2 * (size_t)kHierMaxServers), "hierarchy status");
+  DM_HIP(root, root->hier_status.ensure((size_t)kHierMaxServers), "hierarchy status");
   root->hier_servers = n_servers;
   const bool same = root->stream == leaf->stream;
-  if (!same) {  // root after the leaf's prior work (its config is rewritten)
+  if (!same) {  // the root round after the leaf's prior work (its publish)
     DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
     DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
   }
-  if (root->hier_status_g != n_servers) {  // first round (or a new server count): both rounds' words
-    DM_HIP(root, hipMemsetAsync(root->hier_status.p, 0, 2 * kHierMaxServers * sizeof(uint32_t), root->stream),
-           "hierarchy status");
-    root->hier_status_g = n_servers;
+  ResCfg* tcfg = leaf->cfg.p;
+  ResCold* tcold = leaf->cold.p;
+  const ResCfg* pcfg = leaf->cfg.p;
+  const ResCold* pcold = leaf->cold.p;
+  int slot = -1;
+  if (leaf->tpl_pipe) {
+    if (leaf->tpl_free_slots.empty())
+      return root->fail(DM_E_STATE, "too many staged exchanges: tick the leaf between exchanges");
+    slot = leaf->tpl_free_slots.front();
+    DM_HIP(root, leaf->tpl_cfg[slot].ensure((size_t)leaf->R), "template slot");
+    DM_HIP(root, leaf->tpl_cold[slot].ensure((size_t)leaf->R), "template slot");
+    if (leaf->tpl_free_rec[slot])  // the ticks that read the slot's old templates are done
+      DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_tpl_free[slot], 0), "template slot");
+    tcfg = leaf->tpl_cfg[slot].p;
+    tcold = leaf->tpl_cold[slot].p;
+    if (!leaf->tpl_pending.empty()) {  // a rejected round keeps the newest staged templates
+      pcfg = leaf->tpl_cfg[leaf->tpl_pending.back().slot].p;
+      pcold = leaf->tpl_cold[leaf->tpl_pending.back().slot].p;
+    }
   }
-  root->hier_round += 1;
-  uint32_t* status = root->hier_status.p + (root->hier_round & 1) * kHierMaxServers;
-  uint32_t* status_next = root->hier_status.p + ((root->hier_round + 1) & 1) * kHierMaxServers;
-  DM_HIP(root, launch_hier_validate(root->R, n_servers, gathered, status, status_next, root->stream),
-         "hierarchy validate");
   DevParams p{};
   p.seg_off = root->seg_off.p;
   p.wants = root->wants.p;
@@ -1621,10 +1771,28 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   p.res = root->agg.p;
   p.now = now_ns;
   p.recompute = 0;  // the root's running sums, updated as the reference's Clean + Assigns
-  const HierArgs ha{(const double2*)gathered, status, leaf->cfg.p, leaf->cold.p, root->cold.p,
-                    root->R, n_servers, server};
-  DM_HIP(root, launch_hier_tick(p, ha, root->stream), "hierarchy root tick");
-  if (!same) {  // the leaf's next tick after its new template
+  HierArgs ha{};
+  ha.gathered = (const double2*)gathered;
+  ha.stride = stride;
+  ha.shard_lo = sharded ? root->hier_lo.p : nullptr;
+  ha.status_out = root->hier_status.p;
+  ha.leaf_cfg = tcfg;
+  ha.leaf_cold = tcold;
+  ha.leaf_prev_cfg = pcfg;
+  ha.leaf_prev_cold = pcold;
+  ha.root_cold = root->cold.p;
+  ha.R = root->R;
+  ha.leaf_lo = leaf_lo;
+  ha.G = n_servers;
+  ha.K = K;
+  ha.server = server;
+  DM_HIP(root, root->timed(KC_HIER_ROOT, root->stream, [&] { return launch_hier_tick(p, ha, root->stream); }),
+         "hierarchy root tick");
+  if (slot >= 0) {
+    leaf->tpl_free_slots.erase(leaf->tpl_free_slots.begin());
+    DM_HIP(root, hipEventRecord(leaf->ev_tpl_ready[slot], root->stream), "staged templates");
+    leaf->tpl_pending.push_back(dm_ctx::Staged{slot, leaf->ticks_issued});
+  } else if (!same) {  // the leaf's next tick after its new templates
     DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
     DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
   }
@@ -1640,9 +1808,7 @@ int dm_hier_status(dm_ctx* root, uint32_t* status, int n) {
   if (!status || n < 0) return root->fail(DM_E_INVAL, "bad status buffer");
   if (root->hier_servers == 0) return root->fail(DM_E_STATE, "no dm_hier_root_tick yet");
   if (n != root->hier_servers) return root->fail(DM_E_INVAL, "status buffer must hold one word per server");
-  DM_HIP(root, download(status, (const uint32_t*)root->hier_status.p + (root->hier_round & 1) * kHierMaxServers, 0, n,
-                        root->stream),
-         "hierarchy status");
+  DM_HIP(root, download(status, (const uint32_t*)root->hier_status.p, 0, n, root->stream), "hierarchy status");
   DM_HIP(root, hipStreamSynchronize(root->stream), "hierarchy status");
   int bad = 0;
   for (int g = 0; g < n; ++g) bad += status[g] != 0;

@@ -6,13 +6,15 @@
   ticks with no data-path communication.
 
 * Hierarchy (server.go:227-323 on the intermediate, :822-901 on the root): every
-  GPU is one intermediate server holding its own clients of the same R
-  resources.  Per tick each server publishes {SumWants, Count} per resource
-  (dm_publish_totals), one RCCL all-gather over xGMI shares them, every rank
-  evaluates the root's round of the G server requests redundantly on its own
-  copy of the root store (R x G rows), loads its own new templates (grant,
-  root algorithm, or the "*" default) into its leaf (dm_hier_root_tick) and runs
-  its leaf tick.
+  GPU is one intermediate server.  Sharded (configs[3]): each GPU
+  holds its contiguous range of the resources; replicated: each GPU holds its own
+  clients of the same R resources.  Per exchange each server publishes its
+  request -- {SumWants, Count} per resource plus its validation flags
+  (dm_publish_totals) -- one RCCL all-gather over xGMI shares them, every rank
+  evaluates the root's round redundantly on its own copy of the root store,
+  loads its own new templates (grant, root algorithm, or the "*" default) into
+  its leaf (dm_hier_root_tick) and runs its leaf tick; pipelined, the exchange
+  runs beside the next leaf tick with one tick of lag.
 
 torch is plumbing here (device buffers and torch.distributed); import it before
 doorman_amd so the HIP library binds to torch's HIP runtime.
@@ -54,8 +56,9 @@ def shard(snap: dict, world: int, rank: int) -> dict:
 
 
 def root_snapshot(n_resources: int, n_servers: int, kind, capacity, lease_length_s=20, refresh_interval_s=5) -> dict:
-    """The root server's store for the hierarchy: R resources x G server rows,
-    all released until the first exchange (dm_hier_root_tick)."""
+    """The root server's store for the hierarchy: R resources x G server rows
+    (replicated layout; n_servers = 1 for the sharded layout's one row per
+    resource), all released until the first exchange (dm_hier_root_tick)."""
     G = n_servers
     N = n_resources * G
     return W.make_snapshot(np.full(n_resources, G), np.zeros(N), np.zeros(N), np.zeros(N, np.int64),
@@ -67,38 +70,74 @@ class HierarchicalTick:
     """One rank of the hierarchy: an intermediate server (leaf engine) plus a
     redundant copy of the root (root engine), both on this rank's GPU.
 
-    gather(src, dst): all-gather of the [R, 2] float64 records of every server into
-    dst [G * R, 2] in server order (torch.distributed.all_gather_into_tensor over
-    RCCL on a node; a local copy in single-process tests)."""
+    Layouts (dm_hier_layout): shard_lo None -- replicated, every server holds all
+    n_resources resources (root store R x G rows); shard_lo = G + 1 bounds -- sharded
+    by resource id, server g holds resources [shard_lo[g], shard_lo[g+1]) and its leaf
+    only those (root store R rows, one per resource).
 
-    def __init__(self, torch, leaf, root, n_resources: int, n_servers: int, server: int, gather):
+    gather(src, dst): all-gather of every server's published block ([stride, 2]
+    float64: record 0 = the request's validation flags, 1 + i = {SumWants, Count} of
+    its i-th resource) into dst [G * stride, 2] in server order
+    (torch.distributed.all_gather_into_tensor over RCCL on a node; a local copy in
+    single-process tests).
+
+    pipelined: the exchange (publish -> all-gather -> root round) runs on a stream of
+    its own beside the next leaf tick, and each leaf tick takes the templates of the
+    exchange enqueued before the previous tick (dm_hier_pipeline: one tick of lag, as
+    the reference's intermediate refreshes upstream on its own loop, server.go:227-323).
+    Otherwise every tick first runs its exchange, stream-ordered on one stream."""
+
+    def __init__(self, torch, leaf, root, n_resources: int, n_servers: int, server: int, gather, shard_lo=None,
+                 pipelined: bool = False):
+        from . import _lib
         self.torch = torch
         self.leaf, self.root = leaf, root
         self.R, self.G, self.g = n_resources, n_servers, server
         self.gather = gather
+        self.pipelined = pipelined
+        L = root._L
+        if shard_lo is None:
+            self.stride = 1 + self.R
+            _lib.check(L.dm_hier_layout(root._ctx, self.G, None, self.stride), root._ctx, L)
+        else:
+            lo = np.ascontiguousarray(shard_lo, dtype=np.int64)
+            assert len(lo) == self.G + 1 and lo[0] == 0 and lo[-1] == self.R
+            self.stride = 1 + int(np.diff(lo).max())
+            _lib.check(L.dm_hier_layout(root._ctx, self.G, lo.ctypes.data, self.stride), root._ctx, L)
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.totals = torch.empty((self.R, 2), dtype=torch.float64, device=dev)
-        # one server: the all-gather is the identity, so the root reads the totals in place
-        self.gathered = self.totals if self.G == 1 else torch.empty((self.G * self.R, 2), dtype=torch.float64,
-                                                                      device=dev)
-        # The library's kernels and torch's collective share ONE stream, so publish ->
-        # all-gather -> root -> grants -> leaf tick are ordered without host syncs.  It
-        # is a stream of its own: torch's default stream is the HIP null stream, which
-        # dm_set_stream cannot select (NULL restores the context's own stream) and
-        # which does not order the library's non-blocking streams.
+        nbuf = 2 if pipelined else 1  # a pipelined exchange may still read the previous step's blocks
+        self.totals = [torch.zeros((self.stride, 2), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        # one server: the all-gather is the identity, so the root reads the block in place
+        self.gathered = self.totals if self.G == 1 else [
+            torch.zeros((self.G * self.stride, 2), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        self.step = 0
+        # The library's kernels and torch's collective share streams of their own:
+        # torch's default stream is the HIP null stream, which dm_set_stream cannot
+        # select (NULL restores the context's own stream) and which does not order the
+        # library's non-blocking streams.  Unpipelined: one stream, so publish ->
+        # all-gather -> root -> templates -> leaf tick are ordered without host syncs.
         self.stream = torch.cuda.Stream(device=dev)
+        self.xstream = torch.cuda.Stream(device=dev) if pipelined else self.stream
         leaf.set_stream(self.stream.cuda_stream)
-        root.set_stream(self.stream.cuda_stream)
+        root.set_stream(self.xstream.cuda_stream)
+        _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1 if pipelined else 0), leaf._ctx, leaf._L)
 
     def exchange(self, now_ns: int):
         """publish -> all-gather -> the root's round -> this server's new templates."""
         from . import _lib
-        self.leaf.publish_totals(self.totals.data_ptr())
+        k = self.step % len(self.totals)
+        self.step += 1
+        totals, gathered = self.totals[k], self.gathered[k]
+        self.leaf.publish_totals(totals.data_ptr())
+        if self.pipelined:
+            ev = self.torch.cuda.Event()
+            ev.record(self.stream)
+            self.xstream.wait_event(ev)
         if self.G > 1:
-            with self.torch.cuda.stream(self.stream):  # the collective orders with our stream
-                self.gather(self.totals, self.gathered)
+            with self.torch.cuda.stream(self.xstream):  # the collective orders with the exchange stream
+                self.gather(totals, gathered)
         L = self.root._L
-        _lib.check(L.dm_hier_root_tick(self.root._ctx, self.gathered.data_ptr(), self.G, int(now_ns),
+        _lib.check(L.dm_hier_root_tick(self.root._ctx, gathered.data_ptr(), self.G, int(now_ns),
                                        self.leaf._ctx, self.g), self.root._ctx, L)
 
     def status(self) -> np.ndarray:
@@ -120,5 +159,17 @@ class HierarchicalTick:
                                                    f"(flags {st[bad].tolist()}: 1 = num_clients < 1, 2 = Count >= 2^31)")
 
     def tick(self, now_ns: int, asynchronous: bool = False):
-        self.exchange(now_ns)
-        self.leaf.apportion(now_ns, writeback=True, asynchronous=asynchronous)
+        if self.pipelined:  # the tick takes the templates staged one exchange ago; then this step's exchange
+            self.leaf.apportion(now_ns, writeback=True, asynchronous=True)
+            self.exchange(now_ns)
+            if not asynchronous:
+                self.sync()
+        else:
+            self.exchange(now_ns)
+            self.leaf.apportion(now_ns, writeback=True, asynchronous=asynchronous)
+
+    def sync(self):
+        self.stream.synchronize()
+        self.xstream.synchronize()
+        self.leaf.sync()
+        self.root.sync()

@@ -138,6 +138,33 @@ def uniform(n_resources, clients, kind=FAIR_SHARE, seed=1, now_ns=NOW_NS, capaci
     return make_snapshot(np.full(n_resources, clients), wants, has, 1, exp, kinds, capacity, 300, 5)
 
 
+def uniform_range(n_resources, clients, r0, r1, kind=FAIR_SHARE, seed=3, now_ns=NOW_NS, capacity=1000.0,
+                  block=1000) -> dict:
+    """Resources [r0, r1) of the n_resources x clients uniform workload (the C1 / C3
+    shape), generated block by block -- resource block b from its own generator
+    (seed, b) -- so that the shards of a node (hierarchy.partition) together hold
+    exactly the store one GPU would hold (configs[3]: one 100M-lease snapshot
+    sharded by resource id)."""
+    fair = capacity / clients
+    wants, exp = [], []
+    for b in range(r0 // block, (r1 + block - 1) // block):
+        lo, hi = b * block, min((b + 1) * block, n_resources)
+        rng = np.random.default_rng([seed, b])
+        n = (hi - lo) * clients
+        w = rng.uniform(0.5, 1.5, n) * fair
+        e = now_ns + rng.integers(1, 300, n, dtype=np.int64) * NS
+        a, z = (max(lo, r0) - lo) * clients, (min(hi, r1) - lo) * clients
+        wants.append(w[a:z])
+        exp.append(e[a:z])
+    R = r1 - r0
+    w = np.concatenate(wants) if wants else np.zeros(0)
+    has = np.minimum(w, fair)  # what the previous tick granted (sum_has <= capacity)
+    kinds = (np.where(np.arange(r0, r1) % 2 == 0, FAIR_SHARE, PROPORTIONAL_SHARE).astype(np.int32)
+             if kind == "mixed" else kind)
+    return make_snapshot(np.full(R, clients), w, has, 1, np.concatenate(exp) if exp else np.zeros(0, np.int64),
+                         kinds, capacity, 300, 5)
+
+
 def c1(seed=1, kind=FAIR_SHARE, now_ns=NOW_NS) -> dict:
     """C1: 10,000 resources x 1,000 clients (10M leases), uniform wants."""
     return uniform(10_000, 1_000, kind=kind, seed=seed, now_ns=now_ns)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DM_ABI_VERSION 2
+#define DM_ABI_VERSION 3
 
 /* return codes */
 #define DM_OK 0
@@ -228,44 +228,67 @@ int dm_read_resources(dm_ctx* ctx, int64_t r0, int64_t n, int64_t* count, double
  * DM_E_ARGUMENT when some num_clients < 1 */
 int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t n, double* wants_total,
                        int64_t* subclients_total);
-/* server.go:234-255: per-resource {SumWants f64, Count i64} of the current store into a
- * device buffer (16 B x R, interleaved), ready for an RCCL all-gather */
+/* server.go:234-255: what this intermediate server sends upstream, into a device buffer
+ * of 1 + R records of 16 B, ready for an RCCL all-gather: record 1 + r = {SumWants f64,
+ * Count i64} of resource r (the root sees a band where SumWants > 0, :241); record 0 =
+ * {the request's validation flags as int64 bits, 0}: DM_HIER_INVALID when some band has
+ * Count < 1 (the root fails the whole GetServerCapacity, :863-866), DM_HIER_COUNT_RANGE
+ * when a Count does not fit the root's 32-bit subclients column.  Stream-ordered. */
 int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
+
+/* Layout of the exchange, set once on the root context (default: replicated, with
+ * n_servers from each dm_hier_root_tick and stride 1 + R):
+ *   shard_lo == NULL  replicated: every server holds all R resources of the root; the
+ *                     root store holds R x n_servers rows (resource r: rows r*G .. r*G+G-1).
+ *   shard_lo != NULL  sharded by resource id: n_servers + 1 non-decreasing
+ *                     bounds from 0 to R; server g holds resources [shard_lo[g],
+ *                     shard_lo[g+1]) and only it requests them; the root store holds one
+ *                     row per resource (its owner's).
+ * stride: records per server block in the gathered buffer (server g's dm_publish_totals
+ * block starts at record g * stride), >= 1 + the largest shard; 0 = exactly that. */
+int dm_hier_layout(dm_ctx* root, int n_servers, const int64_t* shard_lo, int64_t stride);
 
 /* One exchange round of the intermediate-server hierarchy, on the root store of this
  * server's device (every server evaluates the root redundantly):
  *
- *   performRequests        go/server/doorman/server.go:227-323  -> the gathered dm_publish_totals records
+ *   performRequests        go/server/doorman/server.go:227-323  -> the gathered dm_publish_totals blocks
  *   GetServerCapacity      go/server/doorman/server.go:822-901  -> the root's round below
  *   Server.LoadConfig      go/server/doorman/server.go:187-218  -> this server's new leaf templates
  *   Resource.LoadConfig    go/server/doorman/resource.go:117-125
  *
- * `root` holds R resources x n_servers rows (resource r owns rows
- * [r*n_servers, (r+1)*n_servers), row g = intermediate server g); dev_gathered is the
- * all-gather of every server's dm_publish_totals ([n_servers][R] x 16 B).
+ * dev_gathered holds every server's dm_publish_totals block (dm_hier_layout).
  *   - Server g requests resource r when its SumWants > 0 (server.go:241): has 0
  *     (Has is never filled, :244/:873), wants = SumWants, subclients = Count.
- *     A band with Count < 1 makes the root reject server g's whole request
- *     (codes.InvalidArgument, :863-866); Count >= 2^31 - 1 (beyond the root's 32-bit
- *     subclients column) is rejected the same way.  A rejected server requests
- *     nothing this round and its leaf keeps its templates (:268-272); see
- *     dm_hier_status.
- *   - The round's requests are decided against the root store as it was before the
- *     round (Clean, then Learn or the resource's algorithm with each request's own
- *     values), then assigned; servers that do not request keep their root lease
- *     until it expires.  The root's running sums follow Clean + one Assign per
- *     request in server order.
- *   - The leaf (`leaf`, this server's store, same device and resources) loads its
- *     new templates: a requested resource takes the grant as capacity, the grant's
+ *     A server whose block carries validation flags requests nothing this round and
+ *     its leaf keeps its templates (:268-272); see dm_hier_status.
+ *   - The round's requests are decided one after another in server order, as the
+ *     root's res.mu serialises GetServerCapacity calls (resource.go:103-104): Clean,
+ *     then Learn or the resource's algorithm with the request's own values against
+ *     the store as the earlier requests' Assigns left it, then its Assign
+ *     (store.go:153-167) -- so the grants never exceed what the reference gives.
+ *     Servers that do not request keep their root lease until it expires.
+ *   - The leaf (`leaf`: this server's store of its own resources, same device) gets
+ *     its new templates: a requested resource takes the grant as capacity, the grant's
  *     expiry in Unix seconds as parent expiry, and the root's algorithm (kind, lease
  *     length, refresh interval) and configured safe capacity (0 when unset,
  *     :293-296,:894); every other resource drops to the "*" default template
  *     (capacity 0, safe capacity 0, FAIR_SHARE, lease 20 s, refresh 1 s, no parent
  *     expiry; server.go:53-63,:305).  Learning-mode end times are kept (fixed when a
- *     resource is created, resource.go:153-163).
- * 1 <= n_servers <= 64.  Two stream-ordered launches; returns without waiting. */
+ *     resource is created, resource.go:153-163).  Without dm_hier_pipeline they are
+ *     written in place, ordered before the leaf's next tick; with it they are staged.
+ * 1 <= n_servers <= 64.  One stream-ordered launch; returns without waiting. */
 int dm_hier_root_tick(dm_ctx* root, const void* dev_gathered, int n_servers, int64_t now_ns, dm_ctx* leaf,
                       int server);
+
+/* Pipelined templates on a leaf (on = 1): each dm_hier_root_tick for this leaf stages
+ * its templates instead of writing them, and every dm_apportion of the leaf first takes
+ * the templates of the exchanges enqueued before the previous dm_apportion call -- one
+ * tick of lag, as the reference's intermediate refreshes upstream on its own loop
+ * (server.go:227-323) while it keeps serving clients -- so the exchange (publish,
+ * all-gather, root round) can run on a stream of its own beside the next leaf tick.
+ * At most 3 staged exchanges; off (default) takes the newest staged templates. */
+int dm_hier_pipeline(dm_ctx* leaf, int on);
+
 /* Per-server outcome of the last dm_hier_root_tick (waits for it): status[g] = 0 when
  * server g's request was accepted, else DM_HIER_INVALID (a band with num_clients < 1,
  * server.go:863-866) and/or DM_HIER_COUNT_RANGE.  Returns the number of rejected

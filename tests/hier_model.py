@@ -55,6 +55,10 @@ class Root:
         out = {}
         for r in range(self.R):
             st = self.stores[r]
+            # Clean (store.go:169-181) on every resource, as the device's round does; the
+            # reference cleans a resource at its next Decide, which leaves every later
+            # decision the same
+            st.clean(now)
             for g in range(self.G):
                 if requests[g] is not None and r in requests[g]:
                     w, s = requests[g][r]

@@ -86,9 +86,32 @@ def assert_root_equal(e, model, label):
         assert res[k].tobytes() == sums[k].tobytes(), f"{label}: root running {k}"
 
 
-def published(gathered, G, R):
+def published(gathered, G, R, stride=None):
+    """Every server's published block (dm_publish_totals): (SumWants, Count, flags)."""
+    S = R + 1 if stride is None else stride
     rec = gathered.cpu().numpy()
-    return [(rec[g * R:(g + 1) * R, 0].copy(), rec[g * R:(g + 1) * R, 1].copy().view(np.int64)) for g in range(G)]
+    out = []
+    for g in range(G):
+        b = rec[g * S:g * S + 1 + R]
+        out.append((b[1:, 0].copy(), b[1:, 1].copy().view(np.int64), int(b[0, 0:1].view(np.int64)[0])))
+    return out
+
+
+def blocks(sum_wants, counts, flags=None):
+    """A gathered buffer built on the host: one block per server, record 0 = flags."""
+    G, R = sum_wants.shape
+    rec = np.zeros((G, R + 1, 2))
+    rec[:, 1:, 0] = sum_wants
+    rec[:, 1:, 1] = np.ascontiguousarray(counts, dtype=np.int64).view(np.float64)
+    if flags is not None:
+        rec[:, 0, 0] = np.asarray(flags, dtype=np.int64).view(np.float64)
+    return rec.reshape(G * (R + 1), 2)
+
+
+def model_flags(sum_wants, counts):
+    """The validation dm_publish_totals attaches (server.go:863-866 + the 32-bit column)."""
+    band = sum_wants > 0
+    return (np.any(band & (counts < 1)) * 1) | (np.any(band & (counts > 2**31 - 2)) * 2)
 
 
 def exchange_all(L, roots, leaves, gathered, G, now):
@@ -125,21 +148,22 @@ def test_hierarchy_rounds_match_the_reference_model(G, clients):
         tpl.append(cfg)
     roots = [root_engine(rcfg, G) for _ in range(G)]
     model = M.Root(rcfg, G)
-    gathered = torch.zeros((G * R, 2), dtype=torch.float64, device="cuda")
+    gathered = torch.zeros((G * (R + 1), 2), dtype=torch.float64, device="cuda")
     for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 40 * W.NS]):
         if t == 2 and G > 1:  # server 1 stops asking for a quarter of the resources
             so = leaves[1].seg_off
             rows = np.arange(so[0], so[R // 4])
             leaves[1].update_wants(rows, np.zeros(len(rows)))
         for g in range(G):
-            leaves[g].publish_totals(gathered[g * R:(g + 1) * R].data_ptr())
+            leaves[g].publish_totals(gathered[g * (R + 1):(g + 1) * (R + 1)].data_ptr())
             leaves[g].sync()
         totals = published(gathered, G, R)
         for g in range(G):  # what the leaves publish: their store's running sums (server.go:235-250)
             res = leaves[g].resources(safe=False)
             assert totals[g][0].tobytes() == res["sum_wants"].tobytes()
             assert totals[g][1].tobytes() == res["count"].tobytes()
-        reqs = [M.server_request(*totals[g]) for g in range(G)]
+            assert totals[g][2] == model_flags(totals[g][0], totals[g][1])
+        reqs = [M.server_request(*totals[g][:2]) for g in range(G)]
         resp = model.round(now, reqs)
         pre = [leaf_snapshot(leaves[g], tpl[g]) for g in range(G)]
         exchange_all(L, roots, leaves, gathered, G, now)
@@ -188,12 +212,11 @@ def test_root_round_grants_stay_within_capacity(G):
     leaf.load(M.with_config(W.uniform(R, 20, kind=W.FAIR_SHARE, seed=1), M.default_config(R)))
     model = M.Root(rcfg, G)
     rng = np.random.default_rng(G)
-    gathered = torch.zeros((G * R, 2), dtype=torch.float64, device="cuda")
+    gathered = torch.zeros((G * (R + 1), 2), dtype=torch.float64, device="cuda")
     for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 10 * W.NS]):
         sw = rng.uniform(100.0, 300.0, (G, R))  # every server wants more than C
         cnt = rng.integers(1, 40, (G, R)).astype(np.int64)
-        rec = np.stack([sw.reshape(-1), cnt.reshape(-1).view(np.float64)], axis=1)
-        gathered.copy_(torch.from_numpy(rec))
+        gathered.copy_(torch.from_numpy(blocks(sw, cnt)))
         resp = model.round(now, [M.server_request(sw[g], cnt[g]) for g in range(G)])
         _lib.check(L.dm_hier_root_tick(roots[0]._ctx, gathered.data_ptr(), G, now, leaf._ctx, 0), roots[0]._ctx)
         roots[0].sync()
@@ -235,17 +258,16 @@ def test_rejected_server_keeps_its_templates_and_root_rows():
         e.load(M.with_config(s, cfg))
         leaves.append(e)
         tpl.append(cfg)
-    rec = np.zeros((G * R, 2))
-    rec[:, 0] = rng.uniform(10.0, 900.0, G * R)
-    cnt = rng.integers(1, 40, G * R).astype(np.int64)
+    sw = rng.uniform(10.0, 900.0, (G, R))
+    cnt = rng.integers(1, 40, (G, R)).astype(np.int64)
     for t, (bad, value) in enumerate([(None, None), (1, 0), (2, 2**31), (None, None)]):
         c = cnt.copy()
         if bad is not None:
-            c[bad * R + 5] = value
-        rec[:, 1] = c.view(np.float64)
-        gathered = torch.from_numpy(rec).to("cuda")
-        totals = [(rec[g * R:(g + 1) * R, 0], c[g * R:(g + 1) * R]) for g in range(G)]
-        reqs = [M.server_request(*totals[g]) for g in range(G)]
+            c[bad, 5] = value
+        flags = [model_flags(sw[g], c[g]) for g in range(G)]
+        gathered = torch.from_numpy(blocks(sw, c, flags)).to("cuda")
+        reqs = [M.server_request(sw[g], c[g]) for g in range(G)]
+        assert [r is None for r in reqs] == [f != 0 for f in flags]
         now = NOW + t * W.NS
         resp = model.round(now, reqs)
         exchange_all(L, roots, leaves, gathered, G, now)
@@ -264,10 +286,9 @@ def test_rejected_server_keeps_its_templates_and_root_rows():
     # HierarchicalTick.check() raises for a rejected server
     ht = HierarchicalTick(torch, leaves[0], roots[0], R, G, 0, lambda src, dst: None)
     c = cnt.copy()
-    c[3] = 0
-    rec[:, 1] = c.view(np.float64)
-    ht.gathered.copy_(torch.from_numpy(rec))
-    L.dm_hier_root_tick(roots[0]._ctx, ht.gathered.data_ptr(), G, NOW + 9 * W.NS, leaves[0]._ctx, 0)
+    c[0, 3] = 0
+    ht.gathered[0].copy_(torch.from_numpy(blocks(sw, c, [model_flags(sw[g], c[g]) for g in range(G)])))
+    L.dm_hier_root_tick(roots[0]._ctx, ht.gathered[0].data_ptr(), G, NOW + 9 * W.NS, leaves[0]._ctx, 0)
     with pytest.raises(_lib.DmError):
         ht.check()
     for e in leaves + roots:
@@ -344,3 +365,163 @@ def test_hierarchical_tick_shares_one_stream_and_matches_synchronous_steps():
         root.close()
     (g1, e1), (g2, e2) = outs
     assert g1.tobytes() == g2.tobytes() and e1.tobytes() == e2.tobytes()
+
+
+def test_publish_carries_the_roots_validation():
+    """dm_publish_totals: record 1 + r = {SumWants, Count} of resource r; record 0 =
+    the flags the root's GetServerCapacity would raise for this request
+    (server.go:858-868): a band (SumWants > 0) with Count < 1 -> DM_HIER_INVALID, a
+    Count beyond the root's 32-bit column -> DM_HIER_COUNT_RANGE; a resource with
+    Count < 1 but no wants is no band and raises nothing."""
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    cases = {
+        "ok": ([5, 7, 300], {}),
+        "zero_count_no_wants": ([3, 2], {"sub0": 0, "wants0": 0.0}),
+        "zero_count_band": ([3, 2, 600], {"sub0": 0}),
+        "count_range": ([2, 1000], {"big0": True}),
+    }
+    for name, (sizes, how) in cases.items():
+        sizes = np.asarray(sizes, dtype=np.int64)
+        N = int(sizes.sum())
+        sub = np.ones(N, np.int64)
+        wants = np.full(N, 3.0)
+        if "sub0" in how:
+            sub[:sizes[0]] = 0
+        if "wants0" in how:
+            wants[:sizes[0]] = 0.0
+        if "big0" in how:
+            sub[:2] = 2**31 - 2
+        snap = W.make_snapshot(sizes, wants, np.zeros(N), sub, np.full(N, NOW + 60 * W.NS), W.FAIR_SHARE, 100.0)
+        R = len(sizes)
+        buf = torch.full((R + 3, 2), -7.0, dtype=torch.float64, device="cuda")
+        with Engine(0) as e:
+            e.load(snap)
+            for _ in range(2):  # twice: the flag accumulator returns to zero after each launch
+                e.publish_totals(buf.data_ptr())
+                e.sync()
+                rec = buf.cpu().numpy()
+                (sw, cnt, flags), = published(buf, 1, R)
+                np.testing.assert_array_equal(sw, snap["agg_sum_wants"])
+                np.testing.assert_array_equal(cnt, snap["agg_count"])
+                assert flags == model_flags(snap["agg_sum_wants"], snap["agg_count"]), name
+                assert rec[0, 1] == 0.0 and np.all(rec[R + 1:] == -7.0), name  # nothing past the block
+        want = {"ok": 0, "zero_count_no_wants": 0, "zero_count_band": _lib.DM_HIER_INVALID,
+                "count_range": _lib.DM_HIER_COUNT_RANGE}[name]
+        assert flags == want, (name, flags)
+
+
+def _shard_rows(model, lo, R):
+    """The model's root rows in the sharded device layout: resource r's one row is its
+    owner's (server g with lo[g] <= r < lo[g + 1])."""
+    G = model.G
+    rows = model.rows()
+    owner = np.searchsorted(lo, np.arange(R), side="right") - 1
+    idx = np.arange(R) * G + owner
+    return {k: v[idx] for k, v in rows.items()}
+
+
+def _shard_templates(prev, g, resp, root_cfg, lo):
+    """Server g's templates after an exchange, on its own resources [lo[g], lo[g+1])."""
+    a, b = int(lo[g]), int(lo[g + 1])
+    local = {(g, r - a): l for (h, r), l in resp.items() if h == g and a <= r < b}
+    cfg = {k: np.asarray(root_cfg[k])[a:b] for k in CFG_FIELDS_ALL}
+    return M.leaf_templates(prev, g, local, cfg)
+
+
+CFG_FIELDS_ALL = W.CFG_FIELDS
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_sharded_exchange_matches_the_reference_model(pipelined):
+    """configs[3]'s layout: resources sharded by id over G servers,
+    each server an intermediate of its own range; the root (one row per resource,
+    its owner's) evaluated redundantly by every server from the gathered blocks.
+    Pipelined (dm_hier_pipeline): each leaf tick takes the templates of the exchange
+    enqueued before the previous tick (one tick of lag).  Every step: root copies
+    bit for bit against the model, every leaf's templates bit for bit, leaf leases
+    against the oracle on the leaf's store under the templates the model says that
+    tick used."""
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import partition, root_snapshot
+    torch.cuda.set_device(0)
+    L = _lib.lib()
+    G = 3
+    rng = np.random.default_rng(31 + pipelined)
+    sizes = rng.integers(5, 700, 60)
+    R = len(sizes)
+    lo = partition(sizes, G)
+    S = 1 + int(np.diff(lo).max())
+    rcfg = root_config(R, rng)
+    full = W.make_snapshot(sizes, rng.uniform(0.2, 3.0, int(sizes.sum())) * 1000.0 / np.repeat(sizes, sizes),
+                           0.0, 1, NOW + 60 * W.NS, W.FAIR_SHARE, 1000.0)
+    leaves, roots, tpl = [], [], []
+    for g in range(G):
+        shard = W.subset(full, np.arange(lo[g], lo[g + 1]))
+        cfg = M.default_config(int(lo[g + 1] - lo[g]))
+        e = Engine(0)
+        e.load(M.with_config(shard, cfg))
+        if pipelined:
+            _lib.check(L.dm_hier_pipeline(e._ctx, 1), e._ctx)
+        leaves.append(e)
+        tpl.append(cfg)
+        root = Engine(0)
+        root.load(M.with_config(root_snapshot(R, 1, W.FAIR_SHARE, 1.0), rcfg))
+        _lib.check(L.dm_hier_layout(root._ctx, G, lo.ctypes.data, S), root._ctx)
+        roots.append(root)
+    model = M.Root(rcfg, G)
+    gathered = torch.zeros((G * S, 2), dtype=torch.float64, device="cuda")
+    staged = []  # templates after each exchange, oldest first (pipelined)
+    for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 30 * W.NS, NOW + 31 * W.NS]):
+        used = tpl if not pipelined else (staged[t - 2] if t >= 2 else [M.default_config(int(lo[g + 1] - lo[g]))
+                                                                         for g in range(G)])
+        if pipelined:  # tick first (it takes the exchange of two steps ago), then this step's exchange
+            for g in range(G):
+                pre = leaf_snapshot(leaves[g], used[g])
+                leaves[g].apportion(now, writeback=True)
+                assert_cfg_equal(leaves[g].config(), used[g], f"step {t} leaf {g} templates in use")
+                gets, exp = leaves[g].leases()
+                assert_leases_match(pre, gets, exp, O.apportion(pre, now), f"step {t} leaf {g}")
+        for g in range(G):
+            leaves[g].publish_totals(gathered[g * S:(g + 1) * S].data_ptr())
+            leaves[g].sync()
+        blocks_ = published(gathered, G, S - 1, S)
+        reqs = []
+        for g in range(G):
+            n = int(lo[g + 1] - lo[g])
+            sw, cnt = blocks_[g][0][:n], blocks_[g][1][:n]
+            req = M.server_request(sw, cnt)
+            reqs.append(None if req is None else {int(lo[g]) + r: v for r, v in req.items()})
+        resp = model.round(now, reqs)
+        for g in range(G):
+            _lib.check(L.dm_hier_root_tick(roots[g]._ctx, gathered.data_ptr(), G, now, leaves[g]._ctx, g), roots[g]._ctx)
+        for e in roots + leaves:
+            e.sync()
+        rows = _shard_rows(model, lo, R)
+        for g in range(G):
+            st, res = roots[g].read_store(), roots[g].resources(safe=False)
+            for k in ("has", "wants", "subclients", "expiry_ns"):
+                assert st[k].tobytes() == rows[k].tobytes(), f"step {t} root copy {g}: {k}"
+            sums = model.sums()
+            for k in ("count", "sum_has", "sum_wants"):
+                assert res[k].tobytes() == sums[k].tobytes(), f"step {t} root copy {g}: running {k}"
+        new = [tpl[g] if reqs[g] is None else _shard_templates(tpl[g], g, resp, model.cfg, lo) for g in range(G)]
+        tpl = new
+        if pipelined:
+            staged.append(new)
+        else:
+            for g in range(G):
+                assert_cfg_equal(leaves[g].config(), tpl[g], f"step {t} leaf {g}")
+                pre = leaf_snapshot(leaves[g], tpl[g])
+                leaves[g].apportion(now, writeback=True)
+                gets, exp = leaves[g].leases()
+                assert_leases_match(pre, gets, exp, O.apportion(pre, now), f"step {t} leaf {g}")
+        for (g, r), l in resp.items():  # one request per resource: FairShare / PS / Static never exceed C
+            if rcfg["kind"][r] != W.NO_ALGORITHM:
+                assert l.has <= rcfg["capacity"][r] * (1 + 1e-12), (t, g, r)
+    for e in leaves + roots:
+        e.close()

@@ -123,3 +123,19 @@ def test_rows_to_mask_round_trip():
     assert mask.dtype == np.uint64 and len(mask) == (1000 + 63) // 64
     got = [128 + 64 * w + j for w in range(len(mask)) for j in range(64) if (int(mask[w]) >> j) & 1]
     np.testing.assert_array_equal(got, rows)
+
+
+def test_uniform_range_shards_make_the_whole_store():
+    """configs[3]: the ranks' shards of the 100M-lease C3 snapshot (W.uniform_range,
+    generated block by block) are exactly the rows of the whole store; bench.py's
+    bounds split 100k resources evenly and cover every lease once at N = 1..8."""
+    import bench
+    full = W.uniform_range(5000, 10, 0, 5000, seed=9)
+    b = H.partition(np.full(5000, 10), 3)
+    parts = [W.uniform_range(5000, 10, int(b[k]), int(b[k + 1]), seed=9) for k in range(3)]
+    for k in ("wants", "has", "expiry_ns", "subclients"):
+        np.testing.assert_array_equal(full[k], np.concatenate([p[k] for p in parts]))
+    for world in range(1, 9):
+        bb = bench.c3_bounds(world)
+        assert bb[0] == 0 and bb[-1] == bench.C3_R and np.all(np.diff(bb) > 0)
+        assert np.diff(bb).max() - np.diff(bb).min() <= 1
