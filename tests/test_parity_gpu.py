@@ -861,3 +861,137 @@ def test_dense_subclients_state(monkeypatch, cols, split):
         assert eng.store_stats()["dense_resources"] == want, f"tick {rnd}"
     assert eng.store_stats()["dense_resources"] == 0  # every follower lapsed at the last tick
     eng.close()
+
+
+def _c4_store(rng, R, n, learning_frac=0.05, short_frac=0.1):
+    """configs[4]'s store shape at test size: FS/PS mixed, 5% learning resources, 2%
+    free slots, loaded rows with explicit expiries (some already past), and a tenth
+    of the resources with a 4-s lease (shorter than the 5-s round: their leases lapse
+    between ticks, so every round's Clean releases rows)."""
+    snap = W.uniform(R, n, kind="mixed", seed=int(rng.integers(1 << 30)))
+    snap["learning_end_ns"] = np.where(rng.random(R) < learning_frac, NOW + 3600 * W.NS, W.INT64_MIN).astype(np.int64)
+    snap["lease_length_s"] = np.where(rng.random(R) < short_frac, 4, 300).astype(np.int64)
+    N = len(snap["wants"])
+    free = rng.random(N) < 0.02
+    snap["wants"][free] = 0.0
+    snap["has"][free] = 0.0
+    snap["subclients"] = np.where(free, 0, 1).astype(np.int64)
+    snap["expiry_ns"] = np.where(free, W.RELEASED, NOW + rng.integers(-20, 3600, N) * W.NS).astype(np.int64)
+    return W.add_store_sums(snap)
+
+
+def _c4_round(rng, host, now):
+    """One round's updates as bench.streaming_step makes them: 10% wants refresh as a
+    row mask + packed values, 1% departures, arrivals into free rows."""
+    N = len(host["wants"])
+    alive = np.flatnonzero(host["expiry_ns"] != W.RELEASED)
+    upd = np.sort(rng.choice(alive, len(alive) // 10, replace=False))
+    w = rng.uniform(0.5, 1.5, len(upd))
+    rest = np.setdiff1d(alive, upd)
+    gone = np.sort(rng.choice(rest, max(1, len(alive) // 100), replace=False))
+    pool = np.setdiff1d(np.flatnonzero(host["expiry_ns"] == W.RELEASED), gone)
+    new = np.sort(rng.choice(pool, min(len(pool), len(gone)), replace=False))
+    k = len(new)
+    return (W.rows_to_mask(upd, N), w, gone, new, np.zeros(k), rng.uniform(0.5, 1.5, k), np.ones(k, np.int64),
+            np.full(k, now + 3600 * W.NS, np.int64), upd)
+
+
+def _apply_host(host, upd, w, gone, new, nh, nw, ns, ne):
+    """The same round on the host copy: Assign of the new wants (store.go:153-167),
+    Release (store.go:142-151), Assign of the arrivals."""
+    host["wants"][upd] = w
+    for k, v in (("wants", 0.0), ("has", 0.0), ("subclients", 0), ("expiry_ns", W.RELEASED)):
+        host[k][gone] = v
+    host["wants"][new], host["has"][new], host["subclients"][new], host["expiry_ns"][new] = nw, nh, ns, ne
+    W.add_store_sums(host)
+
+
+def _writeback_host(host, ref):
+    live = ref["expiry_ns"] != W.RELEASED
+    host["has"] = np.where(live, ref["gets"], 0.0)
+    host["wants"] = np.where(live, host["wants"], 0.0)
+    host["subclients"] = np.where(live, host["subclients"], 0)
+    host["expiry_ns"] = ref["expiry_ns"].copy()
+
+
+@pytest.mark.parametrize("cols", ["inplace", "alternate"])
+def test_c4_loop_store_apply_matches_oracle(eng, cols):
+    """configs[4]'s own loop under the oracle.  Every 5-s round the bench's
+    update call -- dm_store_apply with the wants refresh as a row mask, departures and
+    arrivals -- then a writeback tick; 5% learning resources, leases that lapse
+    between rounds (4-s lease resources, loaded rows whose explicit expiry passes).
+    A host copy takes the same updates and each tick's writeback; the oracle decides
+    every round (store.go:142-181, resource.go:108-111) from exact sums while the
+    device uses its running sums."""
+    rng = np.random.default_rng(404)
+    snap = _c4_store(rng, 2000, 300)
+    eng.load(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    now = NOW
+    released_by_clean = 0
+    for rnd in range(6):
+        now += 5 * W.NS
+        mask, w, gone, new, nh, nw, ns, ne, upd = _c4_round(rng, host, now)
+        eng.apply(mask, w, gone, (new, nh, nw, ns, ne))
+        _apply_host(host, upd, w, gone, new, nh, nw, ns, ne)
+        res = eng.resources(safe=False)
+        np.testing.assert_array_equal(res["count"], host["agg_count"])  # the running Count, exact
+        assert float_close(res["sum_wants"], host["agg_sum_wants"], np.maximum(snap["capacity"], 1.0)).all()
+        eng.apportion(now, writeback=True, wb_columns=cols)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now)
+        assert_leases_match(host, gets, exp, ref, f"C4 loop round {rnd}")
+        released_by_clean += int(((host["expiry_ns"] != W.RELEASED) & (ref["expiry_ns"] == W.RELEASED)).sum())
+        _writeback_host(host, ref)
+    assert released_by_clean > 0  # Clean released leases during the loop
+    st = eng.read_store()
+    for k in ("subclients", "expiry_ns"):
+        np.testing.assert_array_equal(st[k], host[k])
+
+
+def test_c4_full_size_properties_after_bench_rounds(eng):
+    """configs[4] at full per-GPU size (125M leases, bench.make_workload("c4")):
+    three of the bench's own rounds (bench.streaming_step: dm_store_apply + writeback
+    tick), then size-independent properties over every resource: the running Count
+    equals the live rows (bit-exact; every client has one subclient) and the running
+    SumHas equals the sum of the live leases' gets within 1e-9 * capacity."""
+    import bench
+    snap = bench.make_workload("c4", 0)
+    eng.load(snap)
+    step = bench.streaming_step(eng, snap, 0, 3)
+    for _ in range(3):
+        step()
+    eng.sync()
+    gets, exp = eng.leases()
+    res = eng.resources(safe=False)
+    so = snap["seg_off"]
+    live = exp != W.RELEASED
+    np.testing.assert_array_equal(res["count"], np.add.reduceat(live.astype(np.int64), so[:-1]))
+    per_res = np.add.reduceat(np.where(live, gets, 0.0), so[:-1])
+    np.testing.assert_allclose(res["sum_has"], per_res, rtol=0, atol=1e-9 * 1000.0)
+    assert live.sum() > 0.97 * len(live)
+    del snap, gets, exp, live
+
+
+def test_configs0_through_the_hip_path(eng):
+    """BASELINE configs[0] (1 resource x 1,000 clients, ProportionalShare,
+    algorithm.go:213-293) through dm_apportion: every lease against the oracle's
+    literal per-request Decide (one private store copy per client) and its closed
+    form; then three writeback ticks against the oracle replaying them."""
+    snap = W.c0()
+    eng.load(snap)
+    eng.apportion(NOW)
+    gets, exp = eng.leases()
+    for mode in ("literal", "closed"):
+        ref = O.apportion(snap, NOW, mode=mode)
+        assert_leases_match(snap, gets, exp, ref, f"configs[0] vs oracle {mode}")
+        assert_resources_match(snap, eng.resources(), ref, f"configs[0] {mode}")
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    for t in range(3):
+        now = NOW + t * W.NS
+        eng.apportion(now, writeback=True)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now, mode="literal")
+        assert_leases_match(host, gets, exp, ref, f"configs[0] writeback tick {t}")
+        _writeback_host(host, ref)
+        W.add_store_sums(host)
