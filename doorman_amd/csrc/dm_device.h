@@ -200,6 +200,11 @@ struct DevParams {
   int64_t now;
   int32_t recompute;
   int32_t writeback;  // rows become followers / released in the store; out_expiry unused
+  // dm_publish_ring: a writeback tick also writes what dm_publish_totals would (record
+  // 1 + r = {SumWants, Count} as each resource's sums are stored, the validation flags
+  // OR-ed into record 0) and clears record 0 of the ring's next buffer; nullptr: off
+  double2* pub;
+  double2* pub_clear;
 };
 
 // dm_decide: one resource and its requests [qlo, qhi) in the caller's order; the

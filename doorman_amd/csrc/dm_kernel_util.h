@@ -321,6 +321,15 @@ __device__ __forceinline__ void write_resource(const DevParams& p, int seg, cons
   r.sum_has = c.sum_has + delta;  // the tick's Assigns: sumHas += gets - has (store.go:156)
   r.follow_exp = p.writeback ? rs.exp_out : rs.follow_exp;  // a writeback tick's leases follow exp_out
   p.res[seg] = r;
+  if (p.pub) {  // performRequests' band of the resource (server.go:234-255), as dm_publish_totals
+    double2 v;
+    v.x = r.sum_wants;
+    v.y = __longlong_as_double(r.count);
+    p.pub[1 + seg] = v;
+    if (r.sum_wants > 0.0 && (r.count < 1 || r.count > kSubMax))  // the root's validation (:863-866)
+      atomicOr((unsigned int*)p.pub, r.count < 1 ? kHierInvalid : kHierCountRange);
+    if (seg == 0) p.pub_clear[0] = double2{0.0, 0.0};  // the next tick's flags start clear
+  }
   if (p.writeback) {  // ... and none keeps an explicit expiry
     const int had = rs.xstate;
     const int want = dense_next ? dense_next + 1 : 0;

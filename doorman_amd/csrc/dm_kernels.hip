@@ -1647,9 +1647,10 @@ __global__ void k_gather_leases(int64_t n, const int64_t* __restrict__ rows, con
 __global__ __launch_bounds__(256) void k_publish(int64_t R, const ResAgg* __restrict__ agg, double2* __restrict__ dst,
                                                  uint32_t* sync, int nblocks) {
   __shared__ uint32_t wf[4];
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   uint32_t f = 0;
-  if (r < R) {
+  // a few workgroups striding over the records: each one arrives at the counter once
+  // (hundreds of contended arrivals cost ~10 us per launch at R = 100k)
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < R; r += (int64_t)nblocks * 256) {
     const ResAgg a = agg[r];
     double2 v;
     v.x = a.sum_wants;
@@ -2107,7 +2108,7 @@ hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t
 }
 
 hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, uint32_t* sync, hipStream_t st) {
-  const int nb = (int)std::max<int64_t>(1, (R + 255) / 256);
+  const int nb = (int)std::min<int64_t>(64, std::max<int64_t>(1, (R + 255) / 256));
   k_publish<<<(unsigned)nb, 256, 0, st>>>(R, agg, (double2*)dst, sync, nb);
   return hipGetLastError();
 }

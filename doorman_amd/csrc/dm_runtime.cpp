@@ -253,6 +253,9 @@ struct dm_ctx {
   // dm_publish_totals: the workgroups' validation flags and their arrival counter
   // (k_publish; both return to zero after each launch)
   DBuf<uint32_t> pub_sync;
+  // dm_publish_ring: writeback tick k publishes into pub_ring[k % n]
+  std::vector<double2*> pub_ring;
+  int64_t pub_k = 0;
   // root side of the hierarchy: the exchange's layout (dm_hier_layout) and the
   // last round's per-server flags
   int hier_G = 0;                    // 0: not configured (replicated, G from each call)
@@ -960,6 +963,12 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   }
   p.now = now_ns;
   p.recompute = (flags & DM_AGG_RECOMPUTE) ? 1 : 0;
+  if (wb && !c->pub_ring.empty()) {
+    const int64_t n = (int64_t)c->pub_ring.size();
+    p.pub = c->pub_ring[(size_t)(c->pub_k % n)];
+    p.pub_clear = c->pub_ring[(size_t)((c->pub_k + 1) % n)];
+    c->pub_k += 1;
+  }
 
   Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
@@ -1647,6 +1656,19 @@ int dm_publish_totals(dm_ctx* c, void* dst) {
   }
   DM_HIP(c, c->timed(KC_PUBLISH, c->stream, [&] { return launch_publish(c->R, c->agg.p, dst, c->pub_sync.p, c->stream); }),
          "publish");
+  return DM_OK;
+}
+
+int dm_publish_ring(dm_ctx* c, int n, void* const* bufs) {
+  DM_ENTER(c);
+  if (n < 0 || (n > 0 && !bufs)) return c->fail(DM_E_INVAL, "bad publish ring");
+  if (n > 0 && n < 3) return c->fail(DM_E_INVAL, "a publish ring needs at least 3 buffers");
+  for (int i = 0; i < n; ++i)
+    if (!bufs[i]) return c->fail(DM_E_INVAL, "null publish buffer");
+  c->pub_ring.clear();
+  for (int i = 0; i < n; ++i) c->pub_ring.push_back((double2*)bufs[i]);
+  c->pub_k = 0;
+  if (n > 0) DM_HIP(c, hipMemsetAsync(bufs[0], 0, sizeof(double2), c->stream), "publish ring");
   return DM_OK;
 }
 

@@ -21,6 +21,8 @@ doorman_amd so the HIP library binds to torch's HIP runtime.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import workloads as W
@@ -105,11 +107,17 @@ class HierarchicalTick:
             self.stride = 1 + int(np.diff(lo).max())
             _lib.check(L.dm_hier_layout(root._ctx, self.G, lo.ctypes.data, self.stride), root._ctx, L)
         dev = torch.device("cuda", torch.cuda.current_device())
-        nbuf = 2 if pipelined else 1  # a pipelined exchange may still read the previous step's blocks
+        # pipelined: the leaf's writeback ticks publish their blocks themselves
+        # (dm_publish_ring, a ring of three: an exchange may still read the block of
+        # the tick before the previous one); otherwise one block published before
+        # each exchange (dm_publish_totals)
+        nbuf = 3 if pipelined else 1
         self.totals = [torch.zeros((self.stride, 2), dtype=torch.float64, device=dev) for _ in range(nbuf)]
-        # one server: the all-gather is the identity, so the root reads the block in place
-        self.gathered = self.totals if self.G == 1 else [
-            torch.zeros((self.G * self.stride, 2), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        # one server: the all-gather is the identity, so the root reads the block in place.
+        # The exchange stream runs gather -> root round in order, so one gathered buffer
+        # serves every step.
+        g1 = torch.zeros((self.G * self.stride, 2), dtype=torch.float64, device=dev) if self.G > 1 else None
+        self.gathered = self.totals if self.G == 1 else [g1] * nbuf
         self.step = 0
         # The library's kernels and torch's collective share streams of their own:
         # torch's default stream is the HIP null stream, which dm_set_stream cannot
@@ -121,15 +129,19 @@ class HierarchicalTick:
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1 if pipelined else 0), leaf._ctx, leaf._L)
+        ring = (ctypes.c_void_p * nbuf)(*[t.data_ptr() for t in self.totals])
+        _lib.check(leaf._L.dm_publish_ring(leaf._ctx, nbuf if pipelined else 0, ring), leaf._ctx, leaf._L)
 
     def exchange(self, now_ns: int):
-        """publish -> all-gather -> the root's round -> this server's new templates."""
+        """publish -> all-gather -> the root's round -> this server's new templates
+        (pipelined: the block the last leaf tick published)."""
         from . import _lib
         k = self.step % len(self.totals)
         self.step += 1
         totals, gathered = self.totals[k], self.gathered[k]
-        self.leaf.publish_totals(totals.data_ptr())
-        if self.pipelined:
+        if not self.pipelined:
+            self.leaf.publish_totals(totals.data_ptr())
+        else:
             ev = self.torch.cuda.Event()
             ev.record(self.stream)
             self.xstream.wait_event(ev)
@@ -159,7 +171,8 @@ class HierarchicalTick:
                                                    f"(flags {st[bad].tolist()}: 1 = num_clients < 1, 2 = Count >= 2^31)")
 
     def tick(self, now_ns: int, asynchronous: bool = False):
-        if self.pipelined:  # the tick takes the templates staged one exchange ago; then this step's exchange
+        if self.pipelined:  # the tick (templates staged one exchange ago; it publishes its block), then
+            # this step's exchange of that block
             self.leaf.apportion(now_ns, writeback=True, asynchronous=True)
             self.exchange(now_ns)
             if not asynchronous:

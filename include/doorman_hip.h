@@ -236,6 +236,15 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
  * when a Count does not fit the root's 32-bit subclients column.  Stream-ordered. */
 int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
 
+/* The publish fused into the tick: with a ring of n >= 3 device buffers (each 1 + R
+ * records), the k-th writeback tick from this call on also writes what
+ * dm_publish_totals would into bufs[k % n] -- each resource's record as the tick stores
+ * its running sums, the validation flags OR-ed into record 0 -- and clears record 0 of
+ * bufs[(k + 1) % n] for the next tick.  Three buffers keep a tick's block intact while
+ * the pipelined exchange of the tick before (dm_hier_pipeline) still reads it.
+ * n = 0 turns it off. */
+int dm_publish_ring(dm_ctx* ctx, int n, void* const* dev_bufs);
+
 /* Layout of the exchange, set once on the root context (default: replicated, with
  * n_servers from each dm_hier_root_tick and stride 1 + R):
  *   shard_lo == NULL  replicated: every server holds all R resources of the root; the

@@ -525,3 +525,45 @@ def test_sharded_exchange_matches_the_reference_model(pipelined):
                 assert l.has <= rcfg["capacity"][r] * (1 + 1e-12), (t, g, r)
     for e in leaves + roots:
         e.close()
+
+
+def test_publish_ring_matches_publish_totals():
+    """dm_publish_ring: writeback tick k writes into ring buffer k % 3 exactly what
+    dm_publish_totals writes after it (records bit for bit, validation flags in record
+    0 -- here a band with Count 0 from the second tick on), every size bin and kind, and
+    clears the next buffer's flags; a non-writeback tick publishes nothing."""
+    import ctypes
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    from parity_util import binned_sizes, snapshot_with_sizes
+    torch.cuda.set_device(0)
+    L = _lib.lib()
+    rng = np.random.default_rng(61)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, per_bin=2), hetero=False)
+    R = len(snap["seg_off"]) - 1
+    ring = [torch.full((R + 1, 2), -1.0, dtype=torch.float64, device="cuda") for _ in range(3)]
+    ref = torch.zeros((R + 1, 2), dtype=torch.float64, device="cuda")
+    with Engine(0) as e:
+        e.load(snap)
+        ptrs = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ring])
+        _lib.check(L.dm_publish_ring(e._ctx, 3, ptrs), e._ctx)
+        for k in range(5):
+            if k == 1:  # a resource whose rows all carry 0 subclients: Count 0 with SumWants > 0
+                so = e.seg_off
+                r = int(np.flatnonzero(np.diff(so) > 3)[0])
+                rows = np.arange(so[r], so[r + 1])
+                e.upsert(rows, np.zeros(len(rows)), np.full(len(rows), 2.0), np.zeros(len(rows), np.int64),
+                         np.full(len(rows), NOW + 600 * W.NS))
+            e.apportion(NOW + k * W.NS, writeback=True)
+            e.publish_totals(ref.data_ptr())
+            e.sync()
+            got, want = ring[k % 3].cpu().numpy(), ref.cpu().numpy()
+            assert got.tobytes() == want.tobytes(), f"tick {k}"
+            assert (int(got[0, 0:1].view(np.int64)[0]) != 0) == (k >= 1), f"tick {k} flags"
+            assert ring[(k + 1) % 3].cpu().numpy()[0].tobytes() == np.zeros(2).tobytes()  # next flags cleared
+        before = [t.cpu().numpy().copy() for t in ring]
+        e.apportion(NOW + 9 * W.NS)  # no writeback: no publish
+        e.sync()
+        for t, b in zip(ring, before):
+            assert t.cpu().numpy().tobytes() == b.tobytes()

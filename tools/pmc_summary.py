@@ -17,7 +17,8 @@ import sys
 
 CLASS = [
     # template args <G, R[, BATCH]>: BATCH 2 is the HBM-streaming variant of the same bin
-    (r"k_block_dense<4>", "block128x4"), (r"k_block_dense<8>", "block128x8"),
+    (r"k_block_dense<4>", "block128x4_dense"), (r"k_block_dense<8>", "block128x8_dense"),
+    (r"k_publish\b", "hier_publish"), (r"k_hier_tick\b", "hier_root"),
     (r"k_block_rest<4>", "block128x4_rest"), (r"k_block_rest<8>", "block128x8_rest"),
     (r"k_block<128, 4(, \d)?>", "block128x4_mixed"), (r"k_block<128, 8(, \d)?>", "block128x8_mixed"), (r"k_block<256, 2(, \d)?>", "block256x2"), (r"k_block<256, 4(, \d)?>", "block256x4"),
     (r"k_block<256, 8(, \d)?>", "block256x8"), (r"k_block<512, 8(, \d)?>", "block512x8"), (r"k_block<512, 4(, \d)?>", "block512x4"), (r"k_block<1024, 4(, \d)?>", "block1024x4"),
