@@ -48,7 +48,7 @@ WORKLOADS = {
     "c3": "C3 (BASELINE configs[3], north-star size): 100,000 resources x 1,000 clients = 100M leases, FairShare",
     "c4": "C4 (BASELINE configs[4]) per GPU: 125M-lease device-resident store (1B over 8 GPUs), 125k resources x "
           "1k client slots, FS/PS mixed, 5% learning; every step = 5 s refresh tick: 10% wants updates and 1% "
-          "departures + 1% new clients over PCIe, then the tick",
+          "departures + 1% new clients (narrow 20-B arrival records) over PCIe, then the tick",
 }
 
 
@@ -171,9 +171,11 @@ def streaming_step(eng, snap, rank, n_ticks):
         now += 5 * W.NS
         k = len(new)
         # the wants refresh crosses PCIe as a row mask + packed values (1.25 B of mask
-        # per update at 10% instead of an 8-B row index: dm_store_update_wants_mask)
-        cols = (W.rows_to_mask(upd, N), rng.uniform(0.5, 1.5, len(upd)), gone, new, np.zeros(k),
-                rng.uniform(0.5, 1.5, k), np.ones(k, np.int64), np.full(k, now + 3600 * W.NS, np.int64))
+        # per update at 10% instead of an 8-B row index: dm_store_update_wants_mask);
+        # arrivals as narrow records: row, wants, int32 subclients (has 0 and the
+        # expiry now + lease length implied: the Assign of a new client, store.go:153-167)
+        cols = (W.rows_to_mask(upd, N), rng.uniform(0.5, 1.5, len(upd)), gone, new, rng.uniform(0.5, 1.5, k),
+                np.ones(k, np.int32))
         # the RPC layer would decode requests straight into page-locked buffers
         # (dm_host_alloc), which then cross PCIe by DMA
         pinned = []
@@ -185,8 +187,8 @@ def streaming_step(eng, snap, rank, n_ticks):
     it = iter(batches)
 
     def step():
-        mask, w, gone, new, nh, nw, ns, ne, t = next(it)
-        eng.apply(mask, w, gone, (new, nh, nw, ns, ne))  # the round's three update kinds, one call
+        mask, w, gone, new, nw, ns, t = next(it)
+        eng.apply(mask, w, gone, (new, None, nw, ns, None), now_ns=t)  # the round's three update kinds, one call
         eng.apportion(t, writeback=True, asynchronous=True)
 
     return step

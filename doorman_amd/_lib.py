@@ -48,7 +48,8 @@ class StoreBatch(ctypes.Structure):
         ("release_n", ctypes.c_int64), ("release_rows", ctypes.c_void_p),
         ("upsert_n", ctypes.c_int64), ("upsert_rows", ctypes.c_void_p), ("upsert_has", ctypes.c_void_p),
         ("upsert_wants", ctypes.c_void_p), ("upsert_subclients", ctypes.c_void_p),
-        ("upsert_expiry_ns", ctypes.c_void_p),
+        ("upsert_expiry_ns", ctypes.c_void_p), ("upsert_subclients32", ctypes.c_void_p),
+        ("upsert_now_ns", ctypes.c_int64),
     ]
 
 

@@ -1347,7 +1347,8 @@ __device__ __forceinline__ void wave_seg_add(ResAgg* agg, bool active, int seg, 
 // the value flags the planner needs.  The apply kernels run only if no error bit
 // is set, so a rejected call leaves the store untouched.
 __global__ void k_check_rows(int64_t n, const int64_t* __restrict__ rows, int64_t N, uint32_t* bitmap,
-                             const double* __restrict__ wants, const int64_t* __restrict__ sub, uint32_t* flags) {
+                             const double* __restrict__ wants, const int64_t* __restrict__ sub,
+                             const int32_t* __restrict__ sub32, uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t f = 0;
   if (i < n) {
@@ -1359,8 +1360,8 @@ __global__ void k_check_rows(int64_t n, const int64_t* __restrict__ rows, int64_
       if (atomicOr(&bitmap[r >> 5], bit) & bit) f |= kUpdDup;
     }
     if (wants && __builtin_isnan(wants[i])) f |= kUpdNaN;
-    if (sub) {
-      const int64_t v = sub[i];
+    if (sub || sub32) {
+      const int64_t v = sub32 ? (int64_t)sub32[i] : sub[i];
       if (v < 0 || v > kSubMax) f |= kUpdSub;
       if (v != 1) f |= kUpdNotOne;
     }
@@ -1382,9 +1383,13 @@ __global__ void k_clear_rows(int64_t n, const int64_t* __restrict__ rows, int64_
   if (r >= 0 && r < N) bitmap[r >> 5] = 0u;
 }
 
+// Narrow arrivals (dm_store_batch): has == nullptr -> 0; sub32 instead of sub;
+// expiry == nullptr -> the resource's now + lease length (the Assign's expiry,
+// store.go:161).
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
-                         const int64_t* __restrict__ expiry, RowIndex ix, double* s_has, double* s_wants,
+                         const int32_t* __restrict__ sub32, const int64_t* __restrict__ expiry,
+                         const ResCfg* __restrict__ cfg, int64_t now, RowIndex ix, double* s_has, double* s_wants,
                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (*flags & kUpdReject) return;  // uniform over the grid
@@ -1395,13 +1400,15 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
   if (active) {
     const int64_t r = rows[i];
     seg = seg_of_row(ix, r);
-    dh = has[i] - s_has[r];
+    const double hv = has ? has[i] : 0.0;
+    const int64_t sv = sub32 ? (int64_t)sub32[i] : sub[i];
+    dh = hv - s_has[r];
     dw = wants[i] - s_wants[r];
-    ds = sub[i] - sub_value(s_sub[r]);
-    s_has[r] = has[i];
+    ds = sv - sub_value(s_sub[r]);
+    s_has[r] = hv;
     s_wants[r] = wants[i];
-    s_sub[r] = (int32_t)((uint32_t)sub[i] | kSubExplicit);  // in [0, kSubMax] (k_check_rows); expiry explicit
-    s_exp[r] = expiry[i];
+    s_sub[r] = (int32_t)((uint32_t)sv | kSubExplicit);  // in [0, kSubMax] (k_check_rows); expiry explicit
+    s_exp[r] = expiry ? expiry[i] : now + (int64_t)cfg[seg].lease_len_s * kNs;
     expl[seg] = 1;  // the tick reads this resource's expiry column again
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
@@ -2055,12 +2062,12 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 }
 
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
-                         const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
-                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
-                         hipStream_t st) {
+                         const int32_t* sub32, const int64_t* expiry, const ResCfg* cfg, int64_t now,
+                         const RowIndex& ix, double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp,
+                         ResAgg* agg, uint8_t* expl, const uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, expiry, ix, s_has, s_wants, s_sub,
-                                                        s_exp, agg, expl, flags);
+  k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, sub32, expiry, cfg, now, ix, s_has,
+                                                        s_wants, s_sub, s_exp, agg, expl, flags);
   return hipGetLastError();
 }
 
@@ -2095,9 +2102,9 @@ hipError_t launch_gather_leases(int64_t n, const int64_t* rows, const double* ge
 }
 
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
-                             const int64_t* sub, uint32_t* flags, hipStream_t st) {
+                             const int64_t* sub, const int32_t* sub32, uint32_t* flags, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_check_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, N, bitmap, wants, sub, flags);
+  k_check_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, N, bitmap, wants, sub, sub32, flags);
   return hipGetLastError();
 }
 

@@ -33,14 +33,14 @@ hipError_t launch_large_fused(int G, const DevParams& p, const Chunk* chunks, co
                               int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t large_fused_occupancy(int G, int* blocks_per_cu);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
-                         const int64_t* expiry, const RowIndex& ix, double* s_has, double* s_wants,
-                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
-                         hipStream_t st);
+                         const int32_t* sub32, const int64_t* expiry, const ResCfg* cfg, int64_t now,
+                         const RowIndex& ix, double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp,
+                         ResAgg* agg, uint8_t* expl, const uint32_t* flags, hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
                           int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
                           hipStream_t st);
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
-                             const int64_t* sub, uint32_t* flags, hipStream_t st);
+                             const int64_t* sub, const int32_t* sub32, uint32_t* flags, hipStream_t st);
 hipError_t launch_clear_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, hipStream_t st);
 hipError_t launch_resolve_rows(int64_t n, const int64_t* rows, int64_t off, const int32_t* sub, const int64_t* expiry,
                                const RowIndex& ix, const ResAgg* agg, int64_t* out_exp, int64_t* out_sub,
@@ -656,10 +656,35 @@ int dm_create(int device, dm_ctx** out) {
   const bool cumask = !getenv("DM_CUMASK") || atoi(getenv("DM_CUMASK")) != 0;
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-  std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0u);
-  for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
+  const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
+  std::vector<std::vector<uint32_t>> masks(dm_ctx::kAux, std::vector<uint32_t>(mwords, 0u));
+  for (int i = 0; i < dm_ctx::kAux; ++i)
+    for (int b = 0; b < ncu; ++b) masks[i][(size_t)(b / 32)] |= 1u << (b % 32);
+  // A/B probe: DM_CU_PART="n0,n1,n2,n3" gives auxiliary stream i its own n_i CUs
+  // (interleaved over the CU index, so every stream spans every XCD) instead of all
+  if (const char* part = getenv("DM_CU_PART")) {
+    int want[dm_ctx::kAux] = {0, 0, 0, 0}, got[dm_ctx::kAux] = {0, 0, 0, 0}, total = 0;
+    sscanf(part, "%d,%d,%d,%d", &want[0], &want[1], &want[2], &want[3]);
+    for (int i = 0; i < dm_ctx::kAux; ++i) total += want[i];
+    if (total > 0 && total <= ncu) {
+      for (auto& m : masks) std::fill(m.begin(), m.end(), 0u);
+      for (int b = 0; b < total; ++b) {  // the stream furthest below its share takes the next CU
+        int best = 0;
+        double gap = -1e9;
+        for (int i = 0; i < dm_ctx::kAux; ++i) {
+          const double g = (double)want[i] * (b + 1) / total - got[i];
+          if (want[i] > got[i] && g > gap) {
+            gap = g;
+            best = i;
+          }
+        }
+        masks[best][(size_t)(b / 32)] |= 1u << (b % 32);
+        ++got[best];
+      }
+    }
+  }
   for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
-    e = cumask && ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mask.size(), mask.data())
+    e = cumask && ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, masks[i].data())
                           : hipErrorNotSupported;
     if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
       (void)hipGetLastError();
@@ -1361,7 +1386,7 @@ static int staged_check(dm_ctx* c, int64_t n, const StageCol* cols, int ncols, b
     DM_HIP(c, hipEventRecord(ev, cp), "stage update");
     DM_HIP(c, hipStreamWaitEvent(c->stream, ev, 0), "stage update");
     DM_HIP(c, launch_check_rows(m, c->st_rows.p + off, c->N, c->row_bits.p, check_wants ? c->st_wants.p + off : nullptr,
-                                check_sub ? c->st_sub.p + off : nullptr, c->upd_flags.p, c->stream),
+                                check_sub ? c->st_sub.p + off : nullptr, nullptr, c->upd_flags.p, c->stream),
            "check rows");
   }
   return DM_OK;
@@ -1398,9 +1423,9 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
                            {c->st_has.p, has, 8}, {c->st_exp.p, exp, 8}};
   int rc = staged_check(c, n, cols, 5, true, true);
   if (rc) return rc;
-  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->row_index(),
-                          c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, c->upd_flags.p,
-                          c->stream),
+  DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, nullptr, c->st_exp.p, c->cfg.p, 0,
+                          c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p,
+                          c->upd_flags.p, c->stream),
          "upsert");
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
@@ -1516,9 +1541,12 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     if (fr + 64 * (nw - 1) >= c->N) return c->fail(DM_E_RANGE, "mask words past the store's end");
   }
   if (nr > 0 && !b->release_rows) return c->fail(DM_E_INVAL, "bad release");
-  if (nu > 0 && (!b->upsert_rows || !b->upsert_has || !b->upsert_wants || !b->upsert_subclients ||
-                 !b->upsert_expiry_ns))
+  // narrow arrivals: subclients as int32, has NULL (= 0), expiry NULL (= now + lease length)
+  const bool sub32 = b->upsert_subclients32 != nullptr;
+  if (nu > 0 && (!b->upsert_rows || !b->upsert_wants || (!b->upsert_subclients && !sub32)))
     return c->fail(DM_E_INVAL, "bad upsert");
+  if (nu > 0 && !b->upsert_expiry_ns && !c->cfg_loaded)
+    return c->fail(DM_E_STATE, "arrivals without expiries take the resource's lease length: load a configuration");
   if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
   hipStream_t st = c->stream, cp = c->cpy;
   if (!c->bat_flags.p) {
@@ -1553,11 +1581,14 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     DM_HIP(c, c->st_wants.ensure((size_t)nu), "stage wants");
     DM_HIP(c, c->st_sub.ensure((size_t)nu), "stage sub");
     DM_HIP(c, c->st_exp.ensure((size_t)nu), "stage expiry");
-    const StageCol cols[] = {{c->st_rows.p, b->upsert_rows, 8}, {c->st_wants.p, b->upsert_wants, 8},
-                             {c->st_sub.p, b->upsert_subclients, 8}, {c->st_has.p, b->upsert_has, 8},
+    const StageCol cols[] = {{c->st_rows.p, b->upsert_rows, 8},
+                             {c->st_wants.p, b->upsert_wants, 8},
+                             {c->st_sub.p, sub32 ? (const void*)b->upsert_subclients32 : b->upsert_subclients, sub32 ? 4u : 8u},
+                             {c->st_has.p, b->upsert_has, 8},
                              {c->st_exp.p, b->upsert_expiry_ns, 8}};
     for (const auto& col : cols)
-      DM_HIP(c, hipMemcpyAsync(col.dst, col.src, (size_t)nu * col.elem, hipMemcpyHostToDevice, cp), "stage upsert");
+      if (col.src)
+        DM_HIP(c, hipMemcpyAsync(col.dst, col.src, (size_t)nu * col.elem, hipMemcpyHostToDevice, cp), "stage upsert");
     DM_HIP(c, hipEventRecord(c->ev_bat[2], cp), "stage");
   }
   // part 1: wants refresh (validated by its count/scan passes before the apply)
@@ -1570,7 +1601,8 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   // part 2: departures
   if (nr > 0) {
     DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[1], 0), "stage");
-    DM_HIP(c, launch_check_rows(nr, c->st_rel.p, c->N, c->row_bits.p, nullptr, nullptr, F + 1, st), "check rows");
+    DM_HIP(c, launch_check_rows(nr, c->st_rel.p, c->N, c->row_bits.p, nullptr, nullptr, nullptr, F + 1, st),
+           "check rows");
     DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
     DM_HIP(c, launch_release(nr, c->st_rel.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
                              c->expl.p, F + 1, st),
@@ -1582,10 +1614,13 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   // part 3: arrivals / full refreshes
   if (nu > 0) {
     DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[2], 0), "stage");
-    DM_HIP(c, launch_check_rows(nu, c->st_rows.p, c->N, c->row_bits.p, c->st_wants.p, c->st_sub.p, F + 2, st),
+    const int64_t* s64 = sub32 ? nullptr : c->st_sub.p;
+    const int32_t* s32 = sub32 ? (const int32_t*)c->st_sub.p : nullptr;
+    DM_HIP(c, launch_check_rows(nu, c->st_rows.p, c->N, c->row_bits.p, c->st_wants.p, s64, s32, F + 2, st),
            "check rows");
     DM_HIP(c, launch_carry_reject(F + 1, F + 2, st), "carry");
-    DM_HIP(c, launch_upsert(nu, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, c->st_exp.p, c->row_index(),
+    DM_HIP(c, launch_upsert(nu, c->st_rows.p, b->upsert_has ? c->st_has.p : nullptr, c->st_wants.p, s64, s32,
+                            b->upsert_expiry_ns ? c->st_exp.p : nullptr, c->cfg.p, b->upsert_now_ns, c->row_index(),
                             c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, F + 2, st),
            "upsert");
     DM_HIP(c, launch_clear_rows(nu, c->st_rows.p, c->N, c->row_bits.p, st), "clear rows");

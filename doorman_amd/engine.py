@@ -154,9 +154,12 @@ class Engine:
         self._chk(self._L.dm_store_update_wants_mask(self._ctx, int(first_row), len(mask), _ptr(mask), len(wants),
                                                      _ptr(wants)))
 
-    def apply(self, wants_mask=None, wants=None, release_rows=None, upsert=None, wants_first_row: int = 0):
+    def apply(self, wants_mask=None, wants=None, release_rows=None, upsert=None, wants_first_row: int = 0,
+              now_ns: int = 0):
         """dm_store_apply: one round's refresh (row mask + packed wants), departures and
-        arrivals (upsert = (rows, has, wants, subclients, expiry_ns)) in one call."""
+        arrivals (upsert = (rows, has, wants, subclients, expiry_ns)) in one call.
+        Narrow arrivals: has None (= 0), subclients as int32 (sent as 4 B), expiry_ns None
+        (= now_ns + the resource's lease length)."""
         keep = []
 
         def col(a, dt):
@@ -176,8 +179,14 @@ class Engine:
             rows, has, wv, sub, exp = upsert
             rows = col(rows, np.int64)
             b.upsert_n, b.upsert_rows = len(rows), _ptr(rows)
-            b.upsert_has, b.upsert_wants = _ptr(col(has, np.float64)), _ptr(col(wv, np.float64))
-            b.upsert_subclients, b.upsert_expiry_ns = _ptr(col(sub, np.int64)), _ptr(col(exp, np.int64))
+            b.upsert_has = None if has is None else _ptr(col(has, np.float64))
+            b.upsert_wants = _ptr(col(wv, np.float64))
+            if np.asarray(sub).dtype == np.int32:
+                b.upsert_subclients32 = _ptr(col(sub, np.int32))
+            else:
+                b.upsert_subclients = _ptr(col(sub, np.int64))
+            b.upsert_expiry_ns = None if exp is None else _ptr(col(exp, np.int64))
+            b.upsert_now_ns = int(now_ns)
         self._chk(self._L.dm_store_apply(self._ctx, ctypes.byref(b)))
 
     def release(self, rows):

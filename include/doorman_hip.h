@@ -120,10 +120,15 @@ typedef struct {
   /* arrivals and full refreshes (dm_store_upsert) */
   int64_t upsert_n;
   const int64_t* upsert_rows;
-  const double* upsert_has;
+  const double* upsert_has;          /* NULL: 0 for every row (a new client holds nothing yet) */
   const double* upsert_wants;
-  const int64_t* upsert_subclients;
-  const int64_t* upsert_expiry_ns;
+  const int64_t* upsert_subclients;  /* or NULL with upsert_subclients32 */
+  const int64_t* upsert_expiry_ns;   /* NULL: each row's resource's upsert_now_ns + lease length (the
+                                        expiry Assign gives, store.go:161) */
+  /* narrow arrivals: 4-B subclients instead of upsert_subclients (C4's arrivals: 20 B per
+     row over PCIe with has and expiry NULL, instead of 40) */
+  const int32_t* upsert_subclients32;
+  int64_t upsert_now_ns;
 } dm_store_batch;
 
 typedef struct {

@@ -914,15 +914,17 @@ def _writeback_host(host, ref):
     host["expiry_ns"] = ref["expiry_ns"].copy()
 
 
-@pytest.mark.parametrize("cols", ["inplace", "alternate"])
-def test_c4_loop_store_apply_matches_oracle(eng, cols):
+@pytest.mark.parametrize("cols,narrow", [("inplace", False), ("alternate", False), ("inplace", True)])
+def test_c4_loop_store_apply_matches_oracle(eng, cols, narrow):
     """configs[4]'s own loop under the oracle.  Every 5-s round the bench's
     update call -- dm_store_apply with the wants refresh as a row mask, departures and
     arrivals -- then a writeback tick; 5% learning resources, leases that lapse
     between rounds (4-s lease resources, loaded rows whose explicit expiry passes).
     A host copy takes the same updates and each tick's writeback; the oracle decides
     every round (store.go:142-181, resource.go:108-111) from exact sums while the
-    device uses its running sums."""
+    device uses its running sums.  narrow: the arrivals as bench.py sends them -- row,
+    wants, int32 subclients, has and expiry implied (0 and now + the resource's lease
+    length, the Assign of a new client)."""
     rng = np.random.default_rng(404)
     snap = _c4_store(rng, 2000, 300)
     eng.load(snap)
@@ -932,7 +934,12 @@ def test_c4_loop_store_apply_matches_oracle(eng, cols):
     for rnd in range(6):
         now += 5 * W.NS
         mask, w, gone, new, nh, nw, ns, ne, upd = _c4_round(rng, host, now)
-        eng.apply(mask, w, gone, (new, nh, nw, ns, ne))
+        if narrow:
+            so = snap["seg_off"]
+            ne = now + snap["lease_length_s"][np.searchsorted(so, new, side="right") - 1] * W.NS
+            eng.apply(mask, w, gone, (new, None, nw, ns.astype(np.int32), None), now_ns=now)
+        else:
+            eng.apply(mask, w, gone, (new, nh, nw, ns, ne))
         _apply_host(host, upd, w, gone, new, nh, nw, ns, ne)
         res = eng.resources(safe=False)
         np.testing.assert_array_equal(res["count"], host["agg_count"])  # the running Count, exact
