@@ -106,8 +106,29 @@ struct Partials {
   // chunk, pass B totals left by pass C's first chunk, so the map reduces at most
   // one set of partials
   uint8_t* tot;
+  // heterogeneous-subclient FairShare on the chain (only when the store may hold
+  // such resources; nullptr otherwise -- they then go to the one-workgroup k_general):
+  // per chunk the distinct subclient counts of its live rows (pass A; s_cnt 0: the
+  // chunk's rows share one count, its a_smin; -1: more than kHetMaxS), per large
+  // resource a HetRes record, per chunk the round-2 bucket partials (pass C)
+  int32_t* s_list;  // [nchunks * kHetMaxS]
+  int32_t* s_cnt;   // [nchunks]
+  uint8_t* het;     // [large resources * sizeof(HetRes)]
+  double* bk_w;     // [nchunks * kHetBuckets]
+  int64_t* bk_s;
+  int32_t* bk_c;
 };
 constexpr int kSegTotBytes = 128;
+constexpr int kHetMaxS = 256;                    // distinct subclient counts per resource on the chain
+constexpr int kHetBuckets = 2 * kHetMaxS + 1;    // strictly between / equal to the sorted thresholds
+struct HetRes {
+  int32_t mode;  // 0: not heterogeneous FairShare; 1: decided on the chain; 2: handed to k_general
+  int32_t K;     // distinct thresholds
+  double T[kHetMaxS];       // ascending
+  double bw[kHetBuckets];   // per bucket over the resource's chunks (k_large_e): sum of wants,
+  int64_t bs[kHetBuckets];  // sum of subclients,
+  int64_t bc[kHetBuckets];  // count of the wantExtra clients
+};
 
 // One-launch large path (k_large_fused, dm_large.hip): every chunk keeps its rows
 // in VGPRs while the resource's chunks exchange per-resource totals in-launch.

@@ -699,6 +699,57 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
   }
 }
 
+__device__ __forceinline__ HetRes* het_of(const Partials& P, int lseg) {
+  return reinterpret_cast<HetRes*>(P.het + (size_t)lseg * sizeof(HetRes));
+}
+constexpr uint32_t kHetEmpty = 0xFFFFFFFFu;  // never a subclient count (<= kSubMax)
+
+__device__ __forceinline__ bool het_insert(uint32_t* set, int* n, uint32_t key) {  // true when new
+  uint32_t slot = (key * 0x9E3779B1u >> 23) & (2 * kHetMaxS - 1);
+  for (int probe = 0; probe < 2 * kHetMaxS; ++probe, slot = (slot + 1) & (2 * kHetMaxS - 1)) {
+    uint32_t cur = set[slot];
+    if (cur == key) return false;
+    if (cur == kHetEmpty) {
+      cur = atomicCAS(&set[slot], kHetEmpty, key);
+      if (cur == kHetEmpty) {
+        atomicAdd(n, 1);
+        return true;
+      }
+      if (cur == key) return false;
+    }
+  }
+  atomicAdd(n, kHetMaxS + 1);  // table full: overflow
+  return false;
+}
+
+// pass A's list for one chunk (k_large_a, when P.s_cnt): the distinct counts of its
+// live rows when they differ (a chunk whose live rows share one count is a_smin)
+__device__ void chunk_s_list(const Partials& P, int c, const ChunkRows& rw, const AggA& a) {
+  __shared__ uint32_t set[2 * kHetMaxS];
+  __shared__ int n;
+  const int t = threadIdx.x;
+  if (!(a.smin < a.smax)) {
+    if (t == 0) P.s_cnt[c] = 0;
+    return;
+  }
+  for (int i = t; i < 2 * kHetMaxS; i += 256) set[i] = kHetEmpty;
+  if (t == 0) n = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kLR; ++k)
+    if (rw.live >> k & 1) het_insert(set, &n, (uint32_t)rw.s[k]);
+  __syncthreads();
+  const int cnt = n;
+  if (cnt <= kHetMaxS) {
+    __shared__ int fill;
+    if (t == 0) fill = 0;
+    __syncthreads();
+    for (int i = t; i < 2 * kHetMaxS; i += 256)
+      if (set[i] != kHetEmpty) P.s_list[(size_t)c * kHetMaxS + atomicAdd(&fill, 1)] = (int32_t)set[i];
+  }
+  if (t == 0) P.s_cnt[c] = cnt <= kHetMaxS ? cnt : -1;
+}
+
 __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
@@ -762,6 +813,7 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
     if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
     if (spec) b = group_reduce<256>(b, OpB(), lds.b);
   }
+  if (P.s_cnt && !rs.learning && rs.kind == 3) chunk_s_list(P, blockIdx.x, rw, a);  // heterogeneous FairShare
   if (threadIdx.x == 0) {
     const int c = blockIdx.x;
     if (spec) {
@@ -794,12 +846,13 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
   const LargeSeg L = ls[ch.lseg];
   const SegState st = seg_state<256>(p, P, L, lds);
   if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->a = st.a;
-  if (st.general || st.rs.learning || st.rs.kind < 2) return;
+  const bool het = st.general && P.s_cnt;  // heterogeneous FairShare decided on the chain
+  if ((st.general && !het) || st.rs.learning || st.rs.kind < 2) return;
   if (!p.recompute && st.a.cnt == 0) return;  // pass A's speculative partials are exact
   ChunkRows rw;
-  load_chunk_w(p, P, ch, rw, ps);
+  load_chunk_w(p, P, ch, rw, ps || het);
   const double eq = st.rs.C / (double)st.cl.count;
-  if (!ps) {  // FairShare reaches here only with uniform subclients
+  if (!ps && !het) {  // uniform FairShare: one count
 #pragma unroll
     for (int k = 0; k < kLR; ++k) rw.s[k] = st.a.smin;
   }
@@ -938,8 +991,11 @@ __global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* 
   const LargeSeg L = ls[blockIdx.x];
   const SegState st = seg_state<256>(p, P, L, lds);
   if (st.general) {
-    if (threadIdx.x == 0) general_list[atomicAdd(general_count, 1)] = L.seg;
-    return;
+    if (!P.s_cnt) {  // no heterogeneous path on the chain this tick: k_general decides it
+      if (threadIdx.x == 0) general_list[atomicAdd(general_count, 1)] = L.seg;
+      return;
+    }
+    if (het_of(P, blockIdx.x)->mode != 1) return;  // k_large_t handed it to k_general
   }
   SumD d{0.0};
   for (int c = L.chunk_begin + (int)threadIdx.x; c < L.chunk_end; c += 256) d.v += P.d_delta[c];
@@ -1281,6 +1337,288 @@ __global__ __launch_bounds__(256) void k_general(DevParams p, const int32_t* __r
     if (t == 0) write_resource(p, seg, rs, cl, delta.v);
     __syncthreads();  // the next resource reuses the LDS
   }
+}
+
+
+// --------------------------------------------------------------------------
+// Heterogeneous-subclient FairShare of large resources on the chain (instead of
+// one workgroup per resource in k_general): launched only when the store may hold
+// such resources.  After pass B (round 1 with each row's own count):
+//   k_large_t      per resource: round-1 totals, the distinct subclient counts of
+//                  the live rows (from pass A's per-chunk lists) and their round-2
+//                  thresholds T(s) = (E / W) s + eq s -- a row reaching round 2 has
+//                  w > deservedShare, so its wantExtra is W and its threshold
+//                  depends on its count only (algorithm.go:148,175,197) -- sorted;
+//   k_large_c_het  per chunk: (count, sum wants, sum subclients) of the wantExtra
+//                  clients per bucket between / at the thresholds (as k_general);
+//   k_large_e      per resource: the chunks' buckets in chunk order, prefix sums:
+//                  extraExtra(T) = k T - sum(w < T), wantExtraExtra(T) = sum(s : w > T);
+//   k_large_map_het per chunk: every row decided (fs_stage01 / fs_stage2).
+// More than kHetMaxS counts or a non-finite threshold: k_general (HetRes.mode 2).
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_large_t(DevParams p, const LargeSeg* __restrict__ ls, Partials P,
+                                                 int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<256> lds;
+  __shared__ uint32_t set[2 * kHetMaxS];
+  __shared__ double T[kHetMaxS];
+  __shared__ int n, fill;
+  const int t = threadIdx.x;
+  const LargeSeg L = ls[blockIdx.x];
+  SegTot* tot = seg_tot(P, blockIdx.x);
+  HetRes* H = het_of(P, blockIdx.x);
+  const SegState st = seg_state_of(p, L.seg, tot->a);  // left by pass B's first chunk
+  if (!st.general) {
+    if (t == 0) H->mode = 0;
+    return;
+  }
+  const AggB b = seg_b<256>(P, L, lds);  // round 1 with every row's own count: E = b.x, W = b.i
+  if (t == 0) tot->b = b;
+  for (int i = t; i < 2 * kHetMaxS; i += 256) set[i] = kHetEmpty;
+  if (t == 0) {
+    n = 0;
+    fill = 0;
+  }
+  __syncthreads();
+  {  // every chunk's list slot, flattened: 16 independent loads in flight per thread
+    const int nch = L.chunk_end - L.chunk_begin;
+    const int total = nch * kHetMaxS;
+    for (int base = 0; base < total; base += 256 * 16) {
+      int32_t m[16], v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int idx = base + j * 256 + t;
+        const int c = L.chunk_begin + (idx < total ? idx / kHetMaxS : 0);
+        m[j] = idx < total ? P.s_cnt[c] : -2;
+        v[j] = idx < total ? P.s_list[(size_t)L.chunk_begin * kHetMaxS + idx] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int idx = base + j * 256 + t;
+        const int i = idx % kHetMaxS, c = L.chunk_begin + idx / kHetMaxS;
+        if (m[j] == -1) {
+          if (i == 0) atomicAdd(&n, kHetMaxS + 1);  // a chunk beyond the bound
+        } else if (m[j] == 0) {
+          if (i == 0 && P.a_smin[c] <= P.a_smax[c]) het_insert(set, &n, (uint32_t)P.a_smin[c]);  // one count
+        } else if (m[j] > 0 && i < m[j]) {
+          het_insert(set, &n, (uint32_t)v[j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int K0 = n;
+  bool bad = K0 > kHetMaxS;
+  if (!bad) {
+    for (int i = t; i < 2 * kHetMaxS; i += 256)
+      if (set[i] != kHetEmpty) {
+        const double s = (double)set[i];
+        const double eq = st.rs.C / (double)st.cl.count;  // as fs_stage01's arguments
+        const double ds = eq * s;                          // :126
+        const double dE = (b.x / (double)b.i) * s;         // :175 (wantExtra = W for a round-2 row)
+        T[atomicAdd(&fill, 1)] = dE + ds;                  // :197
+      }
+    __syncthreads();
+    if (t >= K0) T[t] = __builtin_inf();
+    int nonfinite = 0;
+    if (t < K0 && !__builtin_isfinite(T[t])) nonfinite = 1;
+    bad = __syncthreads_or(nonfinite) != 0;
+  }
+  if (bad) {  // k_general decides the resource (per-threshold passes)
+    if (t == 0) {
+      H->mode = 2;
+      general_list[atomicAdd(general_count, 1)] = L.seg;
+    }
+    return;
+  }
+  for (int k = 2; k <= kHetMaxS; k <<= 1)  // ascending bitonic sort of the thresholds
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      __syncthreads();
+      const int q = t ^ j;
+      if (q > t) {
+        const double x = T[t], y = T[q];
+        if ((x > y) == ((t & k) == 0)) {
+          T[t] = y;
+          T[q] = x;
+        }
+      }
+    }
+  __syncthreads();
+  if (t == 0) {  // distinct values only (counts may share a threshold)
+    int K = 0;
+    for (int i = 0; i < K0; ++i)
+      if (K == 0 || T[i] != H->T[K - 1]) H->T[K++] = T[i];
+    H->K = K;
+    H->mode = 1;
+  }
+}
+
+// One 64-row tile of a wave into its bucket accumulators (k_general's method:
+// sort the lanes by bucket, segmented scan, one writer per bucket; fixed order).
+__device__ __forceinline__ void het_tile(const double* T, int K, double w, long long s, bool in, double* accw,
+                                         long long* accs, int* accc) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t bk = in ? (uint32_t)gen_bucket(T, K, w) : 0xFFFFu;
+  const uint32_t key = wave_sort64(bk << 6 | (uint32_t)lane);
+  const int src = (int)(key & 63);
+  const int mb = (int)(key >> 6);
+  double vw = shfl_d(in ? w : 0.0, src);
+  long long vs = __shfl(in ? s : 0ll, src, 64);
+  int vc = mb != 0xFFFF ? 1 : 0;
+  const int prevb = __shfl_up(mb, 1, 64);
+  int run = (lane == 0 || prevb != mb) ? 1 : 0;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double ow = shfl_d(vw, lane >= off ? lane - off : lane);
+    const long long os = __shfl(vs, lane >= off ? lane - off : lane, 64);
+    const int oc = __shfl(vc, lane >= off ? lane - off : lane, 64);
+    const int orun = __shfl(run, lane >= off ? lane - off : lane, 64);
+    if (lane >= off && !run) {
+      vw = ow + vw;
+      vs = os + vs;
+      vc = oc + vc;
+      run = orun;
+    }
+  }
+  const int nextb = __shfl_down(mb, 1, 64);
+  if (mb != 0xFFFF && (lane == 63 || nextb != mb)) {
+    accw[mb] += vw;
+    accs[mb] += vs;
+    accc[mb] += vc;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_large_c_het(DevParams p, const Chunk* __restrict__ chunks,
+                                                     const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ double T[kHetMaxS];
+  __shared__ double accw[4][kHetBuckets];
+  __shared__ long long accs[4][kHetBuckets];
+  __shared__ int accc[4][kHetBuckets];
+  const int t = threadIdx.x, wv = t >> 6;
+  const Chunk ch = chunks[blockIdx.x];
+  const HetRes* H = het_of(P, ch.lseg);
+  if (H->mode != 1) return;
+  ChunkRows rw;
+  load_chunk_w(p, P, ch, rw, true);
+  const SegState st = seg_state_of(p, ch.seg, seg_tot(P, ch.lseg)->a);
+  const double eq = st.rs.C / (double)st.cl.count;
+  const int K = H->K;
+  for (int i = t; i < K; i += 256) T[i] = H->T[i];
+  for (int i = t; i < 4 * kHetBuckets; i += 256) {
+    (&accw[0][0])[i] = 0.0;
+    (&accs[0][0])[i] = 0;
+    (&accc[0][0])[i] = 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {  // row k*256 + t: tile 4k + wv, in order per wave
+    const double w = rw.w[k];
+    const long long s = rw.s[k];
+    const bool in = (rw.live >> k & 1) && w > (double)s * eq;  // wantExtraClients (:165-169)
+    het_tile(T, K, w, s, in, accw[wv], accs[wv], accc[wv]);
+  }
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * kHetBuckets;
+  for (int bb = t; bb < 2 * K + 1; bb += 256) {  // the waves combined in a fixed order
+    P.bk_w[base + bb] = ((accw[0][bb] + accw[1][bb]) + accw[2][bb]) + accw[3][bb];
+    P.bk_s[base + bb] = accs[0][bb] + accs[1][bb] + accs[2][bb] + accs[3][bb];
+    P.bk_c[base + bb] = accc[0][bb] + accc[1][bb] + accc[2][bb] + accc[3][bb];
+  }
+}
+
+// one wave per (resource, bucket): the bucket's chunk partials, lanes striding the
+// chunks, combined by the fixed DPP tree of wave_reduce
+__global__ __launch_bounds__(256) void k_large_e(DevParams p, const LargeSeg* __restrict__ ls, Partials P) {
+  const int lane = threadIdx.x & 63;
+  const LargeSeg L = ls[blockIdx.x];
+  HetRes* H = het_of(P, blockIdx.x);
+  if (H->mode != 1) return;
+  const int bb = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (bb >= 2 * H->K + 1) return;  // whole waves
+  AggR v{0, 0.0, 0.0};  // cnt: clients, h: subclients (exact below 2^53), w: wants
+  for (int q = L.chunk_begin + lane; q < L.chunk_end; q += 64) {
+    const size_t i = (size_t)q * kHetBuckets + bb;
+    v.w += P.bk_w[i];
+    v.h += (double)P.bk_s[i];
+    v.cnt += P.bk_c[i];
+  }
+  v = wave_reduce(v, OpR());
+  if (lane == 0) {
+    H->bw[bb] = v.w;
+    H->bs[bb] = (int64_t)v.h;
+    H->bc[bb] = v.cnt;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_large_map_het(DevParams p, const Chunk* __restrict__ chunks,
+                                                       const LargeSeg* __restrict__ ls, Partials P) {
+  __shared__ Lds<256> lds;
+  __shared__ double T[kHetMaxS], ee[kHetMaxS];
+  __shared__ long long sgt[kHetMaxS];
+  const int t = threadIdx.x;
+  const Chunk ch = chunks[blockIdx.x];
+  const HetRes* H = het_of(P, ch.lseg);
+  if (H->mode != 1) return;
+  ChunkRows rw;
+  load_chunk_w(p, P, ch, rw, true, true);
+  const SegTot* tot = seg_tot(P, ch.lseg);
+  const SegState st = seg_state_of(p, ch.seg, tot->a);
+  const AggB b = tot->b;
+  const double C = st.rs.C;
+  const double eq = C / (double)st.cl.count;
+  const int K = H->K;
+  __shared__ double bw[kHetBuckets];
+  __shared__ long long bs[kHetBuckets], bc[kHetBuckets];
+  for (int i = t; i < K; i += 256) T[i] = H->T[i];
+  for (int i = t; i < 2 * K + 1; i += 256) {
+    bw[i] = H->bw[i];
+    bs[i] = H->bs[i];
+    bc[i] = H->bc[i];
+  }
+  __syncthreads();
+  if (t == 0) {  // prefix over the buckets (as k_general): every chunk the same, in LDS
+    long long stot = 0;
+    for (int bb = 0; bb < 2 * K + 1; ++bb) stot += bs[bb];
+    long long cnt = 0, sle = 0;
+    double sw = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const int bl = 2 * k;  // below T_k; bl + 1: w == T_k
+      cnt += bc[bl];
+      sw = sw + bw[bl];
+      sle += bs[bl];
+      const long long seq = bs[bl + 1];
+      ee[k] = cnt == 0 ? 0.0 : (double)cnt * T[k] - sw;  // :197-198
+      sgt[k] = stot - sle - seq;                          // :199-200
+      sle += seq;
+      cnt += bc[bl + 1];
+      sw = sw + bw[bl + 1];
+    }
+  }
+  __syncthreads();
+  SumD delta{0.0};
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.valid >> k & 1)) continue;
+    const unsigned u = (unsigned)(k * 256 + t);
+    const double w = rw.w[k], h = rw.h[k];
+    if (!(rw.live >> k & 1)) {
+      put_released(p, ch.row0, u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
+      continue;
+    }
+    const long long s = rw.s[k];
+    double g, Tr = 0.0;
+    if (!fs_stage01(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, &g, &Tr)) {
+      AggC c{0.0, 0};
+      if (!__builtin_isnan(Tr)) {
+        const int q = gen_index(T, K, Tr);
+        c = AggC{ee[q], sgt[q]};
+      }
+      g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, Tr, c);
+    }
+    put_live(p, ch.row0, u, g, st.rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
+    delta.v += g - h;
+  }
+  delta = group_reduce<256>(delta, OpSumD(), lds.d);
+  if (t == 0) P.d_delta[blockIdx.x] = delta.v;
 }
 
 // --------------------------------------------------------------------------
@@ -2044,6 +2382,10 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st) {
   if (nchunks <= 0) return hipSuccess;
   switch (phase) {
+    case 5: k_large_t<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;
+    case 6: k_large_c_het<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 7: k_large_e<<<dim3(nls, (kHetBuckets + 3) / 4), 256, 0, st>>>(p, ls, P); break;
+    case 8: k_large_map_het<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
     case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;

@@ -85,6 +85,7 @@ enum KClass {
   KC_REST4,
   KC_PUBLISH,   // dm_publish_totals
   KC_HIER_ROOT, // dm_hier_root_tick
+  KC_LARGE_HET, // heterogeneous FairShare on the chain
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
@@ -93,7 +94,7 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release", "large_fused", "subs_merged", "block128x4_dense",
                                      "block128x8_dense", "block128x4_rest", "block128x8_rest", "hier_publish",
-                                     "hier_root"};
+                                     "hier_root", "large_het"};
 
 template <typename T>
 struct DBuf {
@@ -226,6 +227,11 @@ struct dm_ctx {
   DBuf<int32_t> pa_nan;
   DBuf<uint32_t> pa_live;
   DBuf<uint8_t> p_tot;
+  // heterogeneous FairShare on the chain (allocated on the first tick that may need it)
+  DBuf<int32_t> ph_slist, ph_scnt, ph_bkc;
+  DBuf<uint8_t> ph_het;
+  DBuf<double> ph_bkw;
+  DBuf<int64_t> ph_bks;
   // worklist of resources for k_general (heterogeneous-subclient FairShare)
   DBuf<int32_t> glist, gcount;
   bool maybe_general = false;
@@ -350,6 +356,7 @@ struct dm_ctx {
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
     pa_nan.release(); pa_live.release(); p_tot.release();
+    ph_slist.release(); ph_scnt.release(); ph_bkc.release(); ph_het.release(); ph_bkw.release(); ph_bks.release();
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
     st_mask.release(); st_blk.release(); st_wpre.release(); st_mwants.release(); st_rel.release();
@@ -998,7 +1005,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   Partials P{c->pa_cnt.p, c->pa_has.p, c->pa_wants.p, c->pa_cnt_all.p, c->pa_has_all.p, c->pa_wants_all.p,
              c->pa_smin.p, c->pa_smax.p, c->pa_nan.p,
              c->pb_x.p,   c->pb_y.p,   c->pb_w.p,     c->pc_ee.p,   c->pc_sgt.p,  c->pd_delta.p,
-             c->pa_live.p, c->p_tot.p};
+             c->pa_live.p, c->p_tot.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipStream_t st = c->stream;
   auto timed = [&](int cls, hipStream_t s, auto&& fn) -> hipError_t { return c->timed(cls, s, fn); };
   const int nch = (int)c->h_chunks.size();
@@ -1037,10 +1044,35 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
            "large-resource kernel");
   } else {
     const int nls = (int)c->h_large.size();
-    for (int ph = 0; ph < 5 && nch > 0; ++ph)
-      DM_HIP(c, timed(KC_LARGE_A + ph, s_large,
+    // heterogeneous-subclient FairShare is decided on the chain when the store may
+    // hold it (k_large_t, k_large_c_het, k_large_e, k_large_map_het)
+    const bool het = general && nch > 0;
+    if (het) {
+      const size_t nc = (size_t)nch, nl = (size_t)std::max(nls, 1);
+      DM_HIP(c, c->ph_slist.ensure(nc * kHetMaxS), "heterogeneous partials");
+      DM_HIP(c, c->ph_scnt.ensure(nc), "heterogeneous partials");
+      DM_HIP(c, c->ph_het.ensure(nl * sizeof(HetRes)), "heterogeneous partials");
+      DM_HIP(c, c->ph_bkw.ensure(nc * kHetBuckets), "heterogeneous partials");
+      DM_HIP(c, c->ph_bks.ensure(nc * kHetBuckets), "heterogeneous partials");
+      DM_HIP(c, c->ph_bkc.ensure(nc * kHetBuckets), "heterogeneous partials");
+      P.s_list = c->ph_slist.p;
+      P.s_cnt = c->ph_scnt.p;
+      P.het = c->ph_het.p;
+      P.bk_w = c->ph_bkw.p;
+      P.bk_s = c->ph_bks.p;
+      P.bk_c = c->ph_bkc.p;
+    }
+    // A, B, [T], C, [C_het, E], map, [map_het], fin
+    static constexpr int kSeq[9] = {0, 1, 5, 2, 6, 7, 3, 8, 4};
+    static constexpr int kCls[9] = {KC_LARGE_A, KC_LARGE_B, KC_LARGE_HET, KC_LARGE_C, KC_LARGE_HET, KC_LARGE_HET,
+                                    KC_LARGE_MAP, KC_LARGE_HET, KC_LARGE_FIN};
+    for (int i = 0; i < 9 && nch > 0; ++i) {
+      const int ph = kSeq[i];
+      if (ph >= 5 && !het) continue;
+      DM_HIP(c, timed(kCls[i], s_large,
                       [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
+    }
   }
   // the 128-thread bins split by the dense hint after a writeback tick (hints set)
   const bool split_dense = c->have_result && c->last_writeback;

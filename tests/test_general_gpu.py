@@ -90,3 +90,38 @@ def test_general_every_bin_writeback(eng, seed):
         st = eng.read_store()
         snap = dict(snap, has=st["has"], wants=st["wants"], subclients=st["subclients"], expiry_ns=st["expiry_ns"])
         W.add_store_sums(snap)
+
+
+@pytest.mark.parametrize("n,max_sub,nan", [(1_000_000, 150, False), (250_000, 256, False), (60_000, 40, True)])
+def test_general_on_the_chain_multi_workgroup(eng, n, max_sub, nan):
+    """a large heterogeneous-subclient FairShare resource (a leaf whose
+    clients are downstream servers, server.go:850-879) decided by the chunked chain
+    (k_large_t / k_large_c_het / k_large_e / k_large_map_het: per-chunk bucket partials
+    combined in chunk order) instead of one workgroup.  Against the oracle with the
+    observed error printed (bar 1e-12 on this path) and the tick's kernel time; NaN
+    wants (no threshold) in one variant; deterministic."""
+    rng = np.random.default_rng(n + max_sub)
+    snap = hetero_snapshot(rng, [n, 700, 5000], max_sub, dup_frac=0.05)
+    if nan:
+        snap["wants"][rng.choice(n, 50, replace=False)] = np.nan
+        W.add_store_sums(snap)
+    eng.load(snap)
+    eng.apportion(NOW)
+    eng.set_profiling(True)
+    eng.reset_kernel_times()
+    eng.apportion(NOW)
+    kt = eng.kernel_times()
+    eng.set_profiling(False)
+    gets, exp = eng.leases()
+    ref = O.apportion(snap, NOW)
+    assert_leases_match(snap, gets, exp, ref, f"n={n}")
+    assert_resources_match(snap, eng.resources(), ref, f"n={n}")
+    e = max_err(snap, gets, ref)
+    ms = sum(v[1] for v in kt.values())
+    print(f"\nn={n} distinct={len(np.unique(snap['subclients'][:n]))}: observed error {e:.3e}; "
+          f"kernels {ms * 1e3:.0f} us: " + ", ".join(f"{k} {v[1] * 1e3:.0f}" for k, v in kt.items()))
+    assert "large_het" in kt  # decided on the chain (k_general only takes the 700-row resource)
+    assert e <= 1e-12
+    eng.apportion(NOW)
+    g2, e2 = eng.leases()
+    assert g2.tobytes() == gets.tobytes() and e2.tobytes() == exp.tobytes()
