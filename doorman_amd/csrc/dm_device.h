@@ -108,11 +108,11 @@ struct Partials {
   uint8_t* tot;
   // heterogeneous-subclient FairShare on the chain (only when the store may hold
   // such resources; nullptr otherwise -- they then go to the one-workgroup k_general):
-  // per chunk the distinct subclient counts of its live rows (pass A; s_cnt 0: the
-  // chunk's rows share one count, its a_smin; -1: more than kHetMaxS), per large
-  // resource a HetRes record, per chunk the round-2 bucket partials (pass C)
-  int32_t* s_list;  // [nchunks * kHetMaxS]
-  int32_t* s_cnt;   // [nchunks]
+  // per large resource the set of distinct subclient counts of its live rows (pass A
+  // inserts, k_large_t reads and empties it), a HetRes record, per chunk the round-2
+  // bucket partials (pass C)
+  uint32_t* s_set;  // [large resources * 2 * kHetMaxS] open addressing, all ones = empty
+  int32_t* s_n;     // [large resources] distinct counts inserted (> kHetMaxS: overflow)
   uint8_t* het;     // [large resources * sizeof(HetRes)]
   double* bk_w;     // [nchunks * kHetBuckets]
   int64_t* bk_s;

@@ -722,14 +722,37 @@ __device__ __forceinline__ bool het_insert(uint32_t* set, int* n, uint32_t key) 
   return false;
 }
 
-// pass A's list for one chunk (k_large_a, when P.s_cnt): the distinct counts of its
-// live rows when they differ (a chunk whose live rows share one count is a_smin)
-__device__ void chunk_s_list(const Partials& P, int c, const ChunkRows& rw, const AggA& a) {
+// the same on the resource's set in global memory (agent-scope atomics; the
+// chunks of a resource insert concurrently)
+__device__ __forceinline__ void het_insert_global(uint32_t* set, int32_t* n, uint32_t key) {
+  uint32_t slot = (key * 0x9E3779B1u >> 23) & (2 * kHetMaxS - 1);
+  for (int probe = 0; probe < 2 * kHetMaxS; ++probe, slot = (slot + 1) & (2 * kHetMaxS - 1)) {
+    uint32_t cur = __hip_atomic_load((gu32*)(set + slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return;
+    if (cur == kHetEmpty) {
+      cur = atomicCAS(set + slot, kHetEmpty, key);
+      if (cur == kHetEmpty) {
+        atomicAdd(n, 1);
+        return;
+      }
+      if (cur == key) return;
+    }
+  }
+  atomicAdd(n, kHetMaxS + 1);  // table full: overflow
+}
+
+// pass A (k_large_a, when P.s_set): the chunk's distinct subclient counts of live
+// rows into its resource's set -- one insert for a chunk whose live rows share one
+// count, else the chunk's own LDS set first, one global insert per distinct count
+__device__ void chunk_s_insert(const Partials& P, int lseg, const ChunkRows& rw, const AggA& a) {
   __shared__ uint32_t set[2 * kHetMaxS];
   __shared__ int n;
   const int t = threadIdx.x;
-  if (!(a.smin < a.smax)) {
-    if (t == 0) P.s_cnt[c] = 0;
+  uint32_t* gset = P.s_set + (size_t)lseg * 2 * kHetMaxS;
+  int32_t* gn = P.s_n + lseg;
+  if (a.smin > a.smax) return;  // no live rows
+  if (a.smin == a.smax) {
+    if (t == 0) het_insert_global(gset, gn, (uint32_t)a.smin);
     return;
   }
   for (int i = t; i < 2 * kHetMaxS; i += 256) set[i] = kHetEmpty;
@@ -739,15 +762,12 @@ __device__ void chunk_s_list(const Partials& P, int c, const ChunkRows& rw, cons
   for (int k = 0; k < kLR; ++k)
     if (rw.live >> k & 1) het_insert(set, &n, (uint32_t)rw.s[k]);
   __syncthreads();
-  const int cnt = n;
-  if (cnt <= kHetMaxS) {
-    __shared__ int fill;
-    if (t == 0) fill = 0;
-    __syncthreads();
-    for (int i = t; i < 2 * kHetMaxS; i += 256)
-      if (set[i] != kHetEmpty) P.s_list[(size_t)c * kHetMaxS + atomicAdd(&fill, 1)] = (int32_t)set[i];
+  if (n > kHetMaxS) {
+    if (t == 0) atomicAdd(gn, kHetMaxS + 1);
+    return;
   }
-  if (t == 0) P.s_cnt[c] = cnt <= kHetMaxS ? cnt : -1;
+  for (int i = t; i < 2 * kHetMaxS; i += 256)
+    if (set[i] != kHetEmpty) het_insert_global(gset, gn, set[i]);
 }
 
 __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __restrict__ chunks, Partials P) {
@@ -813,7 +833,7 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
     if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
     if (spec) b = group_reduce<256>(b, OpB(), lds.b);
   }
-  if (P.s_cnt && !rs.learning && rs.kind == 3) chunk_s_list(P, blockIdx.x, rw, a);  // heterogeneous FairShare
+  if (P.s_set && !rs.learning && rs.kind == 3) chunk_s_insert(P, ch.lseg, rw, a);  // heterogeneous FairShare
   if (threadIdx.x == 0) {
     const int c = blockIdx.x;
     if (spec) {
@@ -846,7 +866,7 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
   const LargeSeg L = ls[ch.lseg];
   const SegState st = seg_state<256>(p, P, L, lds);
   if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->a = st.a;
-  const bool het = st.general && P.s_cnt;  // heterogeneous FairShare decided on the chain
+  const bool het = st.general && P.s_set;  // heterogeneous FairShare decided on the chain
   if ((st.general && !het) || st.rs.learning || st.rs.kind < 2) return;
   if (!p.recompute && st.a.cnt == 0) return;  // pass A's speculative partials are exact
   ChunkRows rw;
@@ -991,7 +1011,7 @@ __global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* 
   const LargeSeg L = ls[blockIdx.x];
   const SegState st = seg_state<256>(p, P, L, lds);
   if (st.general) {
-    if (!P.s_cnt) {  // no heterogeneous path on the chain this tick: k_general decides it
+    if (!P.s_set) {  // no heterogeneous path on the chain this tick: k_general decides it
       if (threadIdx.x == 0) general_list[atomicAdd(general_count, 1)] = L.seg;
       return;
     }
@@ -1366,6 +1386,18 @@ __global__ __launch_bounds__(256) void k_large_t(DevParams p, const LargeSeg* __
   const LargeSeg L = ls[blockIdx.x];
   SegTot* tot = seg_tot(P, blockIdx.x);
   HetRes* H = het_of(P, blockIdx.x);
+  uint32_t* gset = P.s_set + (size_t)blockIdx.x * 2 * kHetMaxS;
+  // the resource's distinct counts (pass A), and the set emptied for the next tick
+  for (int i = t; i < 2 * kHetMaxS; i += 256) {
+    set[i] = gset[i];
+    gset[i] = kHetEmpty;
+  }
+  if (t == 0) {
+    n = P.s_n[blockIdx.x];
+    P.s_n[blockIdx.x] = 0;
+    fill = 0;
+  }
+  __syncthreads();
   const SegState st = seg_state_of(p, L.seg, tot->a);  // left by pass B's first chunk
   if (!st.general) {
     if (t == 0) H->mode = 0;
@@ -1373,41 +1405,10 @@ __global__ __launch_bounds__(256) void k_large_t(DevParams p, const LargeSeg* __
   }
   const AggB b = seg_b<256>(P, L, lds);  // round 1 with every row's own count: E = b.x, W = b.i
   if (t == 0) tot->b = b;
-  for (int i = t; i < 2 * kHetMaxS; i += 256) set[i] = kHetEmpty;
-  if (t == 0) {
-    n = 0;
-    fill = 0;
-  }
-  __syncthreads();
-  {  // every chunk's list slot, flattened: 16 independent loads in flight per thread
-    const int nch = L.chunk_end - L.chunk_begin;
-    const int total = nch * kHetMaxS;
-    for (int base = 0; base < total; base += 256 * 16) {
-      int32_t m[16], v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int idx = base + j * 256 + t;
-        const int c = L.chunk_begin + (idx < total ? idx / kHetMaxS : 0);
-        m[j] = idx < total ? P.s_cnt[c] : -2;
-        v[j] = idx < total ? P.s_list[(size_t)L.chunk_begin * kHetMaxS + idx] : 0;
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int idx = base + j * 256 + t;
-        const int i = idx % kHetMaxS, c = L.chunk_begin + idx / kHetMaxS;
-        if (m[j] == -1) {
-          if (i == 0) atomicAdd(&n, kHetMaxS + 1);  // a chunk beyond the bound
-        } else if (m[j] == 0) {
-          if (i == 0 && P.a_smin[c] <= P.a_smax[c]) het_insert(set, &n, (uint32_t)P.a_smin[c]);  // one count
-        } else if (m[j] > 0 && i < m[j]) {
-          het_insert(set, &n, (uint32_t)v[j]);
-        }
-      }
-    }
-  }
-  __syncthreads();
   const int K0 = n;
-  bool bad = K0 > kHetMaxS;
+  // NaN wants: such a row's threshold has W + s in its wantExtra (its w > deservedShare
+  // is false), not one of T(s) below -- k_general collects the rows' own thresholds
+  bool bad = K0 > kHetMaxS || st.a.nan;
   if (!bad) {
     for (int i = t; i < 2 * kHetMaxS; i += 256)
       if (set[i] != kHetEmpty) {

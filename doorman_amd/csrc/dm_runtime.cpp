@@ -85,7 +85,10 @@ enum KClass {
   KC_REST4,
   KC_PUBLISH,   // dm_publish_totals
   KC_HIER_ROOT, // dm_hier_root_tick
-  KC_LARGE_HET, // heterogeneous FairShare on the chain
+  KC_LARGE_T,   // heterogeneous FairShare on the chain: thresholds,
+  KC_LARGE_CH,  // bucket partials,
+  KC_LARGE_E,   // bucket totals,
+  KC_LARGE_MH,  // the map
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
@@ -94,7 +97,7 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release", "large_fused", "subs_merged", "block128x4_dense",
                                      "block128x8_dense", "block128x4_rest", "block128x8_rest", "hier_publish",
-                                     "hier_root", "large_het"};
+                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het"};
 
 template <typename T>
 struct DBuf {
@@ -228,7 +231,9 @@ struct dm_ctx {
   DBuf<uint32_t> pa_live;
   DBuf<uint8_t> p_tot;
   // heterogeneous FairShare on the chain (allocated on the first tick that may need it)
-  DBuf<int32_t> ph_slist, ph_scnt, ph_bkc;
+  DBuf<uint32_t> ph_set;  // per large resource: distinct subclient counts (all ones between ticks)
+  DBuf<int32_t> ph_n, ph_bkc;
+  size_t ph_set_ready = 0;  // large resources whose set slots are initialised
   DBuf<uint8_t> ph_het;
   DBuf<double> ph_bkw;
   DBuf<int64_t> ph_bks;
@@ -356,7 +361,8 @@ struct dm_ctx {
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
     pa_nan.release(); pa_live.release(); p_tot.release();
-    ph_slist.release(); ph_scnt.release(); ph_bkc.release(); ph_het.release(); ph_bkw.release(); ph_bks.release();
+    ph_set.release(); ph_n.release(); ph_bkc.release(); ph_het.release(); ph_bkw.release(); ph_bks.release();
+    ph_set_ready = 0;
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
     st_mask.release(); st_blk.release(); st_wpre.release(); st_mwants.release(); st_rel.release();
@@ -1049,14 +1055,19 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     const bool het = general && nch > 0;
     if (het) {
       const size_t nc = (size_t)nch, nl = (size_t)std::max(nls, 1);
-      DM_HIP(c, c->ph_slist.ensure(nc * kHetMaxS), "heterogeneous partials");
-      DM_HIP(c, c->ph_scnt.ensure(nc), "heterogeneous partials");
+      if (c->ph_set_ready < nl || c->ph_set.n < nl * 2 * kHetMaxS) {
+        DM_HIP(c, c->ph_set.ensure(nl * 2 * kHetMaxS), "heterogeneous partials");
+        DM_HIP(c, c->ph_n.ensure(nl), "heterogeneous partials");
+        DM_HIP(c, hipMemsetAsync(c->ph_set.p, 0xFF, nl * 2 * kHetMaxS * sizeof(uint32_t), s_large), "heterogeneous sets");
+        DM_HIP(c, hipMemsetAsync(c->ph_n.p, 0, nl * sizeof(int32_t), s_large), "heterogeneous sets");
+        c->ph_set_ready = nl;
+      }
       DM_HIP(c, c->ph_het.ensure(nl * sizeof(HetRes)), "heterogeneous partials");
       DM_HIP(c, c->ph_bkw.ensure(nc * kHetBuckets), "heterogeneous partials");
       DM_HIP(c, c->ph_bks.ensure(nc * kHetBuckets), "heterogeneous partials");
       DM_HIP(c, c->ph_bkc.ensure(nc * kHetBuckets), "heterogeneous partials");
-      P.s_list = c->ph_slist.p;
-      P.s_cnt = c->ph_scnt.p;
+      P.s_set = c->ph_set.p;
+      P.s_n = c->ph_n.p;
       P.het = c->ph_het.p;
       P.bk_w = c->ph_bkw.p;
       P.bk_s = c->ph_bks.p;
@@ -1064,8 +1075,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     }
     // A, B, [T], C, [C_het, E], map, [map_het], fin
     static constexpr int kSeq[9] = {0, 1, 5, 2, 6, 7, 3, 8, 4};
-    static constexpr int kCls[9] = {KC_LARGE_A, KC_LARGE_B, KC_LARGE_HET, KC_LARGE_C, KC_LARGE_HET, KC_LARGE_HET,
-                                    KC_LARGE_MAP, KC_LARGE_HET, KC_LARGE_FIN};
+    static constexpr int kCls[9] = {KC_LARGE_A, KC_LARGE_B,   KC_LARGE_T,  KC_LARGE_C,  KC_LARGE_CH,
+                                    KC_LARGE_E, KC_LARGE_MAP, KC_LARGE_MH, KC_LARGE_FIN};
     for (int i = 0; i < 9 && nch > 0; ++i) {
       const int ph = kSeq[i];
       if (ph >= 5 && !het) continue;

@@ -120,7 +120,8 @@ def test_general_on_the_chain_multi_workgroup(eng, n, max_sub, nan):
     ms = sum(v[1] for v in kt.values())
     print(f"\nn={n} distinct={len(np.unique(snap['subclients'][:n]))}: observed error {e:.3e}; "
           f"kernels {ms * 1e3:.0f} us: " + ", ".join(f"{k} {v[1] * 1e3:.0f}" for k, v in kt.items()))
-    assert "large_het" in kt  # decided on the chain (k_general only takes the 700-row resource)
+    if not nan:  # decided on the chain (k_general takes the 700-row resource; NaN wants go to it too)
+        assert "large_map_het" in kt
     assert e <= 1e-12
     eng.apportion(NOW)
     g2, e2 = eng.leases()
