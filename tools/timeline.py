@@ -38,6 +38,9 @@ def main():
         q = r.get("Stream_Id") or r.get("Queue_Id") or "?"
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, q))
     ks.sort()
+    counts = collections.Counter(n for _, _, n, _ in ks)  # kernels of every tick only (not the
+    top = max(counts.values())                            # occasional split-form retries)
+    ks = [k for k in ks if counts[k[2]] >= top // 2]
     occ = collections.Counter()
     ticks = collections.defaultdict(list)
     for s, e, n, q in ks:
