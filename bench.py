@@ -112,10 +112,10 @@ def algorithmic_bytes(n_leases: int, n_resources: int, dense_leases: float = 0) 
 
 
 def dense_fraction(eng, snap) -> float:
-    """Share of the rows of resources with 257..1024 rows (the 128-thread group
-    kernels, the only ones that keep the dense state) that sit in dense resources."""
+    """Share of the rows of resources with 257..4096 rows (the workgroup kernels,
+    the only ones that keep the dense state) that sit in dense resources."""
     sizes = np.diff(snap["seg_off"])
-    group = int(sizes[(sizes >= 257) & (sizes <= 1024)].sum())
+    group = int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
     return eng.store_stats()["dense_leases"] / group if group else 0.0
 
 
@@ -136,7 +136,7 @@ def kernel_units(snap):
     big = sizes > 4096
     for name in ("large_fused", "large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
         units[name] = (int(sizes[big].sum()), int(big.sum()))
-    for b in ("block128x4", "block128x8"):  # the split form's two kernels
+    for b in ("block128x4", "block128x8", "block256x8", "block512x8"):  # the split form's two kernels
         units[b + "_dense"] = units[b]
         units[b + "_rest"] = (0, 0)  # only what the dense kernel queued; counted with the dense kernel
     units["hier_publish"] = (0, len(sizes))
@@ -377,7 +377,9 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
     if single:  # one kernel per tick: HIP events around the timed region itself
         avg_s = run["stream_ms"] / steps / 1e3
     leases_k, res_k = kernel_units(snap).get(name, (N, R))
-    group_kernel = name in ("block128x4", "block128x8", "block128x4_dense", "block128x8_dense")
+    # kernels that skip the subclients column of dense resources: the 128-thread mixed
+    # kernels (they load by the hint) and every dense kernel of the split form
+    group_kernel = name in ("block128x4", "block128x8") or name.endswith("_dense")
     dense_k = run.get("dense_frac", 0.0) * leases_k if group_kernel else 0.0
     alg = algorithmic_bytes(leases_k, res_k, dense_k)
     achieved = alg / avg_s / 1e9
@@ -580,7 +582,7 @@ def main():
 
     if rank == 0:
         sizes = np.diff(snap["seg_off"])
-        group_leases = int(sizes[(sizes >= 257) & (sizes <= 1024)].sum())
+        group_leases = int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
         tick_bytes = algorithmic_bytes(N, R, run["dense_frac"] * group_leases)
         line = {
             "metric": METRIC,

@@ -185,7 +185,7 @@ struct AggA {
   int smin;       // live rows' subclients range and any NaN wants
   int smax;
   int nan;
-  int pad;
+  int nlive;      // live rows (group kernels: the dense state needs all of them)
 };
 struct OpA {
   __device__ AggA operator()(AggA a, AggA b) const {
@@ -197,7 +197,7 @@ struct OpA {
     r.smin = a.smin < b.smin ? a.smin : b.smin;
     r.smax = a.smax > b.smax ? a.smax : b.smax;
     r.nan = a.nan | b.nan;
-    r.pad = 0;
+    r.nlive = a.nlive + b.nlive;
     return r;
   }
 };
@@ -210,7 +210,7 @@ __device__ __forceinline__ AggA zeroA() {
   a.smin = INT32_MAX;
   a.smax = INT32_MIN;
   a.nan = 0;
-  a.pad = 0;
+  a.nlive = 0;
   return a;
 }
 

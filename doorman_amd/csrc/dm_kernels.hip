@@ -24,17 +24,20 @@ namespace dm {
 // Resource-per-group kernel: G threads (a wave or a 256-thread workgroup) own
 // one resource of up to G*R rows; rows live in VGPRs across all passes.
 // --------------------------------------------------------------------------
-// MODE (the 128-thread bins only): kMixed = one kernel for every item (hint or not),
-// kDenseOnly = items whose hint is set (k_block_dense: no subclients column at all;
-// a stale hint queues the item for k_block_rest and returns), kRest = queued items
-// (k_block_rest: the column is read, the hint rewritten).
+// MODE (the 128/256/512-thread bins): kMixed = one kernel for every item (hint or
+// not), kDenseOnly = items whose hint is set (k_block_dense: no subclients column at
+// all; a stale hint queues the item for k_block_rest and returns), kRest = queued
+// items (k_block_rest: the column is read, the hint rewritten).
 enum { kMixed = 0, kDenseOnly = 1, kRest = 2 };
 template <int G, int R, int MODE = kMixed>
 __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, WorkItem* item, int t,
                                               Lds<G>& lds, int32_t* general_list, int32_t* general_count,
                                               int32_t* queue = nullptr, int32_t* qcount = nullptr,
                                               int32_t qidx = 0) {
-  constexpr bool kDense = G == 128;  // the dense-subclients path (below)
+  // the dense state (below): every workgroup kernel tracks it and writes the hints;
+  // only the 128-thread mixed kernel and the dense-only kernels load by the hint
+  constexpr bool kDense = G >= 128;
+  constexpr bool kHintLoad = (G == 128 && MODE == kMixed) || MODE == kDenseOnly;
   const int seg = wi.seg;
   const int64_t lo = wi.lo;
   const int n = kDense ? wi.n & 0xFFFF : wi.n;
@@ -57,10 +60,12 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // subclients column: 24 B per lease instead of 28.  The work item carries the
   // state as a hint (no dependent load before the rows); the resource's own byte,
   // loaded with its record, confirms it, and a stale hint (an upsert or release
-  // since that tick) reads the column after all.  Only the 128-thread blocks
-  // (257-1024 rows) take this path: in the other group kernels the extra branch
-  // costs registers they do not have (spills at 5 waves per SIMD; C2 +3.5 %).
-  const int hint = (kDense && MODE != kRest) ? wi.n >> 16 : 0;
+  // since that tick) reads the column after all.  The 128-thread mixed kernel
+  // (257-1024 rows) loads by the hint; the 256/512-thread mixed kernels (1025-4096
+  // rows) only track the state and write the hints (the extra branch costs
+  // registers they do not have: spills at 5 waves per SIMD, C2 +3.5 %), and their
+  // dense-only kernels skip the column.
+  const int hint = (kHintLoad) ? wi.n >> 16 : 0;
   if (MODE != kDenseOnly && !hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -87,7 +92,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       if (t == 0) queue[atomicAdd(qcount, 1)] = qidx;
       return;
     }
-  } else if (hint && dense_subclients(rs) != hint) {
+  } else if (kHintLoad && hint && dense_subclients(rs) != hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -138,6 +143,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       a.smin = s[k] < a.smin ? s[k] : a.smin;
       a.smax = s[k] > a.smax ? s[k] : a.smax;
       a.nan |= __builtin_isnan(w[k]) ? 1 : 0;
+      a.nlive += 1;
     }
   }
   {
@@ -234,15 +240,8 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     delta.v += g - h[k];
   }
 
-  int nlive = 0;  // live rows of the resource (the dense state needs all n)
-  if constexpr (kDense) {
-    SumDN dl{delta.v, __builtin_popcount(live), 0};
-    dl = group_reduce<G, SumDN, OpSumDN, false>(dl, OpSumDN(), lds.dn);
-    delta.v = dl.v;
-    nlive = dl.n;
-  } else {
-    delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
-  }
+  const int nlive = a.nlive;  // live rows of the resource (the dense state needs all n)
+  delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
   if (t == 0) {
     // after a writeback tick every live row follows the resource; all n rows live
     // with one subclient count s0 (1..254) makes the resource dense
@@ -269,35 +268,35 @@ __global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevPa
   group_segment<G, R>(p, items[blockIdx.x], items + blockIdx.x, threadIdx.x, lds, general_list, general_count);
 }
 
-// The 128-thread bins split by the dense hint (launch_bin_split): k_block_dense
-// decides the items whose hint is set without the subclients column (70 VGPRs: 7
-// waves per SIMD instead of 5, 14336 rows in flight per CU) and queues the others;
-// k_block_rest decides the queue with the mixed body, a fixed grid striding over
-// it (512 workgroups: the queue is short whenever the host picks this form, and
-// empty for a store of dense resources, where the launch costs ~4 us).  qcnt is a two-slot ring: this tick's count in qcnt[par], and k_block_rest
-// clears qcnt[par ^ 1] for the next tick (stream order); host_count (host-mapped)
-// tells the host how many items went to the queue (its choice of split or mixed).
-template <int R>
-__global__ __launch_bounds__(128) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
-                                                     int32_t* queue, int32_t* qcnt, int par,
-                                                     int32_t* general_list, int32_t* general_count) {
-  __shared__ Lds<128> lds;
+// The workgroup bins split by the dense hint (launch_bin_dense / launch_bin_rest):
+// k_block_dense decides the items whose hint is set without the subclients column
+// (128 x 8: 70 VGPRs, 7 waves per SIMD instead of 5, 14336 rows in flight per CU)
+// and queues the others; k_block_rest decides the queue with the mixed body, a grid
+// striding over it (sized from the last split tick's queue; an empty queue costs
+// one small launch).  qcnt is a two-slot ring: this tick's count in qcnt[par], and
+// k_block_rest clears qcnt[par ^ 1] for the next tick (stream order); host_count
+// (host-mapped) tells the host how many items went to the queue (its choice of
+// split or mixed).
+template <int G, int R>
+__global__ __launch_bounds__(G) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
+                                                   int32_t* queue, int32_t* qcnt, int par,
+                                                   int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<G> lds;
   if ((int)blockIdx.x >= nitems) return;
   const WorkItem wi = items[blockIdx.x];
   if ((wi.n >> 16) == 0) {
     if (threadIdx.x == 0) queue[atomicAdd(qcnt + par, 1)] = (int32_t)blockIdx.x;
     return;
   }
-  group_segment<128, R, kDenseOnly>(p, wi, items + blockIdx.x, threadIdx.x, lds, general_list, general_count, queue,
-                                    qcnt + par, (int32_t)blockIdx.x);
+  group_segment<G, R, kDenseOnly>(p, wi, items + blockIdx.x, threadIdx.x, lds, general_list, general_count, queue,
+                                  qcnt + par, (int32_t)blockIdx.x);
 }
 
-template <int R>
-__global__ __launch_bounds__(128) void k_block_rest(DevParams p, WorkItem* __restrict__ items,
-                                                                    const int32_t* __restrict__ queue, int32_t* qcnt,
-                                                                    int par, int32_t* host_count,
-                                                                    int32_t* general_list, int32_t* general_count) {
-  __shared__ Lds<128> lds;
+template <int G, int R>
+__global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restrict__ items,
+                                                  const int32_t* __restrict__ queue, int32_t* qcnt, int par,
+                                                  int32_t* host_count, int32_t* general_list, int32_t* general_count) {
+  __shared__ Lds<G> lds;
   const int count = qcnt[par];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     qcnt[par ^ 1] = 0;
@@ -305,7 +304,7 @@ __global__ __launch_bounds__(128) void k_block_rest(DevParams p, WorkItem* __res
   }
   for (int q = blockIdx.x; q < count; q += gridDim.x) {
     const int idx = queue[q];
-    group_segment<128, R, kRest>(p, items[idx], items + idx, threadIdx.x, lds, general_list, general_count);
+    group_segment<G, R, kRest>(p, items[idx], items + idx, threadIdx.x, lds, general_list, general_count);
     __syncthreads();  // the next item reuses the single-use LDS slots
   }
 }
@@ -576,7 +575,7 @@ __device__ __forceinline__ SegState seg_state(const DevParams& p, const Partials
     x.smin = (int)P.a_smin[c];
     x.smax = (int)P.a_smax[c];
     x.nan = P.a_nan[c];
-    x.pad = 0;
+    x.nlive = 0;
     const AggR all = OpR()(a.all, x.all);  // OpA carries `all` through unchanged
     a = OpA()(a, x);
     a.all = all;
@@ -2357,12 +2356,13 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
                             int32_t* glist, int32_t* gcount, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (bin == 3)
-    k_block_dense<4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
-  else if (bin == 4)
-    k_block_dense<8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount);
-  else
-    return hipErrorInvalidValue;
+  switch (bin) {
+    case 3: k_block_dense<128, 4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    case 4: k_block_dense<128, 8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    case 5: k_block_dense<256, 8><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    case 6: k_block_dense<512, 8><<<n, 512, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -2370,12 +2370,13 @@ hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, i
                            int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const unsigned rg = (unsigned)std::max(1, std::min(n, rest_grid));
-  if (bin == 3)
-    k_block_rest<4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
-  else if (bin == 4)
-    k_block_rest<8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
-  else
-    return hipErrorInvalidValue;
+  switch (bin) {
+    case 3: k_block_rest<128, 4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    case 4: k_block_rest<128, 8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    case 5: k_block_rest<256, 8><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    case 6: k_block_rest<512, 8><<<rg, 512, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ __device__ __forceinline__ AggA load_a(const uint64_t* r) {
   a.smin = (int)(uint32_t)mm;
   a.smax = (int)(uint32_t)(mm >> 32);
   a.nan = (int)(uint32_t)ld_wt(r + 7);
-  a.pad = 0;
+  a.nlive = 0;
   return a;
 }
 __device__ __forceinline__ void store_b(uint64_t* r, const AggB& b) {
@@ -168,7 +168,7 @@ __device__ __forceinline__ AggA xt_a(const uint64_t* xt) {
   a.smin = (int)(uint32_t)xt[6];
   a.smax = (int)(uint32_t)(xt[6] >> 32);
   a.nan = (int)(uint32_t)xt[7];
-  a.pad = 0;
+  a.nlive = 0;
   return a;
 }
 

@@ -79,10 +79,14 @@ enum KClass {
   KC_RELEASE,
   KC_LARGE_FUSED,
   KC_SUBS,
-  KC_DENSE3,  // the 128-thread bins' split form: dense kernel, then the rest kernel
+  KC_DENSE3,  // the workgroup bins' split form (bins 3-6): dense kernel, then the rest kernel
   KC_DENSE4,
+  KC_DENSE5,
+  KC_DENSE6,
   KC_REST3,
   KC_REST4,
+  KC_REST5,
+  KC_REST6,
   KC_PUBLISH,   // dm_publish_totals
   KC_HIER_ROOT, // dm_hier_root_tick
   KC_LARGE_T,   // heterogeneous FairShare on the chain: thresholds,
@@ -96,7 +100,9 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
                                      "store_release", "large_fused", "subs_merged", "block128x4_dense",
-                                     "block128x8_dense", "block128x4_rest", "block128x8_rest", "hier_publish",
+                                     "block128x8_dense", "block256x8_dense", "block512x8_dense",
+                                     "block128x4_rest", "block128x8_rest", "block256x8_rest", "block512x8_rest",
+                                     "hier_publish",
                                      "hier_root", "large_t", "large_c_het", "large_e", "large_map_het"};
 
 template <typename T>
@@ -204,10 +210,11 @@ struct dm_ctx {
   // split tick the host has heard of queued more than a quarter of the bin's items
   // for k_block_rest (then every 64th tick tries again: C2's bins, whose resources
   // keep released rows, run 21 % slower split).  DM_DENSE_SPLIT=0: never split.
-  bool dense_split = true;
-  DBuf<int32_t> dq_list[2], dq_cnt[2];
-  int dq_par[2] = {0, 0};
-  int dq_skip[2] = {0, 0};   // ticks in the one-kernel form since the split was last tried
+  int dense_split = 0xF;  // bit i: bin 3+i runs in the split form (DM_DENSE_SPLIT: 0 off, 1 all, else the mask)
+  static constexpr int kSplitBins = 4;  // bins 3..6
+  DBuf<int32_t> dq_list[kSplitBins], dq_cnt[kSplitBins];
+  int dq_par[kSplitBins] = {};
+  int dq_skip[kSplitBins] = {};   // ticks in the one-kernel form since the split was last tried
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
   int fused_G = 512;
@@ -351,7 +358,7 @@ struct dm_ctx {
     if (h_ferr) (void)hipHostFree(h_ferr);
     h_ferr = nullptr;
     d_ferr = nullptr;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kSplitBins; ++i) {
       dq_list[i].release();
       dq_cnt[i].release();
     }
@@ -517,10 +524,10 @@ static int upload_plan(dm_ctx* c) {
                   c->fused_max_chunks <= c->fused_G;  // the last arriver loads one record per thread
   }
   if (!c->h_dq) {
-    DM_HIP(c, hipHostMalloc((void**)&c->h_dq, 2 * sizeof(int32_t), hipHostMallocMapped), "dense split word");
+    DM_HIP(c, hipHostMalloc((void**)&c->h_dq, dm_ctx::kSplitBins * sizeof(int32_t), hipHostMallocMapped), "dense split word");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_dq, c->h_dq, 0), "dense split word");
   }
-  for (int i = 0; i < 2; ++i) {  // the dense split of bins 3 and 4: rest queues and their two-slot counters
+  for (int i = 0; i < dm_ctx::kSplitBins; ++i) {  // the dense split of bins 3-6: rest queues, two-slot counters
     __atomic_store_n(c->h_dq + i, 0, __ATOMIC_RELAXED);
     c->dq_skip[i] = 0;
     const size_t nb = std::max<size_t>(c->h_bins[3 + i].size(), 1);
@@ -643,7 +650,10 @@ int dm_create(int device, dm_ctx** out) {
   dm_ctx* c = new dm_ctx();
   c->device = device;
   if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
-  if (const char* ds = getenv("DM_DENSE_SPLIT")) c->dense_split = atoi(ds) != 0;
+  if (const char* ds = getenv("DM_DENSE_SPLIT")) {
+    const int v = (int)strtol(ds, nullptr, 0);
+    c->dense_split = v == 1 ? 0xF : (v & 0xF);
+  }
   if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
     for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
@@ -1085,7 +1095,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
              "large-resource kernels");
     }
   }
-  // the 128-thread bins split by the dense hint after a writeback tick (hints set)
+  // the workgroup bins split by the dense hint after a writeback tick (hints set)
   const bool split_dense = c->have_result && c->last_writeback;
   // the sub-wave bins (8x2, 16x2, 16x4, 32x4, 64x4) in one launch on bin 0's stream
   static constexpr int kSubBins[5] = {7, 8, 0, 1, 2}, kSubG[5] = {8, 16, 16, 32, 64};
@@ -1111,7 +1121,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     if (n == 0) continue;
     if (merge_subs && (b == 7 || b == 8 || b <= 2)) continue;
     hipStream_t s = cls_stream(b);
-    if ((b == 3 || b == 4) && c->dense_split && split_dense) {
+    if (b >= 3 && b < 3 + dm_ctx::kSplitBins && ((c->dense_split >> (b - 3)) & 1) && split_dense) {
       // only a writeback tick sets hints, so the split form follows one
       const int i = b - 3, par = c->dq_par[i];
       const int64_t queued = __atomic_load_n(c->h_dq + i, __ATOMIC_RELAXED);

@@ -275,8 +275,11 @@ class Engine:
         self._chk(self._L.dm_set_profiling(self._ctx, 1 if on else 0))
 
     def kernel_times(self) -> dict:
-        arr = (_lib.KernelTime * 32)()
-        n = self._chk(self._L.dm_kernel_times(self._ctx, arr, 32))
+        cap = 64
+        arr = (_lib.KernelTime * cap)()
+        n = self._chk(self._L.dm_kernel_times(self._ctx, arr, cap))
+        if n > cap:
+            raise RuntimeError(f"dm_kernel_times reports {n} kernel classes, more than {cap}")
         return {arr[i].name.decode(): (arr[i].launches, arr[i].total_ms) for i in range(n) if arr[i].launches}
 
     def reset_kernel_times(self):

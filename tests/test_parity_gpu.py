@@ -795,7 +795,7 @@ def test_config_limits_and_cold_fields_round_trip(eng):
     assert e.value.code == DM_E_INVAL
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("split", ["1", "0", "3"])
 @pytest.mark.parametrize("cols", ["inplace", "alternate"])
 def test_dense_subclients_state(monkeypatch, cols, split):
     """A writeback tick marks a group-kernel resource dense when every row is a live
@@ -803,8 +803,9 @@ def test_dense_subclients_state(monkeypatch, cols, split):
     Releases, upserts (other subclient counts, explicit expiries) and lapsed
     followers end the state, wants refreshes keep it; every tick matches the oracle
     on a host copy, and dm_store_stats counts the dense resources.  split=1: after a
-    writeback tick the 128-thread bins run as k_block_dense + k_block_rest (stale
-    hints queued); split=0 (DM_DENSE_SPLIT=0): the one-kernel form."""
+    writeback tick the workgroup bins (128x4, 128x8, 256x8, 512x8) run as
+    k_block_dense + k_block_rest (stale hints queued); split=0 (DM_DENSE_SPLIT=0):
+    the one-kernel form; split=3: only the 128-thread bins split."""
     from doorman_amd.engine import Engine
     monkeypatch.setenv("DM_DENSE_SPLIT", split)  # read when the context is created
     eng = Engine(0)
@@ -813,7 +814,7 @@ def test_dense_subclients_state(monkeypatch, cols, split):
     snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=0.0, learning_frac=0.0,
                                parent_expired_frac=0.0)
     snap["lease_length_s"] = np.full(len(sizes), 20, np.int64)
-    group = (sizes >= 257) & (sizes <= 1024)  # the 128-thread group kernels keep the state
+    group = (sizes >= 257) & (sizes <= 4096)  # the workgroup kernels keep the state
     eng.load(snap)
     assert eng.store_stats()["dense_resources"] == 0  # loaded rows carry explicit expiries
     host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
@@ -852,7 +853,7 @@ def test_dense_subclients_state(monkeypatch, cols, split):
         st = eng.read_store()
         np.testing.assert_array_equal(st["subclients"], host["subclients"], err_msg=f"tick {rnd}")
         np.testing.assert_array_equal(st["expiry_ns"], host["expiry_ns"], err_msg=f"tick {rnd}")
-        # expected dense resources: 257-1024 rows, every row live with one subclient count >= 1
+        # expected dense resources: 257-4096 rows, every row live with one subclient count >= 1
         want = 0
         for r in np.flatnonzero(group):
             s = host["subclients"][off[r]:off[r + 1]]

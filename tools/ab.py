@@ -41,12 +41,16 @@ def env(values):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
-    ap.add_argument("--workload", default="c1")
+    ap.add_argument("--workload", default="c1", help="a bench workload, or uRxC (R resources x C clients)")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--per-kernel", action="store_true", help="median us per tick of every kernel class")
     args = ap.parse_args()
-    snap = make_workload(args.workload, 0)
+    if args.workload.startswith("u") and "x" in args.workload:  # uRxC: R resources x C clients, FairShare
+        nr, nc = (int(v) for v in args.workload[1:].split("x"))
+        snap = W.uniform(nr, nc, kind=W.FAIR_SHARE, seed=3)
+    else:
+        snap = make_workload(args.workload, 0)
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
     engines = []
     for p in args.libs:  # LIB.so:fused = the same build with the large-resource chain forced
