@@ -153,6 +153,33 @@ struct FusedState {
   uint32_t spin_limit;  // polls (s_sleep 8 each) before a wait gives up
 };
 
+// Persistent large path (k_large_flow, dm_flow.hip): the chain's phases as tasks of
+// one launch.  A task word is phase << 30 | chunk: phase 0 = pass A (Clean + the
+// speculative round 1) of one chunk, 1 = round 1 again (only where Clean released
+// subclients, or recompute mode) for up to kFlowBundle chunks from that one, 2 =
+// FairShare round 2 of one chunk, 3 = the map of one chunk (its resource's last
+// chunk to finish writes the record).  Workgroups take tasks in list order from a
+// ticket counter; a task only waits for tasks earlier in the list (its resource's
+// previous phases), which running workgroups already hold, so the queue drains
+// with any number of resident workgroups (no co-residency bound).
+constexpr int kFlowBundle = 8;
+constexpr uint32_t kFlowA = 0u, kFlowB = 1u, kFlowC = 2u, kFlowM = 3u;
+struct FlowState {
+  const uint32_t* tasks;   // [ntasks], dependencies before dependants
+  const Chunk* chunks;     // the chain's chunks (kChunkRows rows)
+  const LargeSeg* large;
+  uint32_t* ticket;        // [2]: launch epoch parity picks one, block 0 clears the other
+  uint32_t* sync;          // [nls * kFusedSync] arrive counters (reset by their last arriver) + phase flags
+  uint64_t* part;          // [nchunks * kFusedWords] per-chunk records (dm_records.h)
+  uint64_t* tot;           // [nls * kFusedWords] per-resource totals
+  uint32_t* live;          // [nchunks * 256] pass A's row masks per thread (live | expl << 8 | rel << 16)
+  uint32_t* err;           // host-mapped word: a bounded wait gave up
+  int32_t ntasks;
+  uint32_t epoch;          // launch number, never 0
+  uint32_t spin_limit;
+  int32_t batch;           // consecutive tickets a workgroup takes per counter add (>= 1)
+};
+
 // row -> resource lookup for store updates: seg_off plus, for every block of
 // 2^kRowBlkShift rows, the resource holding its first row
 constexpr int kRowBlkShift = 12;

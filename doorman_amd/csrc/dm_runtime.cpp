@@ -32,6 +32,9 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 hipError_t launch_large_fused(int G, const DevParams& p, const Chunk* chunks, const LargeSeg* ls, const FusedState& F,
                               int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t large_fused_occupancy(int G, int* blocks_per_cu);
+hipError_t launch_large_flow(const DevParams& p, const FlowState& F, int grid, int32_t* glist, int32_t* gcount,
+                             hipStream_t st);
+hipError_t large_flow_occupancy(int* blocks_per_cu);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int32_t* sub32, const int64_t* expiry, const ResCfg* cfg, int64_t now,
                          const RowIndex& ix, double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp,
@@ -93,6 +96,7 @@ enum KClass {
   KC_LARGE_CH,  // bucket partials,
   KC_LARGE_E,   // bucket totals,
   KC_LARGE_MH,  // the map
+  KC_LARGE_FLOW,  // the persistent large path (dm_flow.hip)
   KC_COUNT
 };
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
@@ -103,7 +107,8 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "block128x8_dense", "block256x8_dense", "block512x8_dense",
                                      "block128x4_rest", "block128x8_rest", "block256x8_rest", "block512x8_rest",
                                      "hier_publish",
-                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het"};
+                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het",
+                                     "large_flow"};
 
 template <typename T>
 struct DBuf {
@@ -231,6 +236,16 @@ struct dm_ctx {
   uint32_t* h_ferr = nullptr;  // host-mapped: a fused wait gave up
   uint32_t* d_ferr = nullptr;
   bool use_fused() const { return large_mode == DM_LARGE_FUSED && fused_ok && !h_fchunks.empty(); }
+  // persistent large path (dm_flow.hip): the chain's chunks, phases as listed tasks
+  std::vector<uint32_t> h_fl_tasks;
+  DBuf<uint32_t> fl_tasks, fl_ticket, fl_sync;
+  DBuf<uint64_t> fl_part, fl_tot;
+  int fl_grid = 0;          // workgroups of the persistent launch
+  int fl_wg_per_cu = 2;     // DM_FLOW_WG: resident workgroups per CU it asks for
+  int fl_lag = -1;          // DM_FLOW_LAG: list distance between a phase and the next (-1: the grid)
+  int fl_batch = 1;         // DM_FLOW_BATCH: tickets per counter add
+  int fl_grid_force = 0;    // DM_FLOW_GRID: exact grid (tests run the queue on one or a few workgroups)
+  uint32_t fl_epoch = 0;
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
@@ -355,6 +370,7 @@ struct dm_ctx {
     out_gets.release(); out_expiry.release(); res.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
     fchunks.release(); flarge.release(); f_ticket.release(); f_sync.release(); f_part.release(); f_tot.release();
+    fl_tasks.release(); fl_ticket.release(); fl_sync.release(); fl_part.release(); fl_tot.release();
     if (h_ferr) (void)hipHostFree(h_ferr);
     h_ferr = nullptr;
     d_ferr = nullptr;
@@ -490,6 +506,35 @@ static void build_plan(dm_ctx* c) {
   close();
 }
 
+// The persistent large path's task list (dm_flow.hip): every task after the tasks
+// it waits for.  Keys in units of list positions: pass A of chunk q at q; a
+// resource's round-1 bundles `lag` after its last pass-A task, its round-2 tasks
+// after those, its map tasks `lag` after its last round-2 task -- so a dependent task
+// is taken about one grid's worth of tasks after what it needs (rarely waiting), and
+// the rows it re-reads were read a short while before (Infinity Cache).
+static void build_flow_tasks(dm_ctx* c, int64_t lag) {
+  struct K {
+    int64_t key;
+    uint32_t ph;
+    int32_t q;
+  };
+  std::vector<K> v;
+  v.reserve(c->h_chunks.size() * 3 + c->h_large.size() * 2);
+  for (const LargeSeg& L : c->h_large) {
+    const int64_t f = L.chunk_begin, l = L.chunk_end, n = l - f;
+    for (int64_t q = f; q < l; ++q) v.push_back(K{q, kFlowA, (int32_t)q});
+    const int64_t kb = l - 1 + lag;
+    for (int64_t q = f; q < l; q += kFlowBundle) v.push_back(K{kb, kFlowB, (int32_t)q});
+    for (int64_t q = f; q < l; ++q) v.push_back(K{kb + 1 + (q - f), kFlowC, (int32_t)q});
+    for (int64_t q = f; q < l; ++q) v.push_back(K{kb + 1 + n + lag + (q - f), kFlowM, (int32_t)q});
+  }
+  std::stable_sort(v.begin(), v.end(), [](const K& a, const K& b) {
+    return a.key != b.key ? a.key < b.key : (a.ph != b.ph ? a.ph < b.ph : a.q < b.q);
+  });
+  c->h_fl_tasks.resize(v.size());
+  for (size_t i = 0; i < v.size(); ++i) c->h_fl_tasks[i] = v[i].ph << 30 | (uint32_t)v[i].q;
+}
+
 static int upload_plan(dm_ctx* c) {
   hipStream_t st = c->stream;
   DM_HIP(c, upload(c->packs, c->h_packs.data(), c->h_packs.size(), st), "plan packs");
@@ -537,6 +582,21 @@ static int upload_plan(dm_ctx* c) {
     c->dq_par[i] = 0;
   }
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
+  {  // persistent large path: grid, task list, hand-off state
+    int per_cu = 0, cus = 0;
+    DM_HIP(c, large_flow_occupancy(&per_cu), "flow occupancy");
+    DM_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "CU count");
+    c->fl_grid = c->fl_grid_force > 0 ? c->fl_grid_force : std::max(1, std::min(per_cu, c->fl_wg_per_cu) * cus);
+    build_flow_tasks(c, c->fl_lag >= 0 ? c->fl_lag : c->fl_grid);
+    const size_t nl = std::max<size_t>(c->h_large.size(), 1);
+    DM_HIP(c, upload(c->fl_tasks, c->h_fl_tasks.data(), c->h_fl_tasks.size(), st), "flow tasks");
+    DM_HIP(c, c->fl_ticket.ensure(2), "flow state");
+    DM_HIP(c, c->fl_sync.ensure(nl * kFusedSync), "flow state");
+    DM_HIP(c, c->fl_part.ensure(nc * kFusedWords), "flow state");
+    DM_HIP(c, c->fl_tot.ensure(nl * kFusedWords), "flow state");
+    DM_HIP(c, hipMemsetAsync(c->fl_ticket.p, 0, 2 * sizeof(uint32_t), st), "flow state");
+    DM_HIP(c, hipMemsetAsync(c->fl_sync.p, 0, nl * kFusedSync * sizeof(uint32_t), st), "flow state");
+  }
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
   DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
   DM_HIP(c, c->pa_has_all.ensure(nc), "partials");
@@ -596,6 +656,12 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
 static int check_fused(dm_ctx* c) {
   if (c->h_ferr && __atomic_load_n(c->h_ferr, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(c->h_ferr, 0u, __ATOMIC_RELEASE);
+    // arrive counters of the gave-up launch were left part-way: start the next from zero
+    (void)hipStreamSynchronize(c->stream);
+    if (c->f_sync.p) (void)hipMemset(c->f_sync.p, 0, c->f_sync.n * sizeof(uint32_t));
+    if (c->fl_sync.p) (void)hipMemset(c->fl_sync.p, 0, c->fl_sync.n * sizeof(uint32_t));
+    if (c->fl_ticket.p) (void)hipMemset(c->fl_ticket.p, 0, c->fl_ticket.n * sizeof(uint32_t));
+    if (c->f_ticket.p) (void)hipMemset(c->f_ticket.p, 0, c->f_ticket.n * sizeof(uint32_t));
     c->have_result = false;  // the tick's leases are invalid
     if (c->last_writeback) {
       c->store_lost = true;
@@ -655,6 +721,11 @@ int dm_create(int device, dm_ctx** out) {
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
   }
   if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
+  if (const char* lp = getenv("DM_LARGE_PATH")) c->large_mode = atoi(lp);  // A/B: 0 chain, 1 fused, 2 flow
+  if (const char* fw = getenv("DM_FLOW_WG")) c->fl_wg_per_cu = std::max(1, atoi(fw));
+  if (const char* fl = getenv("DM_FLOW_LAG")) c->fl_lag = atoi(fl);
+  if (const char* fb = getenv("DM_FLOW_BATCH")) c->fl_batch = std::max(1, atoi(fb));
+  if (const char* fg = getenv("DM_FLOW_GRID")) c->fl_grid_force = std::max(0, atoi(fg));  // tests: tiny grids
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
     for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
       const int d = sp[i] >= 'a' ? sp[i] - 'a' + 10 : sp[i] - '0';
@@ -794,7 +865,8 @@ int dm_sync(dm_ctx* c) {
 
 int dm_set_large_path(dm_ctx* c, int mode) {
   DM_ENTER(c);
-  if (mode != DM_LARGE_CHAIN && mode != DM_LARGE_FUSED) return c->fail(DM_E_INVAL, "unknown large-path mode");
+  if (mode != DM_LARGE_CHAIN && mode != DM_LARGE_FUSED && mode != DM_LARGE_FLOW)
+    return c->fail(DM_E_INVAL, "unknown large-path mode");
   c->large_mode = mode;
   return DM_OK;
 }
@@ -1057,6 +1129,13 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                        (int32_t)c->h_fchunks.size(), c->fused_epoch, c->fused_spin_limit};
     DM_HIP(c, timed(KC_LARGE_FUSED, s_large,
                     [&] { return launch_large_fused(c->fused_G, p, c->fchunks.p, c->flarge.p, F, gl, gc, s_large); }),
+           "large-resource kernel");
+  } else if (nch > 0 && c->large_mode == DM_LARGE_FLOW && !general) {
+    c->fl_epoch = c->fl_epoch + 1 == 0 ? 1 : c->fl_epoch + 1;
+    const FlowState F{c->fl_tasks.p, c->chunks.p, c->large.p, c->fl_ticket.p, c->fl_sync.p, c->fl_part.p,
+                      c->fl_tot.p, c->pa_live.p, c->d_ferr, (int32_t)c->h_fl_tasks.size(), c->fl_epoch,
+                      c->fused_spin_limit, c->fl_batch};
+    DM_HIP(c, timed(KC_LARGE_FLOW, s_large, [&] { return launch_large_flow(p, F, c->fl_grid, gl, gc, s_large); }),
            "large-resource kernel");
   } else {
     const int nls = (int)c->h_large.size();
@@ -1956,7 +2035,7 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[8 + kNumBins];
+  int64_t v[11 + kNumBins];
   v[0] = (int64_t)c->h_packs.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
@@ -1966,7 +2045,10 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   v[5 + kNumBins] = (int64_t)c->h_fchunks.size();
   v[6 + kNumBins] = c->fused_max_chunks;
   v[7 + kNumBins] = c->fused_cap;
-  const int n = 8 + kNumBins;
+  v[8 + kNumBins] = (c->large_mode == DM_LARGE_FLOW && !c->h_chunks.empty()) ? 1 : 0;
+  v[9 + kNumBins] = c->fl_grid;
+  v[10 + kNumBins] = (int64_t)c->h_fl_tasks.size();
+  const int n = 11 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }

@@ -321,9 +321,16 @@ int dm_hier_status(dm_ctx* root, uint32_t* status, int n_servers);
  * the chunks of a resource exchange those totals in-launch (one HBM pass); used
  * only when every large resource has at most half as many chunks as the device
  * keeps resident, else the chain runs.  Results are bit-identical; dm_plan_info
- * reports which path a tick takes. */
+ * reports which path a tick takes.
+ * DM_LARGE_FLOW: the chain's phases as tasks of one persistent launch (a fixed grid
+ * takes listed tasks from a ticket counter; a task waits only for its resource's
+ * earlier phases, listed before it), so no launch boundaries and each phase's
+ * totals are reduced once per resource; no co-residency bound.  Ticks that may
+ * hold heterogeneous-subclient FairShare resources use the chain.  Results agree
+ * with the chain's within rounding (different reduction trees). */
 #define DM_LARGE_CHAIN 0
 #define DM_LARGE_FUSED 1
+#define DM_LARGE_FLOW 2
 int dm_set_large_path(dm_ctx* ctx, int mode);
 
 /* ---- profiling ---- */
@@ -334,7 +341,8 @@ int dm_reset_kernel_times(dm_ctx* ctx);
 /* plan summary of the loaded store: counts per dispatch bin (small packs, 64x1,
  * 256x1..256x16, large resources, large chunks, leases), then whether ticks use
  * the one-launch large path, its chunks, the most chunks of one resource and the
- * device's resident-workgroup bound */
+ * device's resident-workgroup bound, then whether large resources take the
+ * persistent path (DM_LARGE_FLOW), its grid and its listed tasks */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),

@@ -1,9 +1,11 @@
-"""Large resources (> 4096 rows): the five-launch chain (default; every chunk
-re-derives the resource's totals from the previous launch's partials) and the one-launch
-path (DM_LARGE_FUSED, dm_large.hip: rows resident in VGPRs, totals exchanged
-in-launch) against each other and against the oracle (SURVEY.md §8c bar, with the
-observed error reported).  Each path is deterministic; the two differ only in the
-rounding of their per-resource sums (different chunking and reduction trees)."""
+"""Large resources (> 4096 rows): the five-launch chain (every chunk re-derives the
+resource's totals from the previous launch's partials), the one-launch path
+(DM_LARGE_FUSED, dm_large.hip: rows resident in VGPRs, totals exchanged in-launch) and
+the persistent task-queue path (DM_LARGE_FLOW, dm_flow.hip: the chain's phases as
+listed tasks of one launch, totals reduced once per resource) against each other and
+against the oracle (SURVEY.md §8c bar, with the observed error reported).  Each path
+is deterministic; they differ only in the rounding of their per-resource sums
+(different chunking and reduction trees)."""
 import os
 
 import numpy as np
@@ -18,21 +20,23 @@ pytestmark = pytest.mark.gpu
 NOW = W.NOW_NS
 
 
-def _engine(G=None, fused=False):
+def _engine(G=None, fused=False, path=None, env=None):
     from doorman_amd.engine import Engine
-    old = os.environ.get("DM_FUSED_G")
+    env = dict(env or {})
     if G is not None:
-        os.environ["DM_FUSED_G"] = str(G)
+        env["DM_FUSED_G"] = str(G)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         e = Engine(0)
-        e.set_large_path(fused=fused)
+        e.set_large_path(fused=fused, path=path)
         return e
     finally:
-        if G is not None:
-            if old is None:
-                os.environ.pop("DM_FUSED_G")
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
             else:
-                os.environ["DM_FUSED_G"] = old
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -41,6 +45,13 @@ def pair():
     yield fused, chain
     fused.close()
     chain.close()
+
+
+@pytest.fixture(scope="module")
+def flow():
+    e = _engine(path="flow")
+    yield e
+    e.close()
 
 
 def _tick(eng, snap, **kw):
@@ -231,6 +242,144 @@ def test_fused_wait_that_gives_up_loses_the_store_until_reload():
                     call()
                 assert e.value.code == DM_E_STATE
         eng.set_large_path(fused=False)
+        a = _tick(eng, snap, writeback=True)
+        b = _tick(chain, snap, writeback=True)
+        for x, y in zip(a[:2], b[:2]):
+            assert x.tobytes() == y.tobytes()
+    finally:
+        eng.close()
+        chain.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("variant", ["uniform", "hetero", "edge", "recompute", "no_expiry", "learning"])
+def test_flow_matches_chain(pair, flow, seed, variant):
+    """The persistent path against the chain on the same snapshots as the fused path
+    (heterogeneous FairShare resources go to k_general either way)."""
+    chain = pair[1]
+    rng = np.random.default_rng(9000 + seed)
+    snap = snapshot_with_sizes(rng, large_sizes(rng), hetero=variant == "hetero", edge=variant == "edge",
+                               expired_frac=0.0 if variant == "no_expiry" else 0.05,
+                               learning_frac=0.5 if variant == "learning" else 0.1)
+    rec = variant == "recompute"
+    if rec:
+        for k in ("agg_count", "agg_sum_has", "agg_sum_wants"):
+            snap.pop(k)
+    a = _tick(flow, snap, recompute=rec)
+    assert flow.plan_info()["large_flow"] == 1
+    b = _tick(chain, snap, recompute=rec)
+    _same(snap, a, b, f"seed={seed} {variant}")
+    _deterministic(flow, snap, a, f"seed={seed} {variant}", recompute=rec)
+
+
+@pytest.mark.parametrize("grid", ["1", "3", "default"])
+@pytest.mark.parametrize("kinds", [(2,), (3,), (0, 1, 2, 3)])
+def test_flow_against_oracle(grid, kinds):
+    """The persistent path against the oracle, also drained by ONE workgroup and by
+    three (the task list alone orders the phases: no co-residency is assumed)."""
+    rng = np.random.default_rng(17 + len(kinds))
+    eng = _engine(path="flow", env={} if grid == "default" else {"DM_FLOW_GRID": grid})
+    try:
+        sizes = np.asarray([4097, 8192, 8193, 20000, 33333, 65537, 5000, 250000], dtype=np.int64)
+        snap = snapshot_with_sizes(rng, sizes, kinds=kinds, expired_frac=0.05)
+        gets, exp, res = _tick(eng, snap)
+        info = eng.plan_info()
+        assert info["large_flow"] == 1 and info["large_chunks"] == int(np.sum(-(-sizes // 2048)))
+        if grid != "default":
+            assert info["flow_grid"] == int(grid)
+        # pass A per chunk, round 1 per bundle of 8 chunks, round 2 and the map per chunk
+        nch = -(-sizes // 2048)
+        assert info["flow_tasks"] == int(3 * nch.sum() + np.sum(-(-nch // 8)))
+    finally:
+        eng.close()
+    ref = O.apportion(snap, NOW)
+    assert_leases_match(snap, gets, exp, ref, f"flow grid={grid}")
+    assert_resources_match(snap, res, ref, f"flow grid={grid}")
+    e = max_err(snap, gets, ref)
+    print(f"\nflow grid={grid} kinds={kinds}: max |got-ref|/max(|ref|, C_r/n_r) = {e:.3e} (bar 1e-9)")
+    assert e <= 1e-9
+
+
+def test_flow_writeback_sequence_matches_chain(pair, flow):
+    """Writeback ticks with rows lapsing between them (round 1 recomputed from the rows
+    where Clean releases subclients), synchronous and deferred-join asynchronous,
+    against the chain: the ticket counters, arrive counters and epoch-tagged flags are
+    reused launch after launch."""
+    chain = pair[1]
+    rng = np.random.default_rng(78)
+    snap = snapshot_with_sizes(rng, large_sizes(rng, n=20), kinds=(0, 1, 2, 3), expired_frac=0.02)
+    # explicit expiries from 10 s before the first tick (its Clean releases rows of
+    # most resources: round 1 recomputed) and lease lengths of 3-20 s (later ticks
+    # see whole resources lapse)
+    live = snap["expiry_ns"] != W.RELEASED
+    snap["expiry_ns"] = np.where(live, NOW + rng.integers(-10, 30, live.size) * W.NS, snap["expiry_ns"])
+    snap["lease_length_s"] = rng.integers(3, 21, len(snap["lease_length_s"])).astype(np.int64)
+    flow.load(snap)
+    chain.load(snap)
+    for i in range(6):
+        now = NOW + i * 5 * W.NS
+        for e in (flow, chain):
+            e.apportion(now, writeback=True, asynchronous=i % 2 == 1, defer_join=i % 2 == 1)
+            e.sync()
+        a = (*flow.leases(), flow.resources())
+        b = (*chain.leases(), chain.resources())
+        _same(snap, a, b, f"tick {i}")
+
+
+def test_flow_large_resources_at_c2(flow):
+    """configs[2]'s large resources (up to 1M rows) through the persistent path,
+    sampled against the oracle with the error reported."""
+    snap = W.c2()
+    flow.load(snap)
+    info = flow.plan_info()
+    assert info["large_flow"] == 1
+    flow.apportion(NOW)
+    gets, exp = flow.leases()
+    so = snap["seg_off"]
+    sample = np.asarray([0, 1, 2, 3, 10, 50, 121, 200, 243], dtype=np.int64)
+    sub = W.subset(snap, sample)
+    ref = O.apportion(sub, NOW)
+    rows = np.concatenate([np.arange(so[r], so[r + 1]) for r in sample])
+    assert_leases_match(sub, gets[rows], exp[rows], ref, "C2 large flow")
+    e = max_err(sub, gets[rows], ref)
+    print(f"C2 large resources (flow): max |got-ref|/max(|ref|, C_r/n_r) = {e:.3e} (bar 1e-9)")
+    assert e <= 1e-9
+
+
+def test_flow_wait_that_gives_up_fails_the_tick():
+    """A persistent-path wait that gives up (a zero spin bound) fails the tick with
+    DM_E_HIP and, after a writeback tick, loses the store until it is reloaded (as the
+    fused path); the reloaded store then ticks as the chain."""
+    from doorman_amd._lib import DM_E_HIP, DM_E_STATE
+    from doorman_amd._lib import DmError as DoormanError
+    rng = np.random.default_rng(79)
+    snap = snapshot_with_sizes(rng, np.array([60000, 70000, 50000, 45000], dtype=np.int64), hetero=False)
+    eng = _engine(path="flow", env={"DM_FUSED_SPIN_LIMIT": "0"})
+    chain = _engine()
+    try:
+        eng.load(snap)
+        before = eng.read_store()
+        failed = False
+        try:
+            eng.apportion(NOW)
+        except DoormanError as e:
+            assert e.code == DM_E_HIP
+            failed = True
+        after = eng.read_store()
+        for k in before:
+            assert before[k].tobytes() == after[k].tobytes(), k
+        if failed:
+            try:
+                eng.apportion(NOW, writeback=True)
+                lost = False
+            except DoormanError as e:
+                assert e.code == DM_E_HIP
+                lost = True
+            if lost:
+                with pytest.raises(DoormanError) as e:
+                    eng.read_store()
+                assert e.value.code == DM_E_STATE
+        eng.set_large_path(path="chain")
         a = _tick(eng, snap, writeback=True)
         b = _tick(chain, snap, writeback=True)
         for x, y in zip(a[:2], b[:2]):
