@@ -556,6 +556,12 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
 struct SegTot {
   AggA a;
   AggB b;
+  uint32_t pad[7];
+  // nonzero when some chunk's Clean released subclients this tick (pass A, atomicOr),
+  // i.e. round 1 must be recomputed; cleared by k_large_fin for the next tick.  With
+  // it zero, pass B's other chunks return at once and its first chunk leaves the
+  // speculative round-1 totals for C and the map (no O(chunks) re-reduction there)
+  uint32_t rel;
 };
 static_assert(sizeof(SegTot) <= kSegTotBytes, "SegTot slot");
 __device__ __forceinline__ SegTot* seg_tot(const Partials& P, int lseg) {
@@ -835,6 +841,7 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
   if (P.s_set && !rs.learning && rs.kind == 3) chunk_s_insert(P, ch.lseg, rw, a);  // heterogeneous FairShare
   if (threadIdx.x == 0) {
     const int c = blockIdx.x;
+    if (a.cnt != 0) atomicOr(&seg_tot(P, ch.lseg)->rel, 1u);
     if (spec) {
       P.b_x[c] = b.x;
       P.b_y[c] = b.y;
@@ -863,11 +870,18 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
     ps = cf.kind == 2;
   }
   const LargeSeg L = ls[ch.lseg];
+  const bool first = (int)blockIdx.x == L.chunk_begin;
+  const bool spec_ok = !p.recompute && seg_tot(P, ch.lseg)->rel == 0;  // pass A's speculative partials are exact
+  if (spec_ok && !first) return;
   const SegState st = seg_state<256>(p, P, L, lds);
-  if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->a = st.a;
+  if (threadIdx.x == 0 && first) seg_tot(P, ch.lseg)->a = st.a;
   const bool het = st.general && P.s_set;  // heterogeneous FairShare decided on the chain
   if ((st.general && !het) || st.rs.learning || st.rs.kind < 2) return;
-  if (!p.recompute && st.a.cnt == 0) return;  // pass A's speculative partials are exact
+  if (spec_ok) {  // the first chunk leaves the speculative round-1 totals (C and the map read them)
+    const AggB b = seg_b<256>(P, L, lds);
+    if (threadIdx.x == 0) seg_tot(P, ch.lseg)->b = b;
+    return;
+  }
   ChunkRows rw;
   load_chunk_w(p, P, ch, rw, ps || het);
   const double eq = st.rs.C / (double)st.cl.count;
@@ -918,8 +932,9 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
   if (st.general || st.rs.learning || st.rs.kind != 3) return;
 #pragma unroll
   for (int k = 0; k < kLR; ++k) rw.s[k] = st.a.smin;  // uniform subclients here
-  const AggB b = seg_b<256>(P, L, lds);
-  if (threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->b = b;
+  const bool spec_ok = !p.recompute && seg_tot(P, ch.lseg)->rel == 0;  // pass B's first chunk left b
+  const AggB b = spec_ok ? seg_tot(P, ch.lseg)->b : seg_b<256>(P, L, lds);
+  if (threadIdx.x == 0 && !spec_ok && (int)blockIdx.x == L.chunk_begin) seg_tot(P, ch.lseg)->b = b;
   const double eq = st.rs.C / (double)st.cl.count;
   const double s0 = (double)st.a.smin;
   const double Tu = (b.x / (double)b.i) * s0 + eq * s0;
@@ -965,7 +980,7 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   const double eq = C / (double)st.cl.count;
   AggB b{0.0, 0.0, 0};
   AggC c{0.0, 0};
-  if (ps) b = seg_b<256>(P, L, lds);
+  if (ps) b = (!p.recompute && seg_tot(P, ch.lseg)->rel == 0) ? seg_tot(P, ch.lseg)->b : seg_b<256>(P, L, lds);
   if (fs) {
     b = seg_tot(P, ch.lseg)->b;  // left by pass C
     c = seg_c<256>(P, L, lds);
@@ -1008,6 +1023,7 @@ __global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* 
                                                    int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<256> lds;
   const LargeSeg L = ls[blockIdx.x];
+  if (threadIdx.x == 0) seg_tot(P, blockIdx.x)->rel = 0;  // pass A of the next tick sets it again
   const SegState st = seg_state<256>(p, P, L, lds);
   if (st.general) {
     if (!P.s_set) {  // no heterogeneous path on the chain this tick: k_general decides it

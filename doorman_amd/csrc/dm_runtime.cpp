@@ -614,6 +614,8 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
   DM_HIP(c, c->pa_live.ensure(nc * 256), "partials");
   DM_HIP(c, c->p_tot.ensure(std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes), "partials");
+  DM_HIP(c, hipMemsetAsync(c->p_tot.p, 0, std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes, st),
+         "partials");  // SegTot::rel starts clear
   c->n_nonsmall = 0;
   for (int64_t r = 0; r < c->R; ++r)
     if (c->h_seg_off[r + 1] - c->h_seg_off[r] > kSmallMax) ++c->n_nonsmall;
