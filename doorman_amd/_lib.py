@@ -82,6 +82,7 @@ _SIGS = {
     "dm_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "dm_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_join": (ctypes.c_int, [ctypes.c_void_p]),
+    "dm_stream_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dm_store_update_wants_mask": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                                   ctypes.c_int64, ctypes.c_void_p]),
     "dm_store_load": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Snapshot)]),

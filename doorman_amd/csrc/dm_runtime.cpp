@@ -149,8 +149,65 @@ struct dm_ctx {
   int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (packs alone)
   hipStream_t aux[kAux] = {};
   hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
-  hipEvent_t ev_fork = nullptr, ev_join[kAux] = {};
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
+  // Cross-stream order between the context's streams (fork / join of a tick's work
+  // classes, the pipelined hierarchy's template slots, dm_stream_wait): an event
+  // recorded on the producing stream and waited on by the consuming one, or with
+  // DM_XS_VALUES=1 a rising sequence number written into a signal word
+  // (hipStreamWriteValue64) and waited for (hipStreamWaitValue64, >=).  Each hop
+  // costs the consuming queue ~12-20 us on the box either way: this ROCm runs the
+  // stream memory operations as blit kernels (__amd_rocclr_streamOps*, 3-5 us each
+  // plus a dispatch gap, tools/gpu_c3trace.sh), so events stay the default.  A wait
+  // on a token signalled on the waiting stream itself is skipped (stream order).
+  static constexpr int kTplSlots = 3;
+  enum : int {
+    XS_FORK = 0,
+    XS_JOIN0 = 1,                       // + aux stream
+    XS_READY0 = XS_JOIN0 + kAux,        // + template slot: the root round wrote it
+    XS_FREE0 = XS_READY0 + kTplSlots,   // + template slot: the ticks that read it are done
+    XS_LEAF = XS_FREE0 + kTplSlots,     // leaf stream -> the root round's stream
+    XS_ROOT,                            // root stream -> the leaf (unpipelined, separate streams)
+    XS_EXT,                             // dm_stream_wait
+    XS_N
+  };
+  struct XsTok {
+    int w = 0;
+    uint64_t v = 0;
+    hipStream_t s = nullptr;  // the stream it was signalled on
+    bool rec = false;         // recorded (else the wait records on s first: lazy signal)
+  };
+  bool xs_events = true;
+  uint64_t* xs_word[XS_N] = {};  // signal memory, one word per allocation
+  uint64_t xs_seq[XS_N] = {};
+  hipEvent_t xs_ev[XS_N] = {};
+  hipError_t xs_signal(int w, hipStream_t s, XsTok* tok) {
+    tok->w = w;
+    tok->s = s;
+    tok->rec = true;
+    if (xs_events) return hipEventRecord(xs_ev[w], s);
+    tok->v = ++xs_seq[w];
+    return hipStreamWriteValue64(s, xs_word[w], tok->v, 0);
+  }
+  // A signal recorded only if a wait on another stream needs it, then at that wait:
+  // it orders after everything the signalling stream holds by then (never less than
+  // at signal time), and a same-stream consumer costs nothing.
+  void xs_signal_lazy(int w, hipStream_t s, XsTok* tok) {
+    tok->w = w;
+    tok->s = s;
+    tok->rec = false;
+  }
+  hipError_t xs_wait(const XsTok& tok, hipStream_t s) {
+    if (tok.s == s) return hipSuccess;
+    if (!tok.rec) return xs_order(tok.w, tok.s, s);
+    if (xs_events) return hipStreamWaitEvent(s, xs_ev[tok.w], 0);
+    return hipStreamWaitValue64(s, xs_word[tok.w], tok.v, hipStreamWaitValueGte, ~0ull);
+  }
+  hipError_t xs_order(int w, hipStream_t from, hipStream_t to) {
+    if (from == to) return hipSuccess;
+    XsTok t;
+    hipError_t e = xs_signal(w, from, &t);
+    return e == hipSuccess ? xs_wait(t, to) : e;
+  }
   std::string err;
 
   int64_t R = 0, N = 0;
@@ -190,8 +247,7 @@ struct dm_ctx {
     if (!aux_pending) return hipSuccess;
     aux_pending = false;
     for (int i = 0; i < kAux; ++i) {
-      hipError_t e = hipEventRecord(ev_join[i], aux[i]);
-      if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join[i], 0);
+      hipError_t e = xs_order(XS_JOIN0 + i, aux[i], stream);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -301,13 +357,12 @@ struct dm_ctx {
   // leaf side: pipelined templates (dm_hier_pipeline).  An exchange stages this
   // leaf's new templates in a free slot; the leaf's ticks take the staged templates
   // of the exchanges enqueued before the previous tick (one tick of lag).
-  static constexpr int kTplSlots = 3;
   bool tpl_pipe = false;
   DBuf<ResCfg> tpl_cfg[kTplSlots];
   DBuf<ResCold> tpl_cold[kTplSlots];
-  hipEvent_t ev_tpl_ready[kTplSlots] = {};  // root stream: the slot's templates are written
-  hipEvent_t ev_tpl_free[kTplSlots] = {};   // leaf stream: the ticks that read the slot are done
-  bool tpl_free_rec[kTplSlots] = {};        // ev_tpl_free holds a record
+  XsTok tpl_ready[kTplSlots];        // root stream: the slot's templates are written
+  XsTok tpl_free[kTplSlots];         // leaf stream: the ticks that read the slot are done
+  bool tpl_free_rec[kTplSlots] = {};  // tpl_free holds a signal
   struct Staged {
     int slot;
     int64_t tag;  // leaf ticks issued before the exchange was enqueued
@@ -697,6 +752,37 @@ int dm_device_count(int* out) {
   return DM_OK;
 }
 
+// The context's cross-stream order (dm_ctx::xs_signal): events, or with DM_XS_VALUES=1
+// signal-memory words, zeroed (events when the device cannot wait on stream values).
+static hipError_t xs_setup(dm_ctx* c) {
+  if (const char* xv = getenv("DM_XS_VALUES")) c->xs_events = atoi(xv) == 0;
+  int can = 0;
+  if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, c->device) != hipSuccess || !can)
+    c->xs_events = true;
+  (void)hipGetLastError();
+  for (int i = 0; i < dm_ctx::XS_N && !c->xs_events; ++i) {
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess ||
+        hipStreamWriteValue64(c->stream, p, 0, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      if (p) (void)hipFree(p);
+      c->xs_events = true;
+      break;
+    }
+    c->xs_word[i] = (uint64_t*)p;
+  }
+  if (c->xs_events) {
+    for (int i = 0; i < dm_ctx::XS_N; ++i) {
+      if (c->xs_word[i]) (void)hipFree(c->xs_word[i]);
+      c->xs_word[i] = nullptr;
+      hipError_t e = hipEventCreateWithFlags(&c->xs_ev[i], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  return hipStreamSynchronize(c->stream);
+}
+
 int dm_create(int device, dm_ctx** out) {
   if (!out) return DM_E_INVAL;
   *out = nullptr;
@@ -786,15 +872,10 @@ int dm_create(int device, dm_ctx** out) {
       (void)hipGetLastError();
       e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
     }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
-  for (int i = 0; i < dm_ctx::kTplSlots && e == hipSuccess; ++i) {
-    e = hipEventCreateWithFlags(&c->ev_tpl_ready[i], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_tpl_free[i], hipEventDisableTiming);
-  }
+  if (e == hipSuccess) e = xs_setup(c);
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
@@ -822,16 +903,14 @@ void dm_destroy(dm_ctx* c) {
       (void)hipStreamSynchronize(c->aux[i]);
       (void)hipStreamDestroy(c->aux[i]);
     }
-    if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
   }
   if (c->cpy) {
     (void)hipStreamSynchronize(c->cpy);
     (void)hipStreamDestroy(c->cpy);
   }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  for (int i = 0; i < dm_ctx::kTplSlots; ++i) {
-    if (c->ev_tpl_ready[i]) (void)hipEventDestroy(c->ev_tpl_ready[i]);
-    if (c->ev_tpl_free[i]) (void)hipEventDestroy(c->ev_tpl_free[i]);
+  for (int i = 0; i < dm_ctx::XS_N; ++i) {
+    if (c->xs_ev[i]) (void)hipEventDestroy(c->xs_ev[i]);
+    if (c->xs_word[i]) (void)hipFree(c->xs_word[i]);
   }
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
@@ -855,6 +934,13 @@ void* dm_get_stream(dm_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int dm_join(dm_ctx* c) {
   DM_ENTER(c);
+  return DM_OK;
+}
+
+int dm_stream_wait(dm_ctx* c, void* s) {
+  DM_ENTER(c);
+  if (!s) return c->fail(DM_E_INVAL, "null stream");
+  DM_HIP(c, c->xs_order(dm_ctx::XS_EXT, c->stream, (hipStream_t)s), "stream order");
   return DM_OK;
 }
 
@@ -1019,12 +1105,12 @@ static int commit_templates(dm_ctx* c) {
   c->tpl_pending.erase(c->tpl_pending.begin(), c->tpl_pending.begin() + (ptrdiff_t)n);
   if (take < 0) return DM_OK;
   DM_HIP(c, c->join_aux(), "join");  // deferred class work also read the old templates
-  DM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_tpl_ready[take], 0), "staged templates");
+  DM_HIP(c, c->xs_wait(c->tpl_ready[take], c->stream), "staged templates");
   c->main_dirty = true;  // the class streams fork after the wait
   std::swap(c->cfg, c->tpl_cfg[take]);
   std::swap(c->cold, c->tpl_cold[take]);
   // the old templates (now in slot `take`) are free after the ticks already enqueued
-  DM_HIP(c, hipEventRecord(c->ev_tpl_free[take], c->stream), "template slot");
+  c->xs_signal_lazy(dm_ctx::XS_FREE0 + take, c->stream, &c->tpl_free[take]);  // the next exchange into it waits
   c->tpl_free_rec[take] = true;
   c->tpl_free_slots.push_back(take);
   return DM_OK;
@@ -1121,8 +1207,9 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     DM_HIP(c, c->join_aux(), "join");
     c->main_dirty = true;
   } else if (c->main_dirty) {  // class streams wait for what the context stream holds
-    DM_HIP(c, hipEventRecord(c->ev_fork, st), "fork");
-    for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork");
+    dm_ctx::XsTok fk;
+    DM_HIP(c, c->xs_signal(dm_ctx::XS_FORK, st, &fk), "fork");
+    for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, c->xs_wait(fk, c->aux[i]), "fork");
     c->main_dirty = false;
   }
   if (nch > 0 && c->use_fused()) {
@@ -1874,7 +1961,7 @@ int dm_hier_pipeline(dm_ctx* leaf, int on) {
   if (!leaf->cfg_loaded) return leaf->fail(DM_E_STATE, "load the leaf's configuration first");
   if (!on && leaf->tpl_pipe && !leaf->tpl_pending.empty()) {  // take the newest staged templates now
     const int take = leaf->tpl_pending.back().slot;
-    DM_HIP(leaf, hipStreamWaitEvent(leaf->stream, leaf->ev_tpl_ready[take], 0), "staged templates");
+    DM_HIP(leaf, leaf->xs_wait(leaf->tpl_ready[take], leaf->stream), "staged templates");
     std::swap(leaf->cfg, leaf->tpl_cfg[take]);
     std::swap(leaf->cold, leaf->tpl_cold[take]);
   }
@@ -1923,8 +2010,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   root->hier_servers = n_servers;
   const bool same = root->stream == leaf->stream;
   if (!same) {  // the root round after the leaf's prior work (its publish)
-    DM_HIP(root, hipEventRecord(leaf->ev_fork, leaf->stream), "leaf->root order");
-    DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_fork, 0), "leaf->root order");
+    DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->root order");
   }
   ResCfg* tcfg = leaf->cfg.p;
   ResCold* tcold = leaf->cold.p;
@@ -1938,7 +2024,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     DM_HIP(root, leaf->tpl_cfg[slot].ensure((size_t)leaf->R), "template slot");
     DM_HIP(root, leaf->tpl_cold[slot].ensure((size_t)leaf->R), "template slot");
     if (leaf->tpl_free_rec[slot])  // the ticks that read the slot's old templates are done
-      DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->ev_tpl_free[slot], 0), "template slot");
+      DM_HIP(root, leaf->xs_wait(leaf->tpl_free[slot], root->stream), "template slot");
     tcfg = leaf->tpl_cfg[slot].p;
     tcold = leaf->tpl_cold[slot].p;
     if (!leaf->tpl_pending.empty()) {  // a rejected round keeps the newest staged templates
@@ -1981,11 +2067,14 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
          "hierarchy root tick");
   if (slot >= 0) {
     leaf->tpl_free_slots.erase(leaf->tpl_free_slots.begin());
-    DM_HIP(root, hipEventRecord(leaf->ev_tpl_ready[slot], root->stream), "staged templates");
+    if (same)  // the leaf's ticks follow in stream order
+      leaf->xs_signal_lazy(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot]);
+    else
+      DM_HIP(root, leaf->xs_signal(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot]),
+             "staged templates");
     leaf->tpl_pending.push_back(dm_ctx::Staged{slot, leaf->ticks_issued});
   } else if (!same) {  // the leaf's next tick after its new templates
-    DM_HIP(root, hipEventRecord(root->ev_join[0], root->stream), "root->leaf order");
-    DM_HIP(root, hipStreamWaitEvent(leaf->stream, root->ev_join[0], 0), "root->leaf order");
+    DM_HIP(root, leaf->xs_order(dm_ctx::XS_ROOT, root->stream, leaf->stream), "root->leaf order");
   }
   root->maybe_general = true;  // rows carry heterogeneous subclient counts
   root->all_sub_one = false;

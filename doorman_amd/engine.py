@@ -91,6 +91,10 @@ class Engine:
         """dm_join: order deferred ticks before later work on the context stream."""
         self._chk(self._L.dm_join(self._ctx))
 
+    def stream_wait(self, hip_stream: int):
+        """dm_stream_wait: order hip_stream after the work enqueued so far on this engine."""
+        self._chk(self._L.dm_stream_wait(self._ctx, ctypes.c_void_p(hip_stream)))
+
     # -- LeaseStore --
     def load(self, snap: dict):
         """NewLeaseStore + Assign of every row (store.go:114,153) and the resolved config."""

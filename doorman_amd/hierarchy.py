@@ -124,8 +124,13 @@ class HierarchicalTick:
         # select (NULL restores the context's own stream) and which does not order the
         # library's non-blocking streams.  Unpipelined: one stream, so publish ->
         # all-gather -> root -> templates -> leaf tick are ordered without host syncs.
+        # Pipelined with G > 1, the exchange (all-gather + root round) gets a stream of its
+        # own so the collective overlaps the next leaf tick.  With one server there is no
+        # collective and the root round (~10 us) is cheaper than the two cross-queue hops
+        # a second stream costs per step (~20 us of idle GPU each): the
+        # exchange then runs on the leaf's stream, still one tick of lag (staged slots).
         self.stream = torch.cuda.Stream(device=dev)
-        self.xstream = torch.cuda.Stream(device=dev) if pipelined else self.stream
+        self.xstream = torch.cuda.Stream(device=dev) if pipelined and self.G > 1 else self.stream
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1 if pipelined else 0), leaf._ctx, leaf._L)
@@ -141,10 +146,8 @@ class HierarchicalTick:
         totals, gathered = self.totals[k], self.gathered[k]
         if not self.pipelined:
             self.leaf.publish_totals(totals.data_ptr())
-        else:
-            ev = self.torch.cuda.Event()
-            ev.record(self.stream)
-            self.xstream.wait_event(ev)
+        else:  # the exchange stream after the leaf tick that published the block
+            self.leaf.stream_wait(self.xstream.cuda_stream)
         if self.G > 1:
             with self.torch.cuda.stream(self.xstream):  # the collective orders with the exchange stream
                 self.gather(totals, gathered)

@@ -152,6 +152,13 @@ int dm_sync(dm_ctx* ctx);
 /* Order every deferred tick (DM_DEFER_JOIN) before later work on the context stream,
    without waiting on the host. */
 int dm_join(dm_ctx* ctx);
+/* Order hip_stream (any stream of the context's device, e.g. a collective's) after the
+   work enqueued so far on the context, deferred tick work included, without waiting on
+   the host: a stream memory write on the context stream and a wait for it on
+   hip_stream.  An event record + hipStreamWaitEvent does the same at several times the
+   GPU-side latency per hop.  Used by the pipelined hierarchy before its
+   all-gather (doorman_amd/hierarchy.py). */
+int dm_stream_wait(dm_ctx* ctx, void* hip_stream);
 
 /* ---- LeaseStore: device-resident columnar table ---- */
 int dm_store_load(dm_ctx* ctx, const dm_snapshot* snap);

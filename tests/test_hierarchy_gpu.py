@@ -567,3 +567,41 @@ def test_publish_ring_matches_publish_totals():
         e.sync()
         for t, b in zip(ring, before):
             assert t.cpu().numpy().tobytes() == b.tobytes()
+
+
+def test_stream_wait_orders_a_foreign_stream_after_the_tick():
+    """dm_stream_wait (stream memory write + wait, not events): a torch stream that
+    snapshots the published block right after dm_stream_wait sees the tick's block,
+    never the previous one -- ticks forked over the auxiliary streams with deferred
+    joins (DM_DEFER_JOIN), wants changed between ticks so every block differs, and a
+    store big enough (8M leases) that an unordered copy would overtake the tick."""
+    import ctypes
+    import torch
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    L = _lib.lib()
+    sizes = np.concatenate([np.full(7000, 1000), np.full(200, 5000), np.full(2000, 40), np.full(1, 50_000)])
+    N, R = int(sizes.sum()), len(sizes)
+    snap = W.make_snapshot(sizes, np.ones(N), np.zeros(N), 1, np.full(N, NOW + 600 * W.NS), W.FAIR_SHARE, 1e6,
+                           300, 5)
+    ring = [torch.zeros((R + 1, 2), dtype=torch.float64, device="cuda") for _ in range(3)]
+    xs = torch.cuda.Stream()
+    with Engine(0) as e:
+        e.load(snap)
+        ptrs = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ring])
+        _lib.check(L.dm_publish_ring(e._ctx, 3, ptrs), e._ctx)
+        shots, vals = [], []
+        for k in range(6):
+            v = 1.0 + k
+            e.update_wants(np.arange(N, dtype=np.int64), np.full(N, v))
+            e.apportion(NOW + k * W.NS, writeback=True, asynchronous=True, defer_join=True)
+            e.stream_wait(xs.cuda_stream)
+            with torch.cuda.stream(xs):
+                shots.append(ring[k % 3].clone())
+            vals.append(v)
+        e.sync()
+        torch.cuda.synchronize()
+    for k, (s, v) in enumerate(zip(shots, vals)):
+        got = s.cpu().numpy()[1:, 0]
+        assert np.array_equal(got, sizes * v), f"tick {k}: block of another tick"
