@@ -276,7 +276,9 @@ __global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevPa
 // one small launch).  qcnt is a two-slot ring: this tick's count in qcnt[par], and
 // k_block_rest clears qcnt[par ^ 1] for the next tick (stream order); host_count
 // (host-mapped) tells the host how many items went to the queue (its choice of
-// split or mixed).
+// split or mixed), written only when the count differs from the last one written
+// (qcnt[2]): a system-scope store to host memory keeps an otherwise empty launch
+// alive ~2 us longer, every tick of a dense store.
 template <int G, int R>
 __global__ __launch_bounds__(G) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
                                                    int32_t* queue, int32_t* qcnt, int par,
@@ -300,7 +302,10 @@ __global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restr
   const int count = qcnt[par];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     qcnt[par ^ 1] = 0;
-    if (host_count) __hip_atomic_store(host_count, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (host_count && qcnt[2] != count) {
+      __hip_atomic_store(host_count, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      qcnt[2] = count;
+    }
   }
   for (int q = blockIdx.x; q < count; q += gridDim.x) {
     const int idx = queue[q];

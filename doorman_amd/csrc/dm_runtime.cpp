@@ -632,8 +632,8 @@ static int upload_plan(dm_ctx* c) {
     c->dq_skip[i] = 0;
     const size_t nb = std::max<size_t>(c->h_bins[3 + i].size(), 1);
     DM_HIP(c, c->dq_list[i].ensure(nb), "dense split queue");
-    DM_HIP(c, c->dq_cnt[i].ensure(2), "dense split queue");
-    DM_HIP(c, hipMemsetAsync(c->dq_cnt[i].p, 0, 2 * sizeof(int32_t), st), "dense split queue");
+    DM_HIP(c, c->dq_cnt[i].ensure(3), "dense split queue");  // two-slot count + the last count told the host
+    DM_HIP(c, hipMemsetAsync(c->dq_cnt[i].p, 0, 3 * sizeof(int32_t), st), "dense split queue");
     c->dq_par[i] = 0;
   }
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);

@@ -387,3 +387,58 @@ def test_flow_wait_that_gives_up_fails_the_tick():
     finally:
         eng.close()
         chain.close()
+
+
+def _store_as_snapshot(snap, eng):
+    """The device store as it now stands, as an oracle snapshot (running sums included)."""
+    st, res = eng.read_store(), eng.resources(safe=False)
+    s = dict(snap)
+    s.update(has=st["has"], wants=st["wants"], subclients=st["subclients"], expiry_ns=st["expiry_ns"],
+             agg_count=res["count"], agg_sum_has=res["sum_has"], agg_sum_wants=res["sum_wants"])
+    return s
+
+
+def test_large_writeback_ticks_against_oracle():
+    """Writeback ticks on large FairShare / ProportionalShare resources (the chain's
+    speculative round 1 and the per-resource totals it leaves in SegTot reused tick
+    after tick), each checked against the oracle on the device store as it stood
+    before it.  Between ticks the wants change by nothing, by a little and by a lot,
+    one resource loses its wantExtra clients entirely (T not finite), and one tick
+    follows releases."""
+    rng = np.random.default_rng(4242)
+    sizes = np.asarray([4097, 6000, 8192, 20000, 65537, 150000], dtype=np.int64)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(3, 3, 3, 2), expired_frac=0.0, learning_frac=0.0)
+    snap["expiry_ns"] = np.full(len(snap["wants"]), NOW + 3600 * W.NS, np.int64)
+    so = snap["seg_off"]
+    N = len(snap["wants"])
+    eng = _engine()
+    try:
+        eng.load(snap)
+        base = np.asarray(snap["wants"], dtype=np.float64).copy()
+        plan = ["same", "same", "small", "same", "large", "same", "zero", "same", "release", "same"]
+        worst = 0.0
+        for i, step in enumerate(plan):
+            now = NOW + i * 5 * W.NS
+            if step == "small":
+                w = base * (1.0 + 1e-7 * rng.standard_normal(N))
+                eng.update_wants(np.arange(N, dtype=np.int64), w)
+            elif step == "large":
+                w = base * rng.uniform(0.5, 2.0, N)
+                eng.update_wants(np.arange(N, dtype=np.int64), w)
+            elif step == "zero":  # resource 1 wants nothing: no wantExtra clients, T not finite
+                rows = np.arange(so[1], so[2], dtype=np.int64)
+                eng.update_wants(rows, np.zeros(len(rows)))
+            elif step == "release":
+                eng.release(rng.choice(N, 500, replace=False).astype(np.int64))
+            cur = _store_as_snapshot(snap, eng)
+            ref = O.apportion(cur, now)
+            eng.apportion(now, writeback=True)
+            st = eng.read_store()
+            live = ref["expiry_ns"] != W.RELEASED
+            gets = np.where(live, st["has"], 0.0)
+            assert float_close(gets, np.where(live, ref["gets"], 0.0), row_capacity(cur)).all(), f"tick {i} ({step})"
+            worst = max(worst, max_err(cur, gets, ref))
+        print(f"\nlarge writeback ticks: max |got-ref|/max(|ref|, C_r/n_r) over {len(plan)} ticks = {worst:.3e}")
+        assert worst <= 1e-9
+    finally:
+        eng.close()
