@@ -162,6 +162,24 @@ __device__ __forceinline__ T group_reduce(T v, Op op, T* lds) {
   }
 }
 
+// As group_reduce, but only thread 0 combines the waves' totals: the result is
+// defined in thread 0 only (partials that one thread stores).  The other threads skip
+// the LDS reads and the combine; the slots are written once (no trailing barrier).
+template <int G, typename T, typename Op>
+__device__ __forceinline__ T group_reduce_t0(T v, Op op, T* lds) {
+  static_assert(G >= 128, "workgroups of two or more waves");
+  v = wave_reduce_g<64>(v, op);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T r = lds[0];
+#pragma unroll
+    for (int i = 1; i < G / 64; ++i) r = op(r, lds[i]);
+    v = r;
+  }
+  return v;
+}
+
 struct AggR {  // every row: the store's sums rebuilt by Assign (recompute mode)
   long long cnt;
   double h;

@@ -664,7 +664,8 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     r.rel |= (sub_released(sr[k]) ? 1u : 0u) << k;
     r.s[k] = sub_value(sr[k]);
   }
-  const unsigned need_h = p.recompute ? r.valid : (r.valid & ~r.live);
+  // a row already marked released holds has 0 (every path that marks one zeroes it)
+  const unsigned need_h = p.recompute ? r.valid : (r.valid & ~r.live & ~r.rel);
   if (__any(need_h != 0)) {
 #pragma unroll
     for (int k = 0; k < kLR; ++k)
@@ -689,13 +690,19 @@ __device__ __forceinline__ void load_chunk_w(const DevParams& p, const Partials&
   // for each row-block before issuing the next, eight memory latencies per chunk
   const int n = ch.nrows;
   int sr[kLR];
+  // wants / has first, subclients after: with_sub comes from the resource's config
+  // (ProportionalShare), which need not have arrived for the first loads to leave
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
     const unsigned u = (unsigned)(i < n ? i : n - 1);
     r.w[k] = *col_at(wb, u);
     r.h[k] = with_has ? *col_at(hb, u) : 0.0;
-    sr[k] = with_sub ? *col_at(sb, u) : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    const int i = k * 256 + threadIdx.x;
+    sr[k] = with_sub ? *col_at(sb, (unsigned)(i < n ? i : n - 1)) : 0;
   }
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
@@ -839,9 +846,12 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
   }
   {
     const AggR all_part = a.all;
-    a = group_reduce<256>(a, OpA(), lds.a);
-    if (p.recompute) a.all = group_reduce<256>(all_part, OpR(), lds.r);
-    if (spec) b = group_reduce<256>(b, OpB(), lds.b);
+    if (P.s_set)  // every thread reads the chunk's count range (chunk_s_insert)
+      a = group_reduce<256>(a, OpA(), lds.a);
+    else
+      a = group_reduce_t0<256>(a, OpA(), lds.a);
+    if (p.recompute) a.all = group_reduce_t0<256>(all_part, OpR(), lds.r);
+    if (spec) b = group_reduce_t0<256>(b, OpB(), lds.b);
   }
   if (P.s_set && !rs.learning && rs.kind == 3) chunk_s_insert(P, ch.lseg, rw, a);  // heterogeneous FairShare
   if (threadIdx.x == 0) {
@@ -868,16 +878,18 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
                                                  const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
+  // most chunks leave here: their resource's round 1 is exact from pass A and they
+  // are not its first chunk (no config load on that path)
+  const LargeSeg L = ls[ch.lseg];
+  const bool first = (int)blockIdx.x == L.chunk_begin;
+  const bool spec_ok = !p.recompute && seg_tot(P, ch.lseg)->rel == 0;  // pass A's speculative partials are exact
+  if (spec_ok && !first) return;
   bool ps;
   {  // only ProportionalShare / FairShare outside learning mode need this pass
     const ResCfg cf = p.cfg[ch.seg];
     if (cf.learning_end_ns > p.now || cf.kind < 2) return;
     ps = cf.kind == 2;
   }
-  const LargeSeg L = ls[ch.lseg];
-  const bool first = (int)blockIdx.x == L.chunk_begin;
-  const bool spec_ok = !p.recompute && seg_tot(P, ch.lseg)->rel == 0;  // pass A's speculative partials are exact
-  if (spec_ok && !first) return;
   const SegState st = seg_state<256>(p, P, L, lds);
   if (threadIdx.x == 0 && first) seg_tot(P, ch.lseg)->a = st.a;
   const bool het = st.general && P.s_set;  // heterogeneous FairShare decided on the chain
@@ -914,7 +926,7 @@ __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __res
         b.i += s;
     }
   }
-  b = group_reduce<256>(b, OpB(), lds.b);
+  b = group_reduce_t0<256>(b, OpB(), lds.b);
   if (threadIdx.x == 0) {
     P.b_x[blockIdx.x] = b.x;
     P.b_y[blockIdx.x] = b.y;
@@ -955,7 +967,7 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
     else if (w > Tu)
       c.sgt += s;
   }
-  c = group_reduce<256>(c, OpC(), lds.c);
+  c = group_reduce_t0<256>(c, OpC(), lds.c);
   if (threadIdx.x == 0) {
     P.c_ee[blockIdx.x] = c.ee;
     P.c_sgt[blockIdx.x] = c.sgt;
@@ -1020,7 +1032,7 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     put_live(p, ch.row0, u, g, rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
     delta.v += g - h;
   }
-  delta = group_reduce<256>(delta, OpSumD(), lds.d);
+  delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
   if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
 }
 
