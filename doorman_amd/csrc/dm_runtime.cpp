@@ -152,13 +152,15 @@ struct dm_ctx {
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
   // Cross-stream order between the context's streams (fork / join of a tick's work
   // classes, the pipelined hierarchy's template slots, dm_stream_wait): an event
-  // recorded on the producing stream and waited on by the consuming one, or with
-  // DM_XS_VALUES=1 a rising sequence number written into a signal word
-  // (hipStreamWriteValue64) and waited for (hipStreamWaitValue64, >=).  Each hop
-  // costs the consuming queue ~12-20 us on the box either way: this ROCm runs the
-  // stream memory operations as blit kernels (__amd_rocclr_streamOps*, 3-5 us each
-  // plus a dispatch gap, tools/gpu_c3trace.sh), so events stay the default.  A wait
-  // on a token signalled on the waiting stream itself is skipped (stream order).
+  // recorded on the producing stream and waited on by the consuming one, or a rising
+  // sequence number written into a signal word (hipStreamWriteValue64) and waited for
+  // (hipStreamWaitValue64, >=).  An event wait idles the consuming queue ~12-20 us on
+  // the box (tools/xs_probe.py); this ROCm runs the stream memory operations as blit
+  // kernels (__amd_rocclr_streamOps*, 3-5 us each plus a dispatch gap,
+  // tools/gpu_c3trace.sh) and measured no cheaper per step.  Events by default;
+  // DM_XS_VALUES=1 every hop as values, DM_XS_READY_VALUE=1 only the staged templates'
+  // hop.  A wait on a token signalled on the waiting stream itself is skipped (stream
+  // order).
   static constexpr int kTplSlots = 3;
   enum : int {
     XS_FORK = 0,
@@ -175,16 +177,24 @@ struct dm_ctx {
     uint64_t v = 0;
     hipStream_t s = nullptr;  // the stream it was signalled on
     bool rec = false;         // recorded (else the wait records on s first: lazy signal)
+    bool val = false;         // a stream-memory signal (else an event)
   };
-  bool xs_events = true;
+  bool xs_values = false;      // every token as stream memory (DM_XS_VALUES=1)
+  bool xs_can_value = false;   // signal words allocated
+  // the staged templates' hop -- the only one a pipelined leaf tick waits on -- as
+  // stream memory (DM_XS_READY_VALUE=1).  Off: with the exchange on a second stream the
+  // C3 step took 455.5 us with it against 451.6 us with an event (one stream: 446 us;
+  // tools/gpu_xs2.sh), the wait kernel's dispatch costing what the barrier did
+  bool xs_ready_value = false;
   uint64_t* xs_word[XS_N] = {};  // signal memory, one word per allocation
   uint64_t xs_seq[XS_N] = {};
   hipEvent_t xs_ev[XS_N] = {};
-  hipError_t xs_signal(int w, hipStream_t s, XsTok* tok) {
+  hipError_t xs_signal(int w, hipStream_t s, XsTok* tok, bool value = false) {
     tok->w = w;
     tok->s = s;
     tok->rec = true;
-    if (xs_events) return hipEventRecord(xs_ev[w], s);
+    tok->val = xs_can_value && (value || xs_values);
+    if (!tok->val) return hipEventRecord(xs_ev[w], s);
     tok->v = ++xs_seq[w];
     return hipStreamWriteValue64(s, xs_word[w], tok->v, 0);
   }
@@ -195,11 +205,12 @@ struct dm_ctx {
     tok->w = w;
     tok->s = s;
     tok->rec = false;
+    tok->val = false;
   }
   hipError_t xs_wait(const XsTok& tok, hipStream_t s) {
     if (tok.s == s) return hipSuccess;
     if (!tok.rec) return xs_order(tok.w, tok.s, s);
-    if (xs_events) return hipStreamWaitEvent(s, xs_ev[tok.w], 0);
+    if (!tok.val) return hipStreamWaitEvent(s, xs_ev[tok.w], 0);
     return hipStreamWaitValue64(s, xs_word[tok.w], tok.v, hipStreamWaitValueGte, ~0ull);
   }
   hipError_t xs_order(int w, hipStream_t from, hipStream_t to) {
@@ -755,31 +766,32 @@ int dm_device_count(int* out) {
 // The context's cross-stream order (dm_ctx::xs_signal): events, or with DM_XS_VALUES=1
 // signal-memory words, zeroed (events when the device cannot wait on stream values).
 static hipError_t xs_setup(dm_ctx* c) {
-  if (const char* xv = getenv("DM_XS_VALUES")) c->xs_events = atoi(xv) == 0;
+  if (const char* xv = getenv("DM_XS_VALUES")) c->xs_values = atoi(xv) != 0;
+  if (const char* xr = getenv("DM_XS_READY_VALUE")) c->xs_ready_value = atoi(xr) != 0;
+  for (int i = 0; i < dm_ctx::XS_N; ++i) {
+    hipError_t e = hipEventCreateWithFlags(&c->xs_ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
   int can = 0;
-  if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, c->device) != hipSuccess || !can)
-    c->xs_events = true;
-  (void)hipGetLastError();
-  for (int i = 0; i < dm_ctx::XS_N && !c->xs_events; ++i) {
+  if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, c->device) != hipSuccess || !can) {
+    (void)hipGetLastError();
+    return hipSuccess;  // events only
+  }
+  for (int i = 0; i < dm_ctx::XS_N; ++i) {
     void* p = nullptr;
     if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess ||
         hipStreamWriteValue64(c->stream, p, 0, 0) != hipSuccess) {
       (void)hipGetLastError();
       if (p) (void)hipFree(p);
-      c->xs_events = true;
-      break;
+      for (int j = 0; j < i; ++j) {
+        (void)hipFree(c->xs_word[j]);
+        c->xs_word[j] = nullptr;
+      }
+      return hipStreamSynchronize(c->stream);  // events only
     }
     c->xs_word[i] = (uint64_t*)p;
   }
-  if (c->xs_events) {
-    for (int i = 0; i < dm_ctx::XS_N; ++i) {
-      if (c->xs_word[i]) (void)hipFree(c->xs_word[i]);
-      c->xs_word[i] = nullptr;
-      hipError_t e = hipEventCreateWithFlags(&c->xs_ev[i], hipEventDisableTiming);
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
+  c->xs_can_value = true;
   return hipStreamSynchronize(c->stream);
 }
 
@@ -2070,7 +2082,8 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     if (same)  // the leaf's ticks follow in stream order
       leaf->xs_signal_lazy(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot]);
     else
-      DM_HIP(root, leaf->xs_signal(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot]),
+      DM_HIP(root,
+             leaf->xs_signal(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot], leaf->xs_ready_value),
              "staged templates");
     leaf->tpl_pending.push_back(dm_ctx::Staged{slot, leaf->ticks_issued});
   } else if (!same) {  // the leaf's next tick after its new templates

@@ -22,6 +22,7 @@ doorman_amd so the HIP library binds to torch's HIP runtime.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -130,7 +131,10 @@ class HierarchicalTick:
         # a second stream costs per step (~20 us of idle GPU each): the
         # exchange then runs on the leaf's stream, still one tick of lag (staged slots).
         self.stream = torch.cuda.Stream(device=dev)
-        self.xstream = torch.cuda.Stream(device=dev) if pipelined and self.G > 1 else self.stream
+        # (DM_HIER_XSTREAM=1: a second stream at G = 1 too -- tests and A/B runs of the
+        # cross-stream form on one GPU)
+        own = self.G > 1 or os.environ.get("DM_HIER_XSTREAM", "0") == "1"
+        self.xstream = torch.cuda.Stream(device=dev) if pipelined and own else self.stream
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1 if pipelined else 0), leaf._ctx, leaf._L)
