@@ -13,7 +13,7 @@ import pytest
 
 from doorman_amd import workloads as W
 from oracle import oracle as O
-from parity_util import (assert_leases_match, assert_resources_match, binned_sizes, float_close,
+from parity_util import (assert_leases_match, assert_resources_match, binned_sizes, float_close, row_capacity,
                          snapshot_with_sizes)
 
 pytestmark = pytest.mark.gpu
@@ -1003,3 +1003,64 @@ def test_configs0_through_the_hip_path(eng):
         assert_leases_match(host, gets, exp, ref, f"configs[0] writeback tick {t}")
         _writeback_host(host, ref)
         W.add_store_sums(host)
+
+
+def test_dense_split_queues_undecided_items():
+    """The split form with items the dense kernel cannot decide (no dense hint: a
+    released row or mixed subclient counts) queued for k_block_rest every tick:
+    resources in all four workgroup bins, FairShare with mixed counts (handed to
+    k_general), ProportionalShare, Static; writeback ticks back to back (no store
+    update between, so the split form runs), every tick against the oracle on the
+    device store as it stood, and gets bit-identical to the one-kernel form
+    (DM_DENSE_SPLIT=0)."""
+    import os
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(8088)
+    sizes = np.concatenate([rng.integers(257, 513, 12), rng.integers(513, 1025, 12), rng.integers(1025, 2049, 8),
+                            rng.integers(2049, 4097, 6)])
+    R, N = len(sizes), int(sizes.sum())
+    snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=0.0, learning_frac=0.0,
+                               parent_expired_frac=0.0)
+    snap["lease_length_s"] = np.full(R, 300, np.int64)
+    snap["expiry_ns"] = np.full(N, NOW + 600 * W.NS, np.int64)
+    off = np.asarray(snap["seg_off"])
+    sub = np.ones(N, np.int64)
+    for r in range(0, R, 5):  # a released row: never dense, streamed every tick
+        snap["expiry_ns"][off[r] + 7] = W.RELEASED
+    for r in range(2, R, 7):  # mixed subclient counts: PS streamed, FS to k_general
+        sub[off[r]:off[r + 1]] = rng.integers(1, 4, sizes[r])
+    snap["subclients"] = sub
+    snap.pop("agg_count", None), snap.pop("agg_sum_has", None), snap.pop("agg_sum_wants", None)
+    old = os.environ.get("DM_DENSE_SPLIT")
+    os.environ["DM_DENSE_SPLIT"] = "1"
+    a = Engine(0)
+    os.environ["DM_DENSE_SPLIT"] = "0"
+    b = Engine(0)
+    if old is None:
+        os.environ.pop("DM_DENSE_SPLIT")
+    else:
+        os.environ["DM_DENSE_SPLIT"] = old
+    try:
+        a.load(snap)
+        b.load(snap)
+        a.set_profiling(True)
+        for i in range(5):
+            now = NOW + i * 5 * W.NS
+            st, res = a.read_store(), a.resources(safe=False)
+            cur = dict(snap)
+            cur.update(has=st["has"], wants=st["wants"], subclients=st["subclients"], expiry_ns=st["expiry_ns"],
+                       agg_count=res["count"], agg_sum_has=res["sum_has"], agg_sum_wants=res["sum_wants"])
+            ref = O.apportion(cur, now)
+            a.apportion(now, writeback=True)
+            b.apportion(now, writeback=True)
+            ga, gb = a.read_store()["has"], b.read_store()["has"]
+            live = ref["expiry_ns"] != W.RELEASED
+            assert float_close(np.where(live, ga, 0.0), np.where(live, ref["gets"], 0.0), row_capacity(cur)).all(), \
+                f"tick {i}"
+            assert ga.tobytes() == gb.tobytes(), f"tick {i}: dense form differs from the one-kernel form"
+        a.sync()
+        kt = a.kernel_times()
+        assert any(k.endswith("_dense") and v[0] > 0 for k, v in kt.items()), kt
+    finally:
+        a.close()
+        b.close()
