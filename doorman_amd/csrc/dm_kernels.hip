@@ -2130,12 +2130,24 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   bool req = false;
   uint32_t flags = 0;
   const Res rs_cfg = load_res(p, (int)rr);
+  // every load the round needs is issued here, before the first is consumed: the
+  // expiry column (root rows are explicit; read unconditionally instead of after the
+  // subclients word) and this server's template inputs (one round trip instead of three)
+  const bool mine = valid && g == ha.server;
+  const int64_t li = mine ? rr - ha.leaf_lo : 0;  // the resource's index in this server's leaf
+  int64_t learn = 0;
+  ResCold rcc{0.0, 0, 0};
+  if (mine) {
+    learn = ha.leaf_prev_cfg[li].learning_end_ns;  // kept (resource.go:163)
+    rcc = ha.root_cold[rr];
+  }
   if (valid) {
     w = p.wants[row];
     h = p.has[row];
     const int32_t raw = p.sub[row];  // expiry encoding (dm_device.h): root rows are explicit or released
+    const int64_t xe = p.expiry[row];
     s = sub_value(raw);
-    e = row_expiry(p, row, raw, rs_cfg.follow_exp);
+    e = sub_released(raw) ? kReleased : (raw < 0 ? xe : rs_cfg.follow_exp);
     const double2* blk = ha.gathered + (int64_t)g * ha.stride;
     flags = (uint32_t)__double_as_longlong(blk[0].x);
     const double2 v = blk[1 + rec];
@@ -2304,11 +2316,9 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   }
 
   // this server's new template for the resource (server.go:279-313)
-  if (valid && g == ha.server) {
-    const int64_t li = rr - ha.leaf_lo;  // the resource's index in this server's leaf
+  if (mine) {
     ResCfg* c = ha.leaf_cfg + li;
     ResCold* cc = ha.leaf_cold + li;
-    const int64_t learn = ha.leaf_prev_cfg[li].learning_end_ns;  // kept (resource.go:163)
     if (flags != 0u) {  // rejected: the templates stay (a staged slot takes a copy)
       if (ha.leaf_prev_cfg != ha.leaf_cfg) {
         *c = ha.leaf_prev_cfg[li];
@@ -2316,7 +2326,6 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
       }
     } else if (req) {
       const ResCfg rc = p.cfg[rr];
-      const ResCold rcc = ha.root_cold[rr];
       const int64_t sec = exp_new >= 0 ? exp_new / kNs : -((-exp_new + kNs - 1) / kNs);  // time.Unix(sec, 0)
       ResCfg t;
       t.capacity = my_gets;               // :293
