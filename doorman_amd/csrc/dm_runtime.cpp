@@ -772,6 +772,7 @@ static hipError_t xs_setup(dm_ctx* c) {
     hipError_t e = hipEventCreateWithFlags(&c->xs_ev[i], hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
+  if (!c->xs_values && !c->xs_ready_value) return hipSuccess;  // events only: no signal memory
   int can = 0;
   if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, c->device) != hipSuccess || !can) {
     (void)hipGetLastError();
