@@ -208,7 +208,7 @@ struct dm_ctx {
     tok->val = false;
   }
   hipError_t xs_wait(const XsTok& tok, hipStream_t s) {
-    if (tok.s == s) return hipSuccess;
+    if (tok.s == s || tok.s == nullptr) return hipSuccess;  // same stream, or known complete
     if (!tok.rec) return xs_order(tok.w, tok.s, s);
     if (!tok.val) return hipStreamWaitEvent(s, xs_ev[tok.w], 0);
     return hipStreamWaitValue64(s, xs_word[tok.w], tok.v, hipStreamWaitValueGte, ~0ull);
@@ -938,6 +938,11 @@ const char* dm_last_error(dm_ctx* c) { return c ? c->err.c_str() : g_last_error.
 int dm_set_stream(dm_ctx* c, void* s) {
   DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  // the template slots' lazy signals on the old stream are complete now, and that
+  // stream may not outlive this call: never record on it again
+  for (int i = 0; i < dm_ctx::kTplSlots; ++i)
+    for (dm_ctx::XsTok* t : {&c->tpl_ready[i], &c->tpl_free[i]})
+      if (!t->rec && t->s == c->stream) t->s = nullptr;
   c->stream = s ? (hipStream_t)s : c->own_stream;
   c->main_dirty = true;
   return DM_OK;
