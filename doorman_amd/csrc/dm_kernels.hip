@@ -561,7 +561,8 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
 struct SegTot {
   AggA a;
   AggB b;
-  uint32_t pad[7];
+  uint32_t pad[7];  // pad[0]: the map's arrival counter (k_large_map finishes the resource; its
+                    // last arriver resets it)
   // nonzero when some chunk's Clean released subclients this tick (pass A, atomicOr),
   // i.e. round 1 must be recomputed; cleared by k_large_fin for the next tick.  With
   // it zero, pass B's other chunks return at once and its first chunk leaves the
@@ -975,7 +976,8 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
 }
 
 __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __restrict__ chunks,
-                                                   const LargeSeg* __restrict__ ls, Partials P) {
+                                                   const LargeSeg* __restrict__ ls, Partials P, int32_t* glist,
+                                                   int32_t* gcount) {
   __shared__ Lds<256> lds;
   const Chunk ch = chunks[blockIdx.x];
   bool ps, fs;
@@ -991,7 +993,16 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   // pass A totals: left by pass B for ProportionalShare / FairShare
   const SegState st =
       uniform((ps || fs) ? seg_state_of(p, L.seg, seg_tot(P, ch.lseg)->a) : seg_state<256>(p, P, L, lds));
-  if (st.general) return;
+  // Without the heterogeneous chain (P.s_set) the map also does k_large_fin's work: the
+  // resource's last-arriving chunk sums the chunks' deltas and writes its record
+  const bool finish = P.s_set == nullptr;
+  if (st.general) {  // k_general decides it; its first chunk lists it (fin's job)
+    if (finish && threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) {
+      glist[atomicAdd(gcount, 1)] = L.seg;
+      seg_tot(P, ch.lseg)->rel = 0;
+    }
+    return;
+  }
   const Res& rs = st.rs;
   const double C = rs.C;
   const double eq = C / (double)st.cl.count;
@@ -1033,7 +1044,21 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     delta.v += g - h;
   }
   delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
-  if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
+  if (!finish) {
+    if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
+    return;
+  }
+  if (threadIdx.x >= 64) return;  // wave 0 hands off (dm_kernel_util.h: write-through, then arrive)
+  if (threadIdx.x == 0) st_wt(P.d_delta + blockIdx.x, delta.v);
+  SegTot* tt = seg_tot(P, ch.lseg);
+  if (!arrive_last(&tt->pad[0], L.chunk_end - L.chunk_begin)) return;
+  SumD d{0.0};
+  for (int q = L.chunk_begin + (int)threadIdx.x; q < L.chunk_end; q += 64) d.v += ld_wt(P.d_delta + q);
+  d = wave_reduce(d, OpSumD());
+  if (threadIdx.x == 0) {
+    tt->rel = 0;  // pass A of the next tick sets it again (every chunk has read it)
+    write_resource(p, L.seg, rs, st.cl, d.v);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P,
@@ -2433,7 +2458,7 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
     case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
     case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
-    case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, glist, gcount); break;
     case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }

@@ -1276,6 +1276,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     for (int i = 0; i < 9 && nch > 0; ++i) {
       const int ph = kSeq[i];
       if (ph >= 5 && !het) continue;
+      if (ph == 4 && !het) continue;  // the map's last-arriving chunks did fin's work
       DM_HIP(c, timed(kCls[i], s_large,
                       [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
