@@ -117,6 +117,9 @@ struct Partials {
   double* bk_w;     // [nchunks * kHetBuckets]
   int64_t* bk_s;
   int32_t* bk_c;
+  // 1: pass B runs one workgroup per large resource (the store holds no
+  // explicit-expiry rows, so pass A's speculative round 1 is exact)
+  int32_t b_first;
 };
 constexpr int kSegTotBytes = 128;
 constexpr int kHetMaxS = 256;                    // distinct subclient counts per resource on the chain

@@ -878,12 +878,17 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
 __global__ __launch_bounds__(256) void k_large_b(DevParams p, const Chunk* __restrict__ chunks,
                                                  const LargeSeg* __restrict__ ls, Partials P) {
   __shared__ Lds<256> lds;
-  const Chunk ch = chunks[blockIdx.x];
+  // P.b_first: one workgroup per large resource, as its first chunk (pass A's
+  // speculative round 1 is exact: the store holds no explicit-expiry rows, so Clean
+  // releases none of the resource's live rows or all of them, and then round 1 sums
+  // nothing either way)
+  const int ci = P.b_first ? ls[blockIdx.x].chunk_begin : (int)blockIdx.x;
+  const Chunk ch = chunks[ci];
   // most chunks leave here: their resource's round 1 is exact from pass A and they
   // are not its first chunk (no config load on that path)
   const LargeSeg L = ls[ch.lseg];
-  const bool first = (int)blockIdx.x == L.chunk_begin;
-  const bool spec_ok = !p.recompute && seg_tot(P, ch.lseg)->rel == 0;  // pass A's speculative partials are exact
+  const bool first = ci == L.chunk_begin;
+  const bool spec_ok = P.b_first || (!p.recompute && seg_tot(P, ch.lseg)->rel == 0);  // pass A's partials are exact
   if (spec_ok && !first) return;
   bool ps;
   {  // only ProportionalShare / FairShare outside learning mode need this pass
@@ -2456,7 +2461,7 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
     case 7: k_large_e<<<dim3(nls, (kHetBuckets + 3) / 4), 256, 0, st>>>(p, ls, P); break;
     case 8: k_large_map_het<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 0: k_large_a<<<nchunks, 256, 0, st>>>(p, chunks, P); break;
-    case 1: k_large_b<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
+    case 1: k_large_b<<<P.b_first ? nls : nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 2: k_large_c<<<nchunks, 256, 0, st>>>(p, chunks, ls, P); break;
     case 3: k_large_map<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, glist, gcount); break;
     case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;

@@ -224,6 +224,11 @@ struct dm_ctx {
   int64_t R = 0, N = 0;
   bool store_loaded = false, cfg_loaded = false;
   bool store_lost = false;  // a failed fused writeback tick wrote part of the store (check_fused)
+  // the store may hold explicit-expiry rows: set by every call that can write one
+  // (load, upserts, decide, the root's tick), cleared by a writeback tick (which
+  // turns every live explicit row into a follower).  Without them pass A's
+  // speculative round 1 is exact and pass B runs one workgroup per large resource.
+  bool expl_rows = true;
   std::vector<int64_t> h_seg_off;
   std::vector<int64_t> h_refresh_s;
 
@@ -1064,6 +1069,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
   c->store_lost = false;
+  c->expl_rows = true;
   c->have_result = false;
   if (c->cfg_loaded && (int64_t)c->h_refresh_s.size() != R) c->cfg_loaded = false;
   return DM_OK;
@@ -1269,6 +1275,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
       P.bk_s = c->ph_bks.p;
       P.bk_c = c->ph_bkc.p;
     }
+    P.b_first = (!het && !p.recompute && !c->expl_rows) ? 1 : 0;
     // A, B, [T], C, [C_het, E], map, [map_het], fin
     static constexpr int kSeq[9] = {0, 1, 5, 2, 6, 7, 3, 8, 4};
     static constexpr int kCls[9] = {KC_LARGE_A, KC_LARGE_B,   KC_LARGE_T,  KC_LARGE_C,  KC_LARGE_CH,
@@ -1351,6 +1358,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (pingpong) std::swap(c->has, c->out_gets);  // the written column becomes the store's (stream order)
   c->last_writeback = wb;
   c->have_result = true;
+  if (wb) c->expl_rows = false;
   if (!(flags & DM_ASYNC)) {
     DM_HIP(c, hipStreamSynchronize(st), "tick");
     c->collect_profile();
@@ -1372,6 +1380,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !subclients || !gets || !expiry_ns)))
     return c->fail(DM_E_INVAL, "bad requests");
   if (n == 0) return DM_OK;
+  c->expl_rows = true;  // decided rows take explicit expiries
   std::vector<int64_t> seg_of((size_t)n);
   for (int64_t k = 0; k < n; ++k) {
     const int64_t r = rows[k];
@@ -1654,6 +1663,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
+  c->expl_rows = true;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   DM_HIP(c, c->st_has.ensure((size_t)n), "stage has");
   DM_HIP(c, c->st_wants.ensure((size_t)n), "stage wants");
@@ -1788,6 +1798,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   if (nu > 0 && !b->upsert_expiry_ns && !c->cfg_loaded)
     return c->fail(DM_E_STATE, "arrivals without expiries take the resource's lease length: load a configuration");
   if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
+  if (nu > 0) c->expl_rows = true;  // arrivals take explicit expiries
   hipStream_t st = c->stream, cp = c->cpy;
   if (!c->bat_flags.p) {
     DM_HIP(c, c->bat_flags.ensure(3), "batch flags");
@@ -2011,6 +2022,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     return root->fail(DM_E_INVAL, "n_servers differs from the root's dm_hier_layout");
   const bool sharded = root->hier_G != 0 && root->hier_sharded;
   const int K = sharded ? 1 : n_servers;
+  root->expl_rows = true;  // the root's rows take the exchange's explicit expiries
   // checked at load (seg_uniform), not per round
   if (root->R <= 0 || root->N != root->R * (int64_t)K || root->seg_uniform != K)
     return root->fail(DM_E_STATE, sharded ? "sharded root store must hold one row per resource"

@@ -404,7 +404,10 @@ def test_large_writeback_ticks_against_oracle():
     after tick), each checked against the oracle on the device store as it stood
     before it.  Between ticks the wants change by nothing, by a little and by a lot,
     one resource loses its wantExtra clients entirely (T not finite), and one tick
-    follows releases."""
+    follows releases.  Then arrivals with explicit expiries, some already past (Clean
+    releases part of a resource: pass B recomputes round 1), and a tick after every
+    follower's lease has lapsed (Clean releases all of them: pass A's speculative
+    round 1 is still exact, so the chain runs without pass B)."""
     rng = np.random.default_rng(4242)
     sizes = np.asarray([4097, 6000, 8192, 20000, 65537, 150000], dtype=np.int64)
     snap = snapshot_with_sizes(rng, sizes, kinds=(3, 3, 3, 2), expired_frac=0.0, learning_frac=0.0)
@@ -415,11 +418,18 @@ def test_large_writeback_ticks_against_oracle():
     try:
         eng.load(snap)
         base = np.asarray(snap["wants"], dtype=np.float64).copy()
-        plan = ["same", "same", "small", "same", "large", "same", "zero", "same", "release", "same"]
+        plan = ["same", "same", "small", "same", "large", "same", "zero", "same", "release", "same", "arrive", "same",
+                "lapse", "same"]
         worst = 0.0
+        now = NOW
         for i, step in enumerate(plan):
-            now = NOW + i * 5 * W.NS
-            if step == "small":
+            now += (1000 if step == "lapse" else 5) * W.NS  # leases are 1..600 s
+            if step == "arrive":  # explicit expiries, half of them already past at this tick
+                rows = rng.choice(N, 400, replace=False).astype(np.int64)
+                st = eng.read_store()
+                exp = np.where(rng.random(400) < 0.5, now - W.NS, now + 30 * W.NS).astype(np.int64)
+                eng.upsert(rows, st["has"][rows], rng.uniform(0.0, 50.0, 400), np.ones(400, np.int64), exp)
+            elif step == "small":
                 w = base * (1.0 + 1e-7 * rng.standard_normal(N))
                 eng.update_wants(np.arange(N, dtype=np.int64), w)
             elif step == "large":
