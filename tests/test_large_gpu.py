@@ -404,7 +404,8 @@ def test_large_writeback_ticks_against_oracle():
     after tick), each checked against the oracle on the device store as it stood
     before it.  Between ticks the wants change by nothing, by a little and by a lot,
     one resource loses its wantExtra clients entirely (T not finite), and one tick
-    follows releases.  Then arrivals with explicit expiries, some already past (Clean
+    follows releases; one follows a non-writeback tick far in the future (every row
+    lapsed in that tick's view, none in the store's).  Then arrivals with explicit expiries, some already past (Clean
     releases part of a resource: pass B recomputes round 1), and a tick after every
     follower's lease has lapsed (Clean releases all of them: pass A's speculative
     round 1 is still exact, so the chain runs without pass B)."""
@@ -418,8 +419,8 @@ def test_large_writeback_ticks_against_oracle():
     try:
         eng.load(snap)
         base = np.asarray(snap["wants"], dtype=np.float64).copy()
-        plan = ["same", "same", "small", "same", "large", "same", "zero", "same", "release", "same", "arrive", "same",
-                "lapse", "same"]
+        plan = ["same", "same", "small", "same", "large", "peek", "same", "zero", "same", "release", "same", "arrive",
+                "same", "lapse", "same"]
         worst = 0.0
         now = NOW
         for i, step in enumerate(plan):
@@ -429,6 +430,9 @@ def test_large_writeback_ticks_against_oracle():
                 st = eng.read_store()
                 exp = np.where(rng.random(400) < 0.5, now - W.NS, now + 30 * W.NS).astype(np.int64)
                 eng.upsert(rows, st["has"][rows], rng.uniform(0.0, 50.0, 400), np.ones(400, np.int64), exp)
+            elif step == "peek":  # (the store's running sums read before it: resources() reads the last tick's)
+                pre = _store_as_snapshot(snap, eng)
+                eng.apportion(now + 10_000 * W.NS, writeback=False)
             elif step == "small":
                 w = base * (1.0 + 1e-7 * rng.standard_normal(N))
                 eng.update_wants(np.arange(N, dtype=np.int64), w)
@@ -440,7 +444,7 @@ def test_large_writeback_ticks_against_oracle():
                 eng.update_wants(rows, np.zeros(len(rows)))
             elif step == "release":
                 eng.release(rng.choice(N, 500, replace=False).astype(np.int64))
-            cur = _store_as_snapshot(snap, eng)
+            cur = pre if step == "peek" else _store_as_snapshot(snap, eng)
             ref = O.apportion(cur, now)
             eng.apportion(now, writeback=True)
             st = eng.read_store()
