@@ -2355,14 +2355,14 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
         *cc = ha.leaf_prev_cold[li];
       }
     } else if (req) {
-      const ResCfg rc = p.cfg[rr];
       const int64_t sec = exp_new >= 0 ? exp_new / kNs : -((-exp_new + kNs - 1) / kNs);  // time.Unix(sec, 0)
       ResCfg t;
       t.capacity = my_gets;               // :293
       t.learning_end_ns = learn;
       t.parent_expiry_ns = sec * kNs;     // :287-288
-      t.lease_len_s = rc.lease_len_s;     // :295 Algorithm
-      t.kind = rc.kind;
+      // :295 Algorithm, from the config loaded up front (no reload after the stores above)
+      t.lease_len_s = (int32_t)((exp_new - p.now) / kNs);
+      t.kind = rs_cfg.kind;
       *c = t;
       ResCold tc;
       tc.safe_capacity = __builtin_isnan(rcc.safe_capacity) ? 0.0 : rcc.safe_capacity;  // :294, :894

@@ -12,6 +12,6 @@ for L in doorman_amd/libdoorman_hip_base.so $VAR; do
   timeout -k 10 200 python -u bench.py --workload ${WL:-c2} --steps ${N:-200} --warmup 5 --no-cpu-baseline --no-extra > gpurun_out/swap/b.json 2> gpurun_out/swap/b.err || { tail -5 gpurun_out/swap/b.err; cp /tmp/cur.so doorman_amd/libdoorman_hip.so; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/swap/b.json').read().strip().splitlines()[-1])
-print('$(basename $L)', round(d['ms_per_step']*1000,1), 'us/step')"
+print('$(basename $L)', round(d['ms_per_step']*1000,1), 'us/step', {k: v['avg_us'] for k, v in d.get('kernels', {}).items()})"
 done; done
 cp /tmp/cur.so doorman_amd/libdoorman_hip.so
