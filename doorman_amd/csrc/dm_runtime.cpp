@@ -285,13 +285,16 @@ struct dm_ctx {
   // The 128-thread bins (3, 4) split by the dense hint (k_block_dense + k_block_rest)
   // on a tick that follows a writeback tick (only those set hints), unless the last
   // split tick the host has heard of queued more than a quarter of the bin's items
-  // for k_block_rest (then every 64th tick tries again: C2's bins, whose resources
-  // keep released rows, run 21 % slower split).  DM_DENSE_SPLIT=0: never split.
+  // for k_block_rest (then it tries again after 64 ticks, doubling the wait after every
+  // try that still queued too many, up to 4096: C2's bins, whose resources keep
+  // released rows, run 21 % slower split, and a try's k_block_rest strides over
+  // thousands of items).  DM_DENSE_SPLIT=0: never split.
   int dense_split = 0xF;  // bit i: bin 3+i runs in the split form (DM_DENSE_SPLIT: 0 off, 1 all, else the mask)
   static constexpr int kSplitBins = 4;  // bins 3..6
   DBuf<int32_t> dq_list[kSplitBins], dq_cnt[kSplitBins];
   int dq_par[kSplitBins] = {};
   int dq_skip[kSplitBins] = {};   // ticks in the one-kernel form since the split was last tried
+  int dq_wait[kSplitBins] = {64, 64, 64, 64};  // ticks before the next try
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
   int fused_G = 512;
@@ -646,6 +649,7 @@ static int upload_plan(dm_ctx* c) {
   for (int i = 0; i < dm_ctx::kSplitBins; ++i) {  // the dense split of bins 3-6: rest queues, two-slot counters
     __atomic_store_n(c->h_dq + i, 0, __ATOMIC_RELAXED);
     c->dq_skip[i] = 0;
+    c->dq_wait[i] = 64;
     const size_t nb = std::max<size_t>(c->h_bins[3 + i].size(), 1);
     DM_HIP(c, c->dq_list[i].ensure(nb), "dense split queue");
     DM_HIP(c, c->dq_cnt[i].ensure(3), "dense split queue");  // two-slot count + the last count told the host
@@ -1319,7 +1323,10 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
       // only a writeback tick sets hints, so the split form follows one
       const int i = b - 3, par = c->dq_par[i];
       const int64_t queued = __atomic_load_n(c->h_dq + i, __ATOMIC_RELAXED);
-      if (4 * queued <= n || ++c->dq_skip[i] >= 64) {
+      const bool good = 4 * queued <= n;
+      if (good) c->dq_wait[i] = 64;
+      if (good || ++c->dq_skip[i] >= c->dq_wait[i]) {
+        if (!good) c->dq_wait[i] = std::min(2 * c->dq_wait[i], 4096);
         c->dq_skip[i] = 0;
         // the rest kernel strides over whatever the dense kernel queues; its grid is
         // only sized from the last split tick's queue (a hint: correctness never
