@@ -434,8 +434,8 @@ def _shard_templates(prev, g, resp, root_cfg, lo):
 CFG_FIELDS_ALL = W.CFG_FIELDS
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
-def test_sharded_exchange_matches_the_reference_model(pipelined):
+@pytest.mark.parametrize("pipelined,large", [(False, False), (True, False), (True, True)])
+def test_sharded_exchange_matches_the_reference_model(pipelined, large):
     """configs[3]'s layout: resources sharded by id over G servers,
     each server an intermediate of its own range; the root (one row per resource,
     its owner's) evaluated redundantly by every server from the gathered blocks.
@@ -443,7 +443,9 @@ def test_sharded_exchange_matches_the_reference_model(pipelined):
     enqueued before the previous tick (one tick of lag).  Every step: root copies
     bit for bit against the model, every leaf's templates bit for bit, leaf leases
     against the oracle on the leaf's store under the templates the model says that
-    tick used."""
+    tick used.  `large`: some leaf resources above 4096 rows, so the leaves' ticks run
+    the large-resource chain (its steady-state form, without pass B's chunk launch,
+    from the second tick) under templates that change kind and capacity."""
     import torch
     from doorman_amd import _lib
     from doorman_amd.engine import Engine
@@ -451,8 +453,10 @@ def test_sharded_exchange_matches_the_reference_model(pipelined):
     torch.cuda.set_device(0)
     L = _lib.lib()
     G = 3
-    rng = np.random.default_rng(31 + pipelined)
+    rng = np.random.default_rng(31 + pipelined + 2 * large)
     sizes = rng.integers(5, 700, 60)
+    if large:
+        sizes[rng.choice(60, 6, replace=False)] = rng.integers(4097, 20000, 6)
     R = len(sizes)
     lo = partition(sizes, G)
     S = 1 + int(np.diff(lo).max())
