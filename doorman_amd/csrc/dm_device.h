@@ -32,7 +32,12 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 constexpr int kSmallMax = 8;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
-constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block256x8, block512x8, sub8x2, sub16x2
+constexpr int kNumBins = 9;
+// Bin 6 (2049-4096 rows) runs on 256 x 16 workgroups (4 wave slots each: they find room
+// beside the other classes' workgroups; C2's bin under contention 63.6 -> 55.0 us of
+// event time) or, when it holds most of the store's rows, on 512 x 8 (12.7 against
+// 15.2 us alone): launch_bin* take kBin6Wide for the latter.
+constexpr int kBin6Wide = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block256x8, block512x8, sub8x2, sub16x2
 // Lease-table footprint (48 B per lease) above which a tick is taken to stream
 // from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
 constexpr int64_t kStreamBytes = 1LL << 30;
@@ -120,6 +125,13 @@ struct Partials {
   // 1: pass B runs one workgroup per large resource (the store holds no
   // explicit-expiry rows, so pass A's speculative round 1 is exact)
   int32_t b_first;
+  // 1: the last call that changed the store was a writeback tick through this chain
+  // (uni and `live` are that tick's), so pass A reads no subclients column for chunks
+  // with uni >= 0: a row live then holds uni, every other row is marked released
+  int32_t s_live;
+  // per chunk: the map leaves the resource's subclients count when every row it left
+  // live holds that count, -1 otherwise
+  int32_t* uni;
 };
 constexpr int kSegTotBytes = 128;
 constexpr int kHetMaxS = 256;                    // distinct subclient counts per resource on the chain

@@ -627,22 +627,37 @@ struct ChunkRows {
 // consumed, see group_segment), liveness from the expiry encoding, then has for
 // the rows Clean releases only (every row in recompute mode): the steady state
 // reads 12 of a lease's 20 bytes here (C2: 122 -> 73 MB per tick).
-__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, const Res& rs) {
+// uni >= 0: the subclients words are not read -- a row whose bit in prev_live (the
+// last writeback tick's live bits, Partials::s_live) is set holds uni, any other row is
+// marked released
+__device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, const Res& rs,
+                                           int uni = -1, uint32_t prev_live = 0) {
   const double* __restrict__ wb = p.wants + ch.row0;
   const double* __restrict__ hb = p.has + ch.row0;
   const int32_t* __restrict__ sb = p.sub + ch.row0;
   const int64_t* __restrict__ eb = p.expiry + ch.row0;
   r.valid = r.live = r.expl = r.rel = 0;
   int sr[kLR];
+  if (uni >= 0) {
 #pragma unroll
-  for (int k = 0; k < kLR; ++k) {
-    const int i = k * 256 + threadIdx.x;
-    const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
-    r.w[k] = wb[u];
-    sr[k] = sb[u];
-    r.h[k] = 0.0;
-    // two round trips of half the rows (C2 tick 163 -> 157 us, tools/ab.py)
-    if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    for (int k = 0; k < kLR; ++k) {
+      const int i = k * 256 + threadIdx.x;
+      r.w[k] = wb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+      sr[k] = (prev_live >> k & 1) ? uni : (int32_t)kSubReleased;
+      r.h[k] = 0.0;
+      if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLR; ++k) {
+      const int i = k * 256 + threadIdx.x;
+      const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
+      r.w[k] = wb[u];
+      sr[k] = sb[u];
+      r.h[k] = 0.0;
+      // two round trips of half the rows (C2 tick 163 -> 157 us, tools/ab.py)
+      if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    }
   }
   int64_t e[kLR];
 #pragma unroll
@@ -793,7 +808,10 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
   const Chunk ch = chunks[blockIdx.x];
   const Res rs = load_res(p, ch.seg);
   ChunkRows rw;
-  load_chunk(p, ch, rw, rs);
+  {
+    const int uni = P.s_live ? __builtin_amdgcn_readfirstlane(P.uni[blockIdx.x]) : -1;
+    load_chunk(p, ch, rw, rs, uni, uni >= 0 ? P.live[(size_t)blockIdx.x * 256 + threadIdx.x] : 0u);
+  }
   AggA a = zeroA();
 #pragma unroll
   for (int k = 0; k < kLR; ++k) {
@@ -1002,6 +1020,7 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   // resource's last-arriving chunk sums the chunks' deltas and writes its record
   const bool finish = P.s_set == nullptr;
   if (st.general) {  // k_general decides it; its first chunk lists it (fin's job)
+    if (threadIdx.x == 0) P.uni[blockIdx.x] = -1;
     if (finish && threadIdx.x == 0 && (int)blockIdx.x == L.chunk_begin) {
       glist[atomicAdd(gcount, 1)] = L.seg;
       seg_tot(P, ch.lseg)->rel = 0;
@@ -1049,6 +1068,8 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
     delta.v += g - h;
   }
   delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
+  if (threadIdx.x == 0)  // after a writeback tick every row this left live holds it (Partials::s_live)
+    P.uni[blockIdx.x] = st.a.smin == st.a.smax ? st.a.smin : -1;
   if (!finish) {
     if (threadIdx.x == 0) P.d_delta[blockIdx.x] = delta.v;
     return;
@@ -2406,7 +2427,8 @@ hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_
     case 3: k_block<128, 4><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
     case 4: k_block<128, 8><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
     case 5: k_block<256, 8><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 6: k_block<512, 8><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
+    case 6: k_block<256, 16><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
+    case kBin6Wide: k_block<512, 8><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
     case 7: k_sub<8, 2><<<(unsigned)((n + 31) / 32), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 8: k_sub<16, 2><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
@@ -2432,7 +2454,8 @@ hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, 
     case 3: k_block_dense<128, 4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
     case 4: k_block_dense<128, 8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
     case 5: k_block_dense<256, 8><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
-    case 6: k_block_dense<512, 8><<<n, 512, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    case 6: k_block_dense<256, 16><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    case kBin6Wide: k_block_dense<512, 8><<<n, 512, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -2446,7 +2469,10 @@ hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, i
     case 3: k_block_rest<128, 4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
     case 4: k_block_rest<128, 8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
     case 5: k_block_rest<256, 8><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
-    case 6: k_block_rest<512, 8><<<rg, 512, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    case 6: k_block_rest<256, 16><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    case kBin6Wide:
+      k_block_rest<512, 8><<<rg, 512, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

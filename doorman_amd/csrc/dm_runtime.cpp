@@ -229,6 +229,10 @@ struct dm_ctx {
   // turns every live explicit row into a follower).  Without them pass A's
   // speculative round 1 is exact and pass B runs one workgroup per large resource.
   bool expl_rows = true;
+  // the last call that changed the store was a writeback tick through the chain
+  // (Partials::s_live): cleared at the start of every tick and by every call that
+  // writes a subclients word or releases a row
+  bool chain_live_ok = false;
   std::vector<int64_t> h_seg_off;
   std::vector<int64_t> h_refresh_s;
 
@@ -295,6 +299,7 @@ struct dm_ctx {
   int dq_par[kSplitBins] = {};
   int dq_skip[kSplitBins] = {};   // ticks in the one-kernel form since the split was last tried
   int dq_wait[kSplitBins] = {64, 64, 64, 64};  // ticks before the next try
+  bool bin6_wide = false;  // bin 6 on 512 x 8 workgroups (kBin6Wide): it holds most of the rows
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
   int fused_G = 512;
@@ -327,6 +332,7 @@ struct dm_ctx {
   DBuf<int32_t> pa_nan;
   DBuf<uint32_t> pa_live;
   DBuf<uint8_t> p_tot;
+  DBuf<int32_t> p_uni;
   // heterogeneous FairShare on the chain (allocated on the first tick that may need it)
   DBuf<uint32_t> ph_set;  // per large resource: distinct subclient counts (all ones between ticks)
   DBuf<int32_t> ph_n, ph_bkc;
@@ -457,7 +463,7 @@ struct dm_ctx {
     d_dq = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pa_live.release(); p_tot.release();
+    pa_nan.release(); pa_live.release(); p_tot.release(); p_uni.release();
     ph_set.release(); ph_n.release(); ph_bkc.release(); ph_het.release(); ph_bkw.release(); ph_bks.release();
     ph_set_ready = 0;
     glist.release(); gcount.release();
@@ -646,6 +652,11 @@ static int upload_plan(dm_ctx* c) {
     DM_HIP(c, hipHostMalloc((void**)&c->h_dq, dm_ctx::kSplitBins * sizeof(int32_t), hipHostMallocMapped), "dense split word");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_dq, c->h_dq, 0), "dense split word");
   }
+  {
+    int64_t rows6 = 0;
+    for (const WorkItem& w : c->h_bins[6]) rows6 += w.n & 0xFFFF;
+    c->bin6_wide = 2 * rows6 > c->N;
+  }
   for (int i = 0; i < dm_ctx::kSplitBins; ++i) {  // the dense split of bins 3-6: rest queues, two-slot counters
     __atomic_store_n(c->h_dq + i, 0, __ATOMIC_RELAXED);
     c->dq_skip[i] = 0;
@@ -688,6 +699,7 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pd_delta.ensure(nc), "partials");
   DM_HIP(c, c->pa_nan.ensure(nc), "partials");
   DM_HIP(c, c->pa_live.ensure(nc * 256), "partials");
+  DM_HIP(c, c->p_uni.ensure(nc), "partials");
   DM_HIP(c, c->p_tot.ensure(std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes), "partials");
   DM_HIP(c, hipMemsetAsync(c->p_tot.p, 0, std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes, st),
          "partials");  // SegTot::rel starts clear
@@ -1074,6 +1086,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   c->store_loaded = true;
   c->store_lost = false;
   c->expl_rows = true;
+  c->chain_live_ok = false;
   c->have_result = false;
   if (c->cfg_loaded && (int64_t)c->h_refresh_s.size() != R) c->cfg_loaded = false;
   return DM_OK;
@@ -1081,6 +1094,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
 
 int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   DM_ENTER(c);
+  c->chain_live_ok = false;
   if (!cfg || R < 0 || !cfg->kind || !cfg->capacity || !cfg->lease_length_s || !cfg->refresh_interval_s ||
       !cfg->learning_end_ns || !cfg->parent_expiry_ns || !cfg->safe_capacity)
     return c->fail(DM_E_INVAL, "bad config");
@@ -1199,6 +1213,9 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   }
   p.now = now_ns;
   p.recompute = (flags & DM_AGG_RECOMPUTE) ? 1 : 0;
+  const bool live_ok = c->chain_live_ok;
+  c->chain_live_ok = false;
+  bool chain_live = false;  // this tick ran the (non-heterogeneous) chain
   if (wb && !c->pub_ring.empty()) {
     const int64_t n = (int64_t)c->pub_ring.size();
     p.pub = c->pub_ring[(size_t)(c->pub_k % n)];
@@ -1280,6 +1297,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
       P.bk_c = c->ph_bkc.p;
     }
     P.b_first = (!het && !p.recompute && !c->expl_rows) ? 1 : 0;
+    P.s_live = (!het && live_ok && !c->expl_rows) ? 1 : 0;
+    P.uni = c->p_uni.p;
     // A, B, [T], C, [C_het, E], map, [map_het], fin
     static constexpr int kSeq[9] = {0, 1, 5, 2, 6, 7, 3, 8, 4};
     static constexpr int kCls[9] = {KC_LARGE_A, KC_LARGE_B,   KC_LARGE_T,  KC_LARGE_C,  KC_LARGE_CH,
@@ -1292,6 +1311,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                       [&] { return launch_large(ph, p, c->chunks.p, nch, c->large.p, nls, P, gl, gc, s_large); }),
              "large-resource kernels");
     }
+    chain_live = nch > 0 && !het;
   }
   // the workgroup bins split by the dense hint after a writeback tick (hints set)
   const bool split_dense = c->have_result && c->last_writeback;
@@ -1319,6 +1339,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     if (n == 0) continue;
     if (merge_subs && (b == 7 || b == 8 || b <= 2)) continue;
     hipStream_t s = cls_stream(b);
+    const int lb = (b == 6 && c->bin6_wide) ? kBin6Wide : b;  // the launchers' bin (shape)
     if (b >= 3 && b < 3 + dm_ctx::kSplitBins && ((c->dense_split >> (b - 3)) & 1) && split_dense) {
       // only a writeback tick sets hints, so the split form follows one
       const int i = b - 3, par = c->dq_par[i];
@@ -1333,11 +1354,11 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
         // depends on it): an empty queue costs 16 workgroups that read one count
         const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
         DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
-                 return launch_bin_dense(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc, s);
+                 return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc, s);
                }),
                "group kernel (dense split)");
         DM_HIP(c, timed(KC_REST3 + i, s, [&] {
-                 return launch_bin_rest(b, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
+                 return launch_bin_rest(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
                                         rest_grid, gl, gc, s);
                }),
                "group kernel (dense split)");
@@ -1345,7 +1366,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
         continue;
       }
     }
-    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(b, p, c->bins[b].p, n, gl, gc, s); }),
+    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(lb, p, c->bins[b].p, n, gl, gc, s); }),
            "group kernel");
   }
   if (!c->h_packs.empty())
@@ -1366,6 +1387,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   c->last_writeback = wb;
   c->have_result = true;
   if (wb) c->expl_rows = false;
+  c->chain_live_ok = wb && chain_live;
   if (!(flags & DM_ASYNC)) {
     DM_HIP(c, hipStreamSynchronize(st), "tick");
     c->collect_profile();
@@ -1388,6 +1410,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
     return c->fail(DM_E_INVAL, "bad requests");
   if (n == 0) return DM_OK;
   c->expl_rows = true;  // decided rows take explicit expiries
+  c->chain_live_ok = false;
   std::vector<int64_t> seg_of((size_t)n);
   for (int64_t k = 0; k < n; ++k) {
     const int64_t r = rows[k];
@@ -1671,6 +1694,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
   c->expl_rows = true;
+  c->chain_live_ok = false;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   DM_HIP(c, c->st_has.ensure((size_t)n), "stage has");
   DM_HIP(c, c->st_wants.ensure((size_t)n), "stage wants");
@@ -1764,6 +1788,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
+  c->chain_live_ok = false;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   const StageCol cols[] = {{c->st_rows.p, rows, 8}};
   int rc = staged_check(c, n, cols, 1, false, false);
@@ -1806,6 +1831,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     return c->fail(DM_E_STATE, "arrivals without expiries take the resource's lease length: load a configuration");
   if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
   if (nu > 0) c->expl_rows = true;  // arrivals take explicit expiries
+  if (nu > 0 || nr > 0) c->chain_live_ok = false;  // subclients words written, rows released
   hipStream_t st = c->stream, cp = c->cpy;
   if (!c->bat_flags.p) {
     DM_HIP(c, c->bat_flags.ensure(3), "batch flags");
@@ -2030,6 +2056,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   const bool sharded = root->hier_G != 0 && root->hier_sharded;
   const int K = sharded ? 1 : n_servers;
   root->expl_rows = true;  // the root's rows take the exchange's explicit expiries
+  root->chain_live_ok = false;
   // checked at load (seg_uniform), not per round
   if (root->R <= 0 || root->N != root->R * (int64_t)K || root->seg_uniform != K)
     return root->fail(DM_E_STATE, sharded ? "sharded root store must hold one row per resource"
