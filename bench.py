@@ -125,7 +125,7 @@ def kernel_units(snap):
     units = {}
     edges = [("sub8x2", 9, 16), ("sub16x2", 17, 32), ("sub16x4", 33, 64), ("sub32x4", 65, 128),
              ("wave64x4", 129, 256), ("block128x4", 257, 512), ("block128x8", 513, 1024), ("block256x8", 1025, 2048),
-             ("block512x8", 2049, 4096)]
+             ("block2k4k", 2049, 4096)]
     small = sizes <= 8
     units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
     for name, lo, hi in edges:
@@ -134,9 +134,9 @@ def kernel_units(snap):
     m = (sizes >= 9) & (sizes <= 256)  # the sub-wave bins in one launch (k_subs)
     units["subs_merged"] = (int(sizes[m].sum()), int(m.sum()))
     big = sizes > 4096
-    for name in ("large_fused", "large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
+    for name in ("large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
         units[name] = (int(sizes[big].sum()), int(big.sum()))
-    for b in ("block128x4", "block128x8", "block256x8", "block512x8"):  # the split form's two kernels
+    for b in ("block128x4", "block128x8", "block256x8", "block2k4k"):  # the split form's two kernels
         units[b + "_dense"] = units[b]
         units[b + "_rest"] = (0, 0)  # only what the dense kernel queued; counted with the dense kernel
     units["hier_publish"] = (0, len(sizes))
@@ -402,6 +402,15 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
                             f"{SURVEY_LEASE_BYTES} B per lease"),
             "dense_lease_share": round(dense_k / leases_k, 4) if leases_k else 0.0,
             "survey_layout_equivalent_GBs": round((SURVEY_LEASE_BYTES * leases_k + 64 * res_k) / avg_s / 1e9, 1),
+            # SURVEY.md 8(d) / BASELINE.md 3's canonical 48 B x N + 64 B x R over the same launch time:
+            # above 1 here because this layout does not move those bytes (layout_note)
+            "frac_survey_model": round((SURVEY_LEASE_BYTES * leases_k + 64 * res_k) / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+            "layout_note": ("frac is over the bytes this layout must move: a lease granted by a writeback tick "
+                            "follows its resource's expiry (one follow_exp per resource, no 8-B expiry read or "
+                            "written per lease) and subclients are int32 (28 B per lease); a dense resource's rows "
+                            "(every row a live follower with one count, recorded in its state byte) skip the "
+                            "subclients column (24 B).  PMC traffic (traffic) confirms the kernel moves these "
+                            "bytes, not the canonical 48 (frac_survey_model)"),
             "avg_launch_us": round(avg_s * 1e6, 2),
             "kernel_time_share": round(total_ms / sum(v[1] for v in ktimes.values()), 3),
             "kernel_time_share_note": "of the summed event time of every profiled kernel class of a step (the "
@@ -409,6 +418,179 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
             "timed_region_stream_us_per_step": round(run["stream_ms"] * 1e3 / steps, 2),
             "duration_source": ("HIP event pair around the timed region on the kernel's stream (one kernel "
                                 "per tick)" if single else "HIP events around every launch, profiled region")}
+
+
+# ---------------------------------------------------------------------------
+# exchange self-check (N > 1 runs: the RCCL leg of the exchange checks itself)
+# ---------------------------------------------------------------------------
+def _minF(l, r):
+    return r if l > r else l  # algorithm.go:50-55
+
+
+def root_round_one(now, cfg, row, sums, flags, sum_wants, count):
+    """The root's round for one resource of the sharded layout (one root row, its
+    owner's; k_hier_tick with K = 1), restated for the bench's self-check from
+    server.go:822-901 -> resource.go:100-113 -> algorithm.go:95-302 / store.go:153-181:
+    Clean, then the owner's request (SumWants, Count) decided by the resource's
+    algorithm against the cleaned store, then the owner's new template
+    (server.go:279-313).  Returns (template fields, gets) or None for a rejected block."""
+    f64 = np.float64
+    kind, cap, lease_s, refresh_s, learn_end, parent, safe = cfg
+    if flags != 0:
+        return None
+    w, h, sub, e = f64(row[0]), f64(row[1]), int(row[2]), int(row[3])
+    cnt, sh, sw = int(sums[0]), f64(sums[1]), f64(sums[2])
+    released = e == W_RELEASED
+    expired = not released and now > e
+    live = not released and not expired
+    if expired:  # Clean (store.go:169-181)
+        sw, sh, cnt = sw - w, sh - h, cnt - sub
+    if not live:
+        w, h, sub = f64(0.0), f64(0.0), 0
+    req = sum_wants > 0.0
+    rw, rs = f64(sum_wants), int(count) if sum_wants > 0.0 else 0
+    C = f64(0.0) if parent < now else f64(cap)
+    learning = learn_end > now
+    gets = f64(0.0)
+    with np.errstate(all="ignore"):
+        if req:
+            if learning:
+                gets = f64(0.0)  # Learn: the request's Has (an intermediate never fills it)
+            elif kind == 0:
+                gets = rw
+            elif kind == 1:
+                gets = _minF(C, rw)
+            elif kind == 2:  # ProportionalShare (algorithm.go:213-293)
+                eq = C / f64(cnt + (0 if live else rs))
+                ds = eq * f64(rs)
+                avail = C - sh + h
+                if sw <= C or rw <= ds:
+                    gets = _minF(rw, avail)
+                else:  # the Map: only the requesting row, with its request values, if present
+                    x = y = f64(0.0)
+                    if live:
+                        esp = eq * f64(rs)
+                        if rw < esp:
+                            x += esp - rw
+                        else:
+                            y += rw - esp
+                    gets = _minF(ds + (rw - ds) * (x / y), avail)
+            else:  # FairShare (algorithm.go:95-206): no other row, so round 1 and 2 sum nothing
+                avail = C - sh + h
+                eq = C / f64(cnt - sub + rs)
+                ds = eq * f64(rs)
+                if rw <= ds:
+                    gets = _minF(rw, avail)
+                else:
+                    dE = (f64(0.0) / f64(rs)) * f64(rs)
+                    if rw < ds + dE:
+                        gets = _minF(rw, avail)
+                    else:
+                        gets = _minF(ds + dE + (f64(0.0) / f64(rs)) * f64(rs), avail)
+    if req:
+        exp_new = now + int(lease_s) * 1_000_000_000
+        sec = exp_new // 1_000_000_000  # time.Unix(sec, 0)
+        tpl = (int(kind), float(gets), int(lease_s), int(refresh_s), sec * 1_000_000_000,
+               0.0 if np.isnan(safe) else float(safe))
+    else:  # the "*" default template (server.go:53-63)
+        tpl = (3, 0.0, 20, 1, W_INT64_MAX, 0.0)
+    return tpl, float(gets)
+
+
+W_RELEASED = np.iinfo(np.int64).min
+W_INT64_MAX = np.iinfo(np.int64).max
+_TPL_FIELDS = ("kind", "capacity", "lease_length_s", "refresh_interval_s", "parent_expiry_ns", "safe_capacity")
+
+
+def exchange_self_check(torch, dist, ht, leaf, root, bounds, rank, world, g, now, red_dev, corrupt=False,
+                        n_sample=64):
+    """One more exchange step after the timed ones, then checks that the exchange moved
+    the right bytes (for N > 1: the RCCL all-gather's first use in a run):
+      blocks  every rank's gathered buffer hashes alike (all-reduce MIN == MAX);
+      own     this rank's block sits at its slot of the gathered buffer, and holds its
+              leaf's running {SumWants, Count};
+      root    rank 0 recomputes, from ITS gathered copy, the root round of a sample of
+              every rank's resources (first, last and random ones: the root rows and
+              sums before the step, gathered from their owners) and compares the
+              templates the owners' leaves took, bit for bit.
+    corrupt (test-only): rank world-1 perturbs its gathered copy after the all-gather."""
+    import hashlib
+    from doorman_amd import _lib
+    ht.sync()
+    lo, hi = int(bounds[g]), int(bounds[g + 1])
+    n = hi - lo
+    pre = root.read_store(lo, n)
+    pres = root.resources(lo, n, safe=False)
+    rng = np.random.default_rng(1234 + g)
+    pick = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, max(0, n_sample - 2))])) if n else []
+    # the block an exchange publishes: the leaf's sums after this step's tick (pipelined:
+    # the tick writes it) or before it (unpipelined: published first)
+    lr = None if ht.pipelined else leaf.resources(safe=False)
+    gather0 = ht.gather
+    if corrupt and rank == world - 1:
+        def bad(src, dst):
+            gather0(src, dst)
+            dst[1, 0] += 1.0  # block 0's first SumWants
+        ht.gather = bad
+    try:
+        ht.tick(now)
+        ht.sync()
+    finally:
+        ht.gather = gather0
+    k = (ht.step - 1) % len(ht.totals)
+    gathered = ht.gathered[k].cpu().numpy().copy()
+    S = ht.stride
+    own = ht.totals[k].cpu().numpy()
+    own_ok = gathered[g * S:(g + 1) * S].tobytes() == own.tobytes()
+    lr = lr or leaf.resources(safe=False)
+    pub_ok = (np.ascontiguousarray(own[1:1 + n, 0]).tobytes() == lr["sum_wants"].tobytes()
+              and np.ascontiguousarray(own[1:1 + n, 1]).view(np.int64).tobytes()
+              == lr["count"].astype(np.int64).tobytes())
+    if ht.pipelined:  # take the staged templates of this exchange
+        _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 0), leaf._ctx, leaf._L)
+        _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1), leaf._ctx, leaf._L)
+    tpl = leaf.config()
+    samples = [(lo + int(i), (pre["wants"][i], pre["has"][i], int(pre["subclients"][i]), int(pre["expiry_ns"][i])),
+                (int(pres["count"][i]), pres["sum_has"][i], pres["sum_wants"][i]),
+                tuple(tpl[f][i].item() for f in _TPL_FIELDS)) for i in pick]
+    h = int.from_bytes(hashlib.blake2b(gathered.tobytes(), digest_size=8).digest(), "little", signed=True)
+    ok = 1 if (own_ok and pub_ok) else 0
+    if world > 1:
+        allsamp = [None] * world
+        dist.all_gather_object(allsamp, samples)
+        allsamp = [x for part in allsamp for x in part]
+        t = torch.tensor([h, -h, ok], dtype=torch.int64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        hmin, hmax, ok_all = int(t[0].item()), -int(t[1].item()), int(t[2].item())
+    else:
+        allsamp, hmin, hmax, ok_all = samples, h, h, ok
+    if rank != 0:
+        return None
+    rc = root.config()
+    cfg_cols = [rc[f] for f in ("kind", "capacity", "lease_length_s", "refresh_interval_s", "learning_end_ns",
+                                "parent_expiry_ns", "safe_capacity")]
+    owners = np.searchsorted(bounds, [r for r, *_ in allsamp], side="right") - 1
+    mism, rejected = 0, 0
+    for (r, row, sums, got), o in zip(allsamp, owners):
+        blk = gathered[o * S:(o + 1) * S]
+        flags = int(blk[0, 0:1].view(np.int64)[0])
+        v = blk[1 + r - int(bounds[o])]
+        res = root_round_one(now, [c[r] for c in cfg_cols], row, sums, flags, v[0], int(v[1:2].view(np.int64)[0]))
+        if res is None:
+            rejected += 1
+            continue
+        want = res[0]
+        if any(np.float64(a).tobytes() != np.float64(b).tobytes() if isinstance(a, float) else a != b
+               for a, b in zip(want, got)):
+            mism += 1
+    return {"consistent": bool(hmin == hmax and ok_all == 1 and mism == 0 and rejected == 0),
+            "blocks_hash_equal": hmin == hmax, "own_blocks_ok": ok_all == 1,
+            "sample": len(allsamp), "template_mismatches": mism, "rejected": rejected,
+            "corrupted_on_purpose": bool(corrupt),
+            "how": "one more exchange step after the timed ones: gathered buffers hashed and compared over ranks "
+                   "(all-reduce MIN/MAX), every rank's own block at its slot and equal to its leaf's running sums, "
+                   "and rank 0 recomputing from its gathered copy the root round of a sample of every rank's "
+                   "resources and comparing the owners' templates bit for bit"}
 
 
 def spawn_ranks(args) -> int:
@@ -445,7 +627,24 @@ def main():
                          "strong scaling; auto); replicated = a full store per GPU (weak scaling)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's exchange before its leaf tick on one stream instead of beside the next tick")
+    ap.add_argument("--rehearse-shard", type=int, default=0, metavar="N",
+                    help="c3 only, one process on one GPU: run rank --rehearse-rank's full step of an N-GPU node "
+                         "(its shard of the 100M-lease snapshot, the leaf tick with its publish, an N-block gathered "
+                         "buffer -- the other N-1 blocks synthesized from their shards' totals, this rank's block "
+                         "copied in place of the RCCL all-gather -- and the root round), on the exchange's own stream "
+                         "as at N > 1; prints the rank's step time (not a whole-node measurement)")
+    ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--check-corrupt", action="store_true",
+                    help="test only: the exchange self-check's step corrupts one rank's gathered copy (expect "
+                         "dist.consistent false)")
     args = ap.parse_args()
+    if args.rehearse_shard:
+        if args.workload != "c3" or args.gpus != 1 or args.rehearse_shard < 2:
+            raise SystemExit("--rehearse-shard N (N >= 2) rehearses one rank of configs[3] on one GPU: --workload c3, "
+                             "--gpus 1")
+        if not 0 <= args.rehearse_rank < args.rehearse_shard:
+            raise SystemExit("--rehearse-rank must be in [0, N)")
+        args.layout, args.hier = "sharded", "on"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
@@ -499,10 +698,37 @@ def main():
         else:
             dst.copy_(src)
 
+    # the node this rank's shard belongs to: the real one, or the rehearsed one
+    s_world, s_rank = (args.rehearse_shard, args.rehearse_rank) if args.rehearse_shard else (world, rank)
+
+    def rehearsal_gather(stride):
+        """--rehearse-shard: the gathered buffer of an s_world-rank node as this rank sees
+        it.  The other ranks' blocks are synthesized once from their shards' initial
+        totals ({SumWants, Count} per resource, no flags); each step copies this rank's
+        block into its slot, where the RCCL all-gather would put it (the transfer itself
+        is not rehearsed)."""
+        b = c3_bounds(s_world)
+        blocks = np.zeros((s_world * stride, 2))
+        for j in range(s_world):
+            if j == s_rank:
+                continue
+            sj = W.uniform_range(C3_R, C3_CLIENTS, int(b[j]), int(b[j + 1]), kind=W.FAIR_SHARE, seed=3)
+            n = int(b[j + 1] - b[j])
+            blocks[j * stride + 1: j * stride + 1 + n, 0] = sj["agg_sum_wants"]
+            blocks[j * stride + 1: j * stride + 1 + n, 1] = np.asarray(sj["agg_count"], np.int64).view(np.float64)
+        state = {"filled": False}
+
+        def gather(src, dst):
+            if not state["filled"]:
+                dst.copy_(torch.from_numpy(blocks).to(dst.device))
+                state["filled"] = True
+            dst[s_rank * stride:(s_rank + 1) * stride].copy_(src)
+        return gather
+
     def measure(layout):
         """Load this rank's store (and root copy), run the timed steps; returns the run,
         the snapshot and the engines (closed by the caller)."""
-        snap = make_workload(args.workload, rank, world, layout)
+        snap = make_workload(args.workload, s_rank, s_world, layout)
         R = len(snap["seg_off"]) - 1
         eng = Engine(dev_index)
         eng.load(snap)
@@ -516,10 +742,12 @@ def main():
             from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
             root = Engine(dev_index)
             if layout == "sharded":  # the root of the whole snapshot: one row per resource (its owner's)
-                bounds = c3_bounds(world)
+                bounds = c3_bounds(s_world)
                 root.load(root_snapshot(C3_R, 1, W.FAIR_SHARE, 1000.0, lease_length_s=20))
-                ht = HierarchicalTick(torch, eng, root, C3_R, world, rank, gather, shard_lo=bounds,
-                                      pipelined=not args.no_pipeline)
+                stride = 1 + int(np.diff(bounds).max())
+                ht = HierarchicalTick(torch, eng, root, C3_R, s_world, s_rank,
+                                      rehearsal_gather(stride) if args.rehearse_shard else gather,
+                                      shard_lo=bounds, pipelined=not args.no_pipeline)
             else:
                 root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world,
                                         lease_length_s=20))
@@ -531,6 +759,9 @@ def main():
         if ht is not None:
             ht.sync()
             ht.check()  # any server whose request the root rejected (server.go:863-866) fails loudly
+            if layout == "sharded":
+                run["self_check"] = exchange_self_check(torch, dist, ht, eng, root, c3_bounds(s_world), rank, world,
+                                                        s_rank, now, red_dev, corrupt=args.check_corrupt)
         t = torch.tensor([run["elapsed"]], dtype=torch.float64, device=red_dev)
         n = torch.tensor([len(snap["wants"])], dtype=torch.float64, device=red_dev)
         if world > 1:
@@ -547,6 +778,9 @@ def main():
     now = W.NOW_NS
 
     extra = {}
+    if args.rehearse_shard:
+        args.no_extra = True
+        args.no_cpu_baseline = True
     if rank == 0 and world == 1 and not args.no_extra and args.workload == "c3":
         # the 10M-lease C1 tick (BASELINE configs[1]) beside the north-star line
         eng.close()
@@ -611,7 +845,10 @@ def main():
                        "parallelism": (f"intermediate-server hierarchy x{world}, {layout}" if hier
                                        else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
-            "dist": dist_info,
+            "dist": (((dist_info or {}) | {"consistent": run["self_check"]["consistent"],
+                                          "check_sample": run["self_check"]["sample"],
+                                          "exchange_check": run["self_check"]})
+                     if run.get("self_check") else dist_info),
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
                         for k, v in run["ktimes"].items()},
@@ -619,6 +856,16 @@ def main():
             "extra": extra or None,
             "cpu_baseline": cpu,
         }
+        if args.rehearse_shard:
+            line["metric"] = "rehearsal: one rank's step of an N-GPU configs[3] node on one GPU (not a bench line)"
+            line["value"] = N * args.steps / t_max
+            line["unit"] = "leases/s of this rank"
+            line["rehearsal"] = {
+                "node_gpus": s_world, "rank": s_rank, "shard_resources": R, "shard_leases": N,
+                "step_us": round(t_max / args.steps * 1e6, 2),
+                "gather": "this rank's block copied into its slot of an N-block buffer (the other N-1 synthesized "
+                          "once from their shards' totals); the RCCL transfer itself is not rehearsed",
+                "projected_node_leases_per_s_if_ranks_alike": s_world * N * args.steps / t_max}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

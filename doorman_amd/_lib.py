@@ -111,7 +111,6 @@ _SIGS = {
     "dm_hier_pipeline": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_publish_ring": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "dm_set_large_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_plan_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),

@@ -32,12 +32,12 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 constexpr int kSmallMax = 8;
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
-constexpr int kNumBins = 9;
+constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block256x8, the 2049-4096 bin, sub8x2, sub16x2
 // Bin 6 (2049-4096 rows) runs on 256 x 16 workgroups (4 wave slots each: they find room
 // beside the other classes' workgroups; C2's bin under contention 63.6 -> 55.0 us of
 // event time) or, when it holds most of the store's rows, on 512 x 8 (12.7 against
 // 15.2 us alone): launch_bin* take kBin6Wide for the latter.
-constexpr int kBin6Wide = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block256x8, block512x8, sub8x2, sub16x2
+constexpr int kBin6Wide = 9;
 // Lease-table footprint (48 B per lease) above which a tick is taken to stream
 // from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
 constexpr int64_t kStreamBytes = 1LL << 30;
@@ -143,56 +143,6 @@ struct HetRes {
   double bw[kHetBuckets];   // per bucket over the resource's chunks (k_large_e): sum of wants,
   int64_t bs[kHetBuckets];  // sum of subclients,
   int64_t bc[kHetBuckets];  // count of the wantExtra clients
-};
-
-// One-launch large path (k_large_fused, dm_large.hip): every chunk keeps its rows
-// in VGPRs while the resource's chunks exchange per-resource totals in-launch.
-// Chunk records and totals records are kFusedWords u64 words:
-//   0 cnt  1 has  2 wants  3 all.cnt  4 all.has  5 all.wants  6 smin|smax<<32  7 nan
-//   8 b.x  9 b.y  10 b.i   11 c.ee  12 c.sgt  13 delta
-constexpr int kFusedRows = 8;    // rows per thread: a chunk is G * kFusedRows rows
-constexpr int kFusedWords = 16;
-// per large resource, in u32 words: arrive[4] counters on one 128-B line, then per
-// phase kFusedFlagCopies replicas of its flag, each on its own 128-B line (hundreds
-// of polling chunks spread over the replicas instead of hammering one line)
-constexpr int kFusedFlagCopies = 8;
-constexpr int kFusedSync = 32 + 4 * kFusedFlagCopies * 32;
-struct FusedState {
-  uint32_t* ticket;  // chunk dispenser: chunks start in resource order (co-residency argument)
-  uint32_t* sync;    // [nls * kFusedSync], zero at plan build; counters reset by their last arriver
-  uint64_t* part;    // [nchunks * kFusedWords]
-  uint64_t* tot;     // [nls * kFusedWords]
-  uint32_t* err;     // host-mapped word: a bounded wait gave up (residency bound violated)
-  int32_t nchunks;
-  uint32_t epoch;    // launch number, never 0: the value a phase's flag takes when its totals are out
-  uint32_t spin_limit;  // polls (s_sleep 8 each) before a wait gives up
-};
-
-// Persistent large path (k_large_flow, dm_flow.hip): the chain's phases as tasks of
-// one launch.  A task word is phase << 30 | chunk: phase 0 = pass A (Clean + the
-// speculative round 1) of one chunk, 1 = round 1 again (only where Clean released
-// subclients, or recompute mode) for up to kFlowBundle chunks from that one, 2 =
-// FairShare round 2 of one chunk, 3 = the map of one chunk (its resource's last
-// chunk to finish writes the record).  Workgroups take tasks in list order from a
-// ticket counter; a task only waits for tasks earlier in the list (its resource's
-// previous phases), which running workgroups already hold, so the queue drains
-// with any number of resident workgroups (no co-residency bound).
-constexpr int kFlowBundle = 8;
-constexpr uint32_t kFlowA = 0u, kFlowB = 1u, kFlowC = 2u, kFlowM = 3u;
-struct FlowState {
-  const uint32_t* tasks;   // [ntasks], dependencies before dependants
-  const Chunk* chunks;     // the chain's chunks (kChunkRows rows)
-  const LargeSeg* large;
-  uint32_t* ticket;        // [2]: launch epoch parity picks one, block 0 clears the other
-  uint32_t* sync;          // [nls * kFusedSync] arrive counters (reset by their last arriver) + phase flags
-  uint64_t* part;          // [nchunks * kFusedWords] per-chunk records (dm_records.h)
-  uint64_t* tot;           // [nls * kFusedWords] per-resource totals
-  uint32_t* live;          // [nchunks * 256] pass A's row masks per thread (live | expl << 8 | rel << 16)
-  uint32_t* err;           // host-mapped word: a bounded wait gave up
-  int32_t ntasks;
-  uint32_t epoch;          // launch number, never 0
-  uint32_t spin_limit;
-  int32_t batch;           // consecutive tickets a workgroup takes per counter add (>= 1)
 };
 
 // row -> resource lookup for store updates: seg_off plus, for every block of
@@ -311,6 +261,8 @@ struct HierArgs {
   const ResCold* root_cold; // the root's safe capacity / refresh interval
   int64_t R;
   int64_t leaf_lo;          // first resource of this server's leaf (0 when replicated)
+  int64_t r_lo, r_hi;       // the resources this launch decides: this server's own range when
+                            // sharded (no other server's leaf reads the rest), else [0, R)
   int G;                    // servers
   int K;                    // root rows per resource: G (replicated) or 1 (sharded: its owner's)
   int server;

@@ -2128,7 +2128,10 @@ __global__ __launch_bounds__(256) void k_publish(int64_t R, const ResAgg* __rest
 // store has K = G rows per resource (row r*G + g = server g); sharded -- server g
 // holds resources [lo[g], lo[g+1]) (contiguous resource-id ranges),
 // so only the owner ever requests resource r and the root store has one row per
-// resource (K = 1).  A server whose published flags are set (a band with
+// resource (K = 1); there each rank decides only its own range [r_lo, r_hi): no
+// other server requests those resources and no other resource's root rows reach this
+// server's leaf, so the launch shrinks with the shard (the other ranks decide theirs).
+// A server whose published flags are set (a band with
 // num_clients < 1, server.go:863-866, or a Count beyond 2^31 - 2) requests nothing
 // this round.
 //
@@ -2167,10 +2170,10 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < ha.G)  // the round's per-server flags (dm_hier_status)
     ha.status_out[threadIdx.x] = (uint32_t)__double_as_longlong(ha.gathered[(int64_t)threadIdx.x * ha.stride].x);
-  const int64_t r = wave * per + rl;
-  if (wave * per >= ha.R) return;  // whole waves only
-  const bool valid = g0 < K && r < ha.R;
-  const int64_t rr = r < ha.R ? r : 0;
+  const int64_t r = ha.r_lo + wave * per + rl;
+  if (ha.r_lo + wave * per >= ha.r_hi) return;  // whole waves only
+  const bool valid = g0 < K && r < ha.r_hi;
+  const int64_t rr = r < ha.r_hi ? r : ha.r_lo;
   const int64_t row = rr * K + (valid ? g0 : 0);
   // the server this row belongs to, and its record of the resource
   const int g = ha.shard_lo ? hier_owner(ha.shard_lo, ha.G, rr) : g0;
@@ -2586,7 +2589,8 @@ hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t 
   int P = 1;
   while (P < ha.K) P <<= 1;
   const int64_t per = 64 / P;
-  const int64_t waves = (ha.R + per - 1) / per;
+  // at least one workgroup: block 0 also writes the round's per-server flags
+  const int64_t waves = std::max<int64_t>(1, (ha.r_hi - ha.r_lo + per - 1) / per);
   k_hier_tick<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(p, ha);
   return hipGetLastError();
 }

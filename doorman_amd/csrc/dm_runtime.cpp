@@ -29,12 +29,6 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
                           hipStream_t st);
-hipError_t launch_large_fused(int G, const DevParams& p, const Chunk* chunks, const LargeSeg* ls, const FusedState& F,
-                              int32_t* glist, int32_t* gcount, hipStream_t st);
-hipError_t large_fused_occupancy(int G, int* blocks_per_cu);
-hipError_t launch_large_flow(const DevParams& p, const FlowState& F, int grid, int32_t* glist, int32_t* gcount,
-                             hipStream_t st);
-hipError_t large_flow_occupancy(int* blocks_per_cu);
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int32_t* sub32, const int64_t* expiry, const ResCfg* cfg, int64_t now,
                          const RowIndex& ix, double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp,
@@ -80,7 +74,6 @@ enum KClass {
   KC_GENERAL,
   KC_UPSERT,
   KC_RELEASE,
-  KC_LARGE_FUSED,
   KC_SUBS,
   KC_DENSE3,  // the workgroup bins' split form (bins 3-6): dense kernel, then the rest kernel
   KC_DENSE4,
@@ -96,19 +89,19 @@ enum KClass {
   KC_LARGE_CH,  // bucket partials,
   KC_LARGE_E,   // bucket totals,
   KC_LARGE_MH,  // the map
-  KC_LARGE_FLOW,  // the persistent large path (dm_flow.hip)
   KC_COUNT
 };
+// bin 6 (2049-4096 rows) runs on 256 x 16 or 512 x 8 workgroups (kBin6Wide):
+// "block2k4k" names the bin, dm_plan_info says which shape ran
 const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
-                                     "block128x8",   "block256x8", "block512x8",  "sub8x2",    "sub16x2",
+                                     "block128x8",   "block256x8", "block2k4k",  "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
-                                     "store_release", "large_fused", "subs_merged", "block128x4_dense",
-                                     "block128x8_dense", "block256x8_dense", "block512x8_dense",
-                                     "block128x4_rest", "block128x8_rest", "block256x8_rest", "block512x8_rest",
+                                     "store_release", "subs_merged", "block128x4_dense",
+                                     "block128x8_dense", "block256x8_dense", "block2k4k_dense",
+                                     "block128x4_rest", "block128x8_rest", "block256x8_rest", "block2k4k_rest",
                                      "hier_publish",
-                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het",
-                                     "large_flow"};
+                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het"};
 
 template <typename T>
 struct DBuf {
@@ -223,7 +216,6 @@ struct dm_ctx {
 
   int64_t R = 0, N = 0;
   bool store_loaded = false, cfg_loaded = false;
-  bool store_lost = false;  // a failed fused writeback tick wrote part of the store (check_fused)
   // the store may hold explicit-expiry rows: set by every call that can write one
   // (load, upserts, decide, the root's tick), cleared by a writeback tick (which
   // turns every live explicit row into a follower).  Without them pass A's
@@ -281,8 +273,6 @@ struct dm_ctx {
   DBuf<WorkItem> bins[kNumBins];
   DBuf<Chunk> chunks;
   DBuf<LargeSeg> large;
-  // one-launch large path (dm_large.hip): its own chunking (fused_G * kFusedRows rows)
-  int large_mode = DM_LARGE_CHAIN;
   // the sub-wave bins in one launch (k_subs; DM_MERGE_SUBS=0: one launch per bin):
   // C2 tick 144-145 -> 138 us (tools/ab.py, both orders, one box)
   bool merge_subs = true;
@@ -302,30 +292,6 @@ struct dm_ctx {
   bool bin6_wide = false;  // bin 6 on 512 x 8 workgroups (kBin6Wide): it holds most of the rows
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
-  int fused_G = 512;
-  bool fused_ok = false;       // every large resource within the co-residency bound
-  int64_t fused_max_chunks = 0, fused_cap = 0;
-  uint32_t fused_epoch = 0;
-  uint32_t fused_spin_limit = 1u << 21;  // x s_sleep 8 (~512 clocks): ~0.4 s, far beyond any real wait
-  std::vector<Chunk> h_fchunks;
-  std::vector<LargeSeg> h_flarge;
-  DBuf<Chunk> fchunks;
-  DBuf<LargeSeg> flarge;
-  DBuf<uint32_t> f_ticket, f_sync;
-  DBuf<uint64_t> f_part, f_tot;
-  uint32_t* h_ferr = nullptr;  // host-mapped: a fused wait gave up
-  uint32_t* d_ferr = nullptr;
-  bool use_fused() const { return large_mode == DM_LARGE_FUSED && fused_ok && !h_fchunks.empty(); }
-  // persistent large path (dm_flow.hip): the chain's chunks, phases as listed tasks
-  std::vector<uint32_t> h_fl_tasks;
-  DBuf<uint32_t> fl_tasks, fl_ticket, fl_sync;
-  DBuf<uint64_t> fl_part, fl_tot;
-  int fl_grid = 0;          // workgroups of the persistent launch
-  int fl_wg_per_cu = 2;     // DM_FLOW_WG: resident workgroups per CU it asks for
-  int fl_lag = -1;          // DM_FLOW_LAG: list distance between a phase and the next (-1: the grid)
-  int fl_batch = 1;         // DM_FLOW_BATCH: tickets per counter add
-  int fl_grid_force = 0;    // DM_FLOW_GRID: exact grid (tests run the queue on one or a few workgroups)
-  uint32_t fl_epoch = 0;
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
@@ -449,11 +415,6 @@ struct dm_ctx {
     agg.release(); expl.release(); cfg.release(); cold.release();
     out_gets.release(); out_expiry.release(); res.release();
     packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
-    fchunks.release(); flarge.release(); f_ticket.release(); f_sync.release(); f_part.release(); f_tot.release();
-    fl_tasks.release(); fl_ticket.release(); fl_sync.release(); fl_part.release(); fl_tot.release();
-    if (h_ferr) (void)hipHostFree(h_ferr);
-    h_ferr = nullptr;
-    d_ferr = nullptr;
     for (int i = 0; i < kSplitBins; ++i) {
       dq_list[i].release();
       dq_cnt[i].release();
@@ -536,9 +497,6 @@ static void build_plan(dm_ctx* c) {
   for (auto& b : c->h_bins) b.clear();
   c->h_chunks.clear();
   c->h_large.clear();
-  c->h_fchunks.clear();
-  c->h_flarge.clear();
-  const int64_t frows = (int64_t)c->fused_G * kFusedRows;
   const std::vector<int64_t>& off = c->h_seg_off;
   Pack cur{};
   bool open = false;
@@ -574,45 +532,9 @@ static void build_plan(dm_ctx* c) {
       }
       L.chunk_end = (int32_t)c->h_chunks.size();
       c->h_large.push_back(L);
-      LargeSeg F{(int32_t)r, (int32_t)c->h_fchunks.size(), 0, 0};
-      for (int64_t o = off[r]; o < off[r + 1]; o += frows) {
-        Chunk ch{(int32_t)r, (int32_t)c->h_flarge.size(), o, (int32_t)std::min<int64_t>(frows, off[r + 1] - o), 0};
-        c->h_fchunks.push_back(ch);
-      }
-      F.chunk_end = (int32_t)c->h_fchunks.size();
-      c->h_flarge.push_back(F);
     }
   }
   close();
-}
-
-// The persistent large path's task list (dm_flow.hip): every task after the tasks
-// it waits for.  Keys in units of list positions: pass A of chunk q at q; a
-// resource's round-1 bundles `lag` after its last pass-A task, its round-2 tasks
-// after those, its map tasks `lag` after its last round-2 task -- so a dependent task
-// is taken about one grid's worth of tasks after what it needs (rarely waiting), and
-// the rows it re-reads were read a short while before (Infinity Cache).
-static void build_flow_tasks(dm_ctx* c, int64_t lag) {
-  struct K {
-    int64_t key;
-    uint32_t ph;
-    int32_t q;
-  };
-  std::vector<K> v;
-  v.reserve(c->h_chunks.size() * 3 + c->h_large.size() * 2);
-  for (const LargeSeg& L : c->h_large) {
-    const int64_t f = L.chunk_begin, l = L.chunk_end, n = l - f;
-    for (int64_t q = f; q < l; ++q) v.push_back(K{q, kFlowA, (int32_t)q});
-    const int64_t kb = l - 1 + lag;
-    for (int64_t q = f; q < l; q += kFlowBundle) v.push_back(K{kb, kFlowB, (int32_t)q});
-    for (int64_t q = f; q < l; ++q) v.push_back(K{kb + 1 + (q - f), kFlowC, (int32_t)q});
-    for (int64_t q = f; q < l; ++q) v.push_back(K{kb + 1 + n + lag + (q - f), kFlowM, (int32_t)q});
-  }
-  std::stable_sort(v.begin(), v.end(), [](const K& a, const K& b) {
-    return a.key != b.key ? a.key < b.key : (a.ph != b.ph ? a.ph < b.ph : a.q < b.q);
-  });
-  c->h_fl_tasks.resize(v.size());
-  for (size_t i = 0; i < v.size(); ++i) c->h_fl_tasks[i] = v[i].ph << 30 | (uint32_t)v[i].q;
 }
 
 static int upload_plan(dm_ctx* c) {
@@ -621,33 +543,6 @@ static int upload_plan(dm_ctx* c) {
   for (int b = 0; b < kNumBins; ++b) DM_HIP(c, upload(c->bins[b], c->h_bins[b].data(), c->h_bins[b].size(), st), "plan bins");
   DM_HIP(c, upload(c->chunks, c->h_chunks.data(), c->h_chunks.size(), st), "plan chunks");
   DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
-  {  // one-launch large path: chunks, hand-off state, co-residency bound
-    DM_HIP(c, upload(c->fchunks, c->h_fchunks.data(), c->h_fchunks.size(), st), "plan fused chunks");
-    DM_HIP(c, upload(c->flarge, c->h_flarge.data(), c->h_flarge.size(), st), "plan fused large");
-    const size_t nf = std::max<size_t>(c->h_fchunks.size(), 1), nl = std::max<size_t>(c->h_flarge.size(), 1);
-    DM_HIP(c, c->f_ticket.ensure(4), "fused state");
-    DM_HIP(c, c->f_sync.ensure(nl * kFusedSync), "fused state");
-    DM_HIP(c, c->f_part.ensure(nf * kFusedWords), "fused state");
-    DM_HIP(c, c->f_tot.ensure(nl * kFusedWords), "fused state");
-    DM_HIP(c, hipMemsetAsync(c->f_ticket.p, 0, 4 * sizeof(uint32_t), st), "fused state");
-    DM_HIP(c, hipMemsetAsync(c->f_sync.p, 0, nl * kFusedSync * sizeof(uint32_t), st), "fused state");
-    if (!c->h_ferr) {
-      DM_HIP(c, hipHostMalloc((void**)&c->h_ferr, sizeof(uint32_t), hipHostMallocMapped), "fused error word");
-      *c->h_ferr = 0;
-      DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_ferr, c->h_ferr, 0), "fused error word");
-    }
-    c->fused_max_chunks = 0;
-    for (const LargeSeg& L : c->h_flarge)
-      c->fused_max_chunks = std::max<int64_t>(c->fused_max_chunks, L.chunk_end - L.chunk_begin);
-    int per_cu = 0, cus = 0;
-    DM_HIP(c, large_fused_occupancy(c->fused_G, &per_cu), "fused occupancy");
-    DM_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "CU count");
-    c->fused_cap = (int64_t)per_cu * cus;
-    // half the resident workgroups: room for a second process's fused launch on
-    // the same device (dm_large.hip, co-residency)
-    c->fused_ok = c->fused_max_chunks > 0 && 2 * c->fused_max_chunks <= c->fused_cap &&
-                  c->fused_max_chunks <= c->fused_G;  // the last arriver loads one record per thread
-  }
   if (!c->h_dq) {
     DM_HIP(c, hipHostMalloc((void**)&c->h_dq, dm_ctx::kSplitBins * sizeof(int32_t), hipHostMallocMapped), "dense split word");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_dq, c->h_dq, 0), "dense split word");
@@ -668,21 +563,6 @@ static int upload_plan(dm_ctx* c) {
     c->dq_par[i] = 0;
   }
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
-  {  // persistent large path: grid, task list, hand-off state
-    int per_cu = 0, cus = 0;
-    DM_HIP(c, large_flow_occupancy(&per_cu), "flow occupancy");
-    DM_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "CU count");
-    c->fl_grid = c->fl_grid_force > 0 ? c->fl_grid_force : std::max(1, std::min(per_cu, c->fl_wg_per_cu) * cus);
-    build_flow_tasks(c, c->fl_lag >= 0 ? c->fl_lag : c->fl_grid);
-    const size_t nl = std::max<size_t>(c->h_large.size(), 1);
-    DM_HIP(c, upload(c->fl_tasks, c->h_fl_tasks.data(), c->h_fl_tasks.size(), st), "flow tasks");
-    DM_HIP(c, c->fl_ticket.ensure(2), "flow state");
-    DM_HIP(c, c->fl_sync.ensure(nl * kFusedSync), "flow state");
-    DM_HIP(c, c->fl_part.ensure(nc * kFusedWords), "flow state");
-    DM_HIP(c, c->fl_tot.ensure(nl * kFusedWords), "flow state");
-    DM_HIP(c, hipMemsetAsync(c->fl_ticket.p, 0, 2 * sizeof(uint32_t), st), "flow state");
-    DM_HIP(c, hipMemsetAsync(c->fl_sync.p, 0, nl * kFusedSync * sizeof(uint32_t), st), "flow state");
-  }
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
   DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
   DM_HIP(c, c->pa_has_all.ensure(nc), "partials");
@@ -736,33 +616,6 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
   return hipMemcpyAsync(dst, src + off, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, st);
 }
 
-// A wait of the one-launch large path gave up (its co-residency bound was
-// violated, e.g. by other processes' launches on the same device): the tick's
-// large-resource results are not valid.
-// A fused tick whose in-launch hand-off gave up: its leases are invalid, and a
-// writeback tick may have written part of the store (chunks that got their totals
-// wrote their rows), so the store is unusable until the next dm_store_load.
-static int check_fused(dm_ctx* c) {
-  if (c->h_ferr && __atomic_load_n(c->h_ferr, __ATOMIC_ACQUIRE)) {
-    __atomic_store_n(c->h_ferr, 0u, __ATOMIC_RELEASE);
-    // arrive counters of the gave-up launch were left part-way: start the next from zero
-    (void)hipStreamSynchronize(c->stream);
-    if (c->f_sync.p) (void)hipMemset(c->f_sync.p, 0, c->f_sync.n * sizeof(uint32_t));
-    if (c->fl_sync.p) (void)hipMemset(c->fl_sync.p, 0, c->fl_sync.n * sizeof(uint32_t));
-    if (c->fl_ticket.p) (void)hipMemset(c->fl_ticket.p, 0, c->fl_ticket.n * sizeof(uint32_t));
-    if (c->f_ticket.p) (void)hipMemset(c->f_ticket.p, 0, c->f_ticket.n * sizeof(uint32_t));
-    c->have_result = false;  // the tick's leases are invalid
-    if (c->last_writeback) {
-      c->store_lost = true;
-      return c->fail(DM_E_HIP, "large-resource hand-off timed out (too few resident workgroups) in a writeback "
-                               "tick: the store is partly written and must be reloaded (dm_store_load); use "
-                               "dm_set_large_path(ctx, DM_LARGE_CHAIN)");
-    }
-    return c->fail(DM_E_HIP, "large-resource hand-off timed out (too few resident workgroups); the tick's leases "
-                             "are invalid -- retry with dm_set_large_path(ctx, DM_LARGE_CHAIN)");
-  }
-  return DM_OK;
-}
 
 // ---------------------------------------------------------------------------
 // C-ABI
@@ -842,20 +695,12 @@ int dm_create(int device, dm_ctx** out) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
   }
-  if (const char* g = getenv("DM_FUSED_G")) c->fused_G = atoi(g) == 256 ? 256 : 512;  // A/B of the chunk shape
-  if (const char* lp = getenv("DM_LARGE_PATH")) c->large_mode = atoi(lp);  // A/B: 0 chain, 1 fused, 2 flow
-  if (const char* fw = getenv("DM_FLOW_WG")) c->fl_wg_per_cu = std::max(1, atoi(fw));
-  if (const char* fl = getenv("DM_FLOW_LAG")) c->fl_lag = atoi(fl);
-  if (const char* fb = getenv("DM_FLOW_BATCH")) c->fl_batch = std::max(1, atoi(fb));
-  if (const char* fg = getenv("DM_FLOW_GRID")) c->fl_grid_force = std::max(0, atoi(fg));  // tests: tiny grids
   if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
     for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
       const int d = sp[i] >= 'a' ? sp[i] - 'a' + 10 : sp[i] - '0';
       if (d < 0 || d >= dm_ctx::kAux) break;
       c->class_stream[i] = d;
     }
-  // test hook: a tiny bound makes the fused path's waits give up (tests/test_large_gpu.py)
-  if (const char* sl = getenv("DM_FUSED_SPIN_LIMIT")) c->fused_spin_limit = (uint32_t)strtoul(sl, nullptr, 10);
   e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -987,14 +832,6 @@ int dm_sync(dm_ctx* c) {
   DM_ENTER(c);
   DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   c->collect_profile();
-  return check_fused(c);
-}
-
-int dm_set_large_path(dm_ctx* c, int mode) {
-  DM_ENTER(c);
-  if (mode != DM_LARGE_CHAIN && mode != DM_LARGE_FUSED && mode != DM_LARGE_FLOW)
-    return c->fail(DM_E_INVAL, "unknown large-path mode");
-  c->large_mode = mode;
   return DM_OK;
 }
 
@@ -1084,7 +921,6 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     c->all_sub_one = s->subclients[i] == 1 || s->expiry_ns[i] == DM_RELEASED;
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
-  c->store_lost = false;
   c->expl_rows = true;
   c->chain_live_ok = false;
   c->have_result = false;
@@ -1130,7 +966,6 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
 
 static int ready(dm_ctx* c) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!c->cfg_loaded || (int64_t)c->h_refresh_s.size() != c->R)
     return c->fail(DM_E_STATE, "no configuration loaded for the store's resources");
   return DM_OK;
@@ -1257,21 +1092,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, c->xs_wait(fk, c->aux[i]), "fork");
     c->main_dirty = false;
   }
-  if (nch > 0 && c->use_fused()) {
-    c->fused_epoch = c->fused_epoch + 1 == 0 ? 1 : c->fused_epoch + 1;
-    const FusedState F{c->f_ticket.p, c->f_sync.p, c->f_part.p, c->f_tot.p, c->d_ferr,
-                       (int32_t)c->h_fchunks.size(), c->fused_epoch, c->fused_spin_limit};
-    DM_HIP(c, timed(KC_LARGE_FUSED, s_large,
-                    [&] { return launch_large_fused(c->fused_G, p, c->fchunks.p, c->flarge.p, F, gl, gc, s_large); }),
-           "large-resource kernel");
-  } else if (nch > 0 && c->large_mode == DM_LARGE_FLOW && !general) {
-    c->fl_epoch = c->fl_epoch + 1 == 0 ? 1 : c->fl_epoch + 1;
-    const FlowState F{c->fl_tasks.p, c->chunks.p, c->large.p, c->fl_ticket.p, c->fl_sync.p, c->fl_part.p,
-                      c->fl_tot.p, c->pa_live.p, c->d_ferr, (int32_t)c->h_fl_tasks.size(), c->fl_epoch,
-                      c->fused_spin_limit, c->fl_batch};
-    DM_HIP(c, timed(KC_LARGE_FLOW, s_large, [&] { return launch_large_flow(p, F, c->fl_grid, gl, gc, s_large); }),
-           "large-resource kernel");
-  } else {
+  {
     const int nls = (int)c->h_large.size();
     // heterogeneous-subclient FairShare is decided on the chain when the store may
     // hold it (k_large_t, k_large_c_het, k_large_e, k_large_map_het)
@@ -1391,7 +1212,6 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (!(flags & DM_ASYNC)) {
     DM_HIP(c, hipStreamSynchronize(st), "tick");
     c->collect_profile();
-    if ((rc = check_fused(c))) return rc;
   }
   return DM_OK;
 }
@@ -1607,7 +1427,6 @@ int dm_read_config(dm_ctx* c, int64_t r0, int64_t n, int32_t* kind, double* capa
 int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants, int64_t* sub, int64_t* exp) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
   DM_HIP(c, download(has, (const double*)c->has.p, off, n, c->stream), "read has");
@@ -1690,7 +1509,6 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
                     const int64_t* sub, const int64_t* exp) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
   c->expl_rows = true;
@@ -1721,7 +1539,6 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
 int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
@@ -1747,7 +1564,6 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
                                const double* wants) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (first_row < 0 || (first_row & 63) || nwords < 0 || n < 0 || (nwords > 0 && !mask) || (n > 0 && !wants))
     return c->fail(DM_E_INVAL, "bad masked update (first_row must be a multiple of 64)");
   if (nwords == 0) return n == 0 ? DM_OK : c->fail(DM_E_INVAL, "packed values without a mask");
@@ -1785,7 +1601,6 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
 int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
   c->chain_live_ok = false;
@@ -1811,7 +1626,6 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
 int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!b) return c->fail(DM_E_INVAL, "null batch");
   const int64_t nw = b->wants_nwords, nm = b->wants_n, nr = b->release_n, nu = b->upsert_n;
   if (nw < 0 || nm < 0 || nr < 0 || nu < 0) return c->fail(DM_E_INVAL, "negative batch sizes");
@@ -1967,7 +1781,6 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
 int dm_publish_totals(dm_ctx* c, void* dst) {
   DM_ENTER(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
   if (!c->pub_sync.p) {
     DM_HIP(c, c->pub_sync.ensure(2), "publish state");
@@ -2125,6 +1938,11 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   ha.root_cold = root->cold.p;
   ha.R = root->R;
   ha.leaf_lo = leaf_lo;
+  // Sharded: only this server ever requests its resources (server.go:234-255), and its
+  // leaf reads only their templates, so the round is decided over its own range; the
+  // root copy's other rows are the other ranks' (each decides its own range).
+  ha.r_lo = sharded ? leaf_lo : 0;
+  ha.r_hi = sharded ? leaf_lo + leaf_R : root->R;
   ha.G = n_servers;
   ha.K = K;
   ha.server = server;
@@ -2192,20 +2010,14 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[11 + kNumBins];
+  int64_t v[5 + kNumBins];
   v[0] = (int64_t)c->h_packs.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
   v[2 + kNumBins] = (int64_t)c->h_chunks.size();
   v[3 + kNumBins] = c->N;
-  v[4 + kNumBins] = c->use_fused() ? 1 : 0;
-  v[5 + kNumBins] = (int64_t)c->h_fchunks.size();
-  v[6 + kNumBins] = c->fused_max_chunks;
-  v[7 + kNumBins] = c->fused_cap;
-  v[8 + kNumBins] = (c->large_mode == DM_LARGE_FLOW && !c->h_chunks.empty()) ? 1 : 0;
-  v[9 + kNumBins] = c->fl_grid;
-  v[10 + kNumBins] = (int64_t)c->h_fl_tasks.size();
-  const int n = 11 + kNumBins;
+  v[4 + kNumBins] = c->bin6_wide ? 1 : 0;  // bin 6 on 512 x 8 workgroups (else 256 x 16)
+  const int n = 5 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }
@@ -2214,7 +2026,6 @@ int dm_store_stats(dm_ctx* c, int64_t* out, int max) {
   DM_ENTER(c);
   if (!out || max < 0) return c->fail(DM_E_INVAL, "bad output buffer");
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
-  if (c->store_lost) return c->fail(DM_E_STATE, "the store was lost by a failed writeback tick; reload it");
   std::vector<uint8_t> ex((size_t)c->R);
   DM_HIP(c, download(ex.data(), (const uint8_t*)c->expl.p, 0, c->R, c->stream), "read row states");
   DM_HIP(c, hipStreamSynchronize(c->stream), "read row states");

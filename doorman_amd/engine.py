@@ -16,9 +16,7 @@ from ._lib import check, lib
 from .workloads import CFG_FIELDS
 
 _BIN_NAMES = ("small_packs", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8", "block256x8",
-              "block512x8", "sub8x2", "sub16x2", "large_resources", "large_chunks", "leases",
-              "large_fused", "fused_chunks", "fused_max_chunks", "fused_capacity", "large_flow", "flow_grid",
-              "flow_tasks")
+              "block2k4k", "sub8x2", "sub16x2", "large_resources", "large_chunks", "leases", "bin6_wide")
 
 
 def _ptr(a):
@@ -269,15 +267,6 @@ class Engine:
     def publish_totals(self, dev_ptr: int):
         """{SumWants, Count} per resource into a 16 B x R device buffer (server.go:234-255)."""
         self._chk(self._L.dm_publish_totals(self._ctx, ctypes.c_void_p(dev_ptr)))
-
-    LARGE_PATHS = {"chain": 0, "fused": 1, "flow": 2}
-
-    def set_large_path(self, fused: bool = False, path: str | None = None):
-        """Large resources: the five-launch chain, the one-launch path (DM_LARGE_FUSED,
-        when it fits the device's residency bound) or the persistent task-queue path
-        (DM_LARGE_FLOW).  `path` names one of them; `fused=True` is path="fused"."""
-        mode = self.LARGE_PATHS[path] if path is not None else (1 if fused else 0)
-        self._chk(self._L.dm_set_large_path(self._ctx, mode))
 
     # -- profiling --
     def set_profiling(self, on: bool):

@@ -318,38 +318,23 @@ int dm_hier_pipeline(dm_ctx* leaf, int on);
 #define DM_HIER_COUNT_RANGE 2u
 int dm_hier_status(dm_ctx* root, uint32_t* status, int n_servers);
 
-/* ---- large resources (more than 4096 rows) ----
- * DM_LARGE_CHAIN (default): 2048-row chunks in five stream-ordered launches (Clean
- * + speculative round 1, round 1 again where Clean released subclients, FairShare
- * round 2, the map, the resource records); every chunk re-derives the resource's
- * totals (algorithm.go:156-204, 259-279) from the previous launch's per-chunk
- * partials with one fixed tree.
- * DM_LARGE_FUSED: one launch in which every chunk keeps its rows in registers while
- * the chunks of a resource exchange those totals in-launch (one HBM pass); used
- * only when every large resource has at most half as many chunks as the device
- * keeps resident, else the chain runs.  Results are bit-identical; dm_plan_info
- * reports which path a tick takes.
- * DM_LARGE_FLOW: the chain's phases as tasks of one persistent launch (a fixed grid
- * takes listed tasks from a ticket counter; a task waits only for its resource's
- * earlier phases, listed before it), so no launch boundaries and each phase's
- * totals are reduced once per resource; no co-residency bound.  Ticks that may
- * hold heterogeneous-subclient FairShare resources use the chain.  Results agree
- * with the chain's within rounding (different reduction trees). */
-#define DM_LARGE_CHAIN 0
-#define DM_LARGE_FUSED 1
-#define DM_LARGE_FLOW 2
-int dm_set_large_path(dm_ctx* ctx, int mode);
+/* Large resources (more than 4096 rows) run on 2048-row chunks in stream-ordered
+ * launches (Clean + speculative round 1, round 1 again only where Clean released
+ * subclients, FairShare round 2, the map, whose last-arriving chunk per resource writes
+ * the record); every chunk re-derives the resource's totals (algorithm.go:156-204,
+ * 259-279) from the previous launch's per-chunk partials with one fixed tree.  (The
+ * one-launch and persistent-queue forms of rounds 2-3 lost to it and were retired in
+ * round 4: DESIGN.md §4.3.) */
 
 /* ---- profiling ---- */
 int dm_set_profiling(dm_ctx* ctx, int on);
 /* fills up to max entries; returns the number of kernel classes (>= 0) */
 int dm_kernel_times(dm_ctx* ctx, dm_kernel_time* out, int max);
 int dm_reset_kernel_times(dm_ctx* ctx);
-/* plan summary of the loaded store: counts per dispatch bin (small packs, 64x1,
- * 256x1..256x16, large resources, large chunks, leases), then whether ticks use
- * the one-launch large path, its chunks, the most chunks of one resource and the
- * device's resident-workgroup bound, then whether large resources take the
- * persistent path (DM_LARGE_FLOW), its grid and its listed tasks */
+/* plan summary of the loaded store: small packs, items per dispatch bin (sub16x4,
+ * sub32x4, wave64x4, block128x4, block128x8, block256x8, the 2049-4096-row bin,
+ * sub8x2, sub16x2), large resources, large chunks, leases, then 1 when the
+ * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16); returns 14 */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),

@@ -27,10 +27,54 @@ def test_kernel_units_cover_every_row_once():
     snap = W.make_snapshot(sizes, 1.0, 0.0, 1, W.NOW_NS + W.NS, W.FAIR_SHARE, 10.0)
     units = bench.kernel_units(snap)
     bins = ["small_packed", "sub8x2", "sub16x2", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8",
-            "block256x8", "block512x8", "large_a"]
+            "block256x8", "block2k4k", "large_a"]
     assert sum(units[b][0] for b in bins) == int(sizes.sum())
     assert sum(units[b][1] for b in bins) == len(sizes)
     # the merged sub-wave launch covers exactly the five sub-wave bins
     sub = ["sub8x2", "sub16x2", "sub16x4", "sub32x4", "wave64x4"]
     assert units["subs_merged"] == (sum(units[b][0] for b in sub), sum(units[b][1] for b in sub))
     assert units["block128x8"] == (513 + 1024, 2)
+
+
+def test_self_check_root_round_matches_the_reference_model():
+    """bench.root_round_one (the N > 1 exchange self-check's restatement of the sharded
+    root round, one row per resource) against the hierarchy model (tests/hier_model.py:
+    the oracle's literal Decide) over rounds with every kind, learning resources, an
+    expired parent, rows that lapse between rounds and resources left unrequested:
+    templates and grants bit for bit."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import hier_model as M
+    rng = np.random.default_rng(77)
+    R = 200
+    now = W.NOW_NS
+    cfg = {"kind": rng.integers(0, 4, R).astype(np.int32), "capacity": rng.choice([0.0, 5.0, 300.0, 1000.0], R),
+           "lease_length_s": rng.choice([1, 10, 20], R).astype(np.int64),
+           "refresh_interval_s": rng.choice([1, 5], R).astype(np.int64),
+           "learning_end_ns": np.where(rng.random(R) < 0.1, now + 3 * W.NS, W.INT64_MIN).astype(np.int64),
+           "parent_expiry_ns": np.where(rng.random(R) < 0.1, now + 2 * W.NS, W.INT64_MAX).astype(np.int64),
+           "safe_capacity": np.where(rng.random(R) < 0.3, 4.5, np.nan)}
+    model = M.Root(cfg, 1)
+    cols = [cfg[f] for f in ("kind", "capacity", "lease_length_s", "refresh_interval_s", "learning_end_ns",
+                             "parent_expiry_ns", "safe_capacity")]
+    checked = 0
+    for t in range(8):
+        now += int(rng.choice([0, 1, 4, 12])) * W.NS
+        sw = np.where(rng.random(R) < 0.8, rng.uniform(0.0, 2000.0, R), 0.0)
+        cnt = rng.integers(1, 6, R)
+        rows, sums = model.rows(), model.sums()
+        req = M.server_request(sw, cnt)
+        resp = model.round(now, [req])
+        tpl = M.leaf_templates(M.default_config(R), 0, resp, model.cfg)
+        for r in range(R):
+            got = bench.root_round_one(now, [c[r] for c in cols],
+                                       (rows["wants"][r], rows["has"][r], rows["subclients"][r], rows["expiry_ns"][r]),
+                                       (sums["count"][r], sums["sum_has"][r], sums["sum_wants"][r]), 0, sw[r],
+                                       int(cnt[r]))
+            want = tuple(np.asarray(tpl[f][r]).item() for f in bench._TPL_FIELDS)
+            assert np.asarray(got[0], dtype=object).tolist() == list(want) or all(
+                np.float64(a).tobytes() == np.float64(b).tobytes() for a, b in zip(got[0], want)), (t, r, got, want)
+            if (0, r) in resp:
+                assert np.float64(got[1]).tobytes() == np.float64(resp[(0, r)].has).tobytes(), (t, r)
+            checked += 1
+    assert checked == 8 * R
+    assert bench.root_round_one(now, [c[0] for c in cols], (0.0, 0.0, 0, W.RELEASED), (0, 0.0, 0.0), 1, 5.0, 1) is None

@@ -188,8 +188,8 @@ def test_sharded_pipelined_hierarchical_tick_two_processes():
     """bench.py's configs[3] path across processes: the resources of one snapshot
     sharded by id over two ranks, each an intermediate server of its range; every
     step a leaf tick, then the pipelined exchange (publish, all-gather, the root's
-    round over every resource on each rank, staged templates taken by the leaf tick
-    two steps later).  Root copies bit for bit against the model on both ranks,
+    round over each rank's own resources, staged templates taken by the leaf tick
+    two steps later).  Root copies bit for bit against the model on both ranks' ranges,
     templates bit for bit, leaf leases against the oracle under the templates the
     model says each tick used."""
     import torch.multiprocessing as mp
@@ -239,12 +239,13 @@ def test_sharded_pipelined_hierarchical_tick_two_processes():
         resp = model.round(now, reqs)
         rows, sums = model.rows(), model.sums()
         idx = np.arange(RS) * world + owner
-        for g in range(world):
+        for g in range(world):  # each rank decides the root round over its own range only
             got = res[g][t]["root"]
+            a, b = int(lo[g]), int(lo[g + 1])
             for k in ("has", "wants", "subclients", "expiry_ns"):
-                assert got[k].tobytes() == rows[k][idx].tobytes(), (t, g, k)
+                assert got[k][a:b].tobytes() == rows[k][idx][a:b].tobytes(), (t, g, k)
             for k in ("count", "sum_has", "sum_wants"):
-                assert got[k].tobytes() == sums[k].tobytes(), (t, g, k)
+                assert got[k][a:b].tobytes() == sums[k][a:b].tobytes(), (t, g, k)
         new = []
         for g in range(world):
             a, b = int(lo[g]), int(lo[g + 1])

@@ -506,13 +506,19 @@ def test_sharded_exchange_matches_the_reference_model(pipelined, large):
         for e in roots + leaves:
             e.sync()
         rows = _shard_rows(model, lo, R)
+        sums = model.sums()
         for g in range(G):
+            # each rank decides the root round over its own range only (the other ranks
+            # decide theirs): root copy g is compared on [lo[g], lo[g+1]), and the rows
+            # outside it must still be the loaded (all released) ones
+            a, b = int(lo[g]), int(lo[g + 1])
             st, res = roots[g].read_store(), roots[g].resources(safe=False)
             for k in ("has", "wants", "subclients", "expiry_ns"):
-                assert st[k].tobytes() == rows[k].tobytes(), f"step {t} root copy {g}: {k}"
-            sums = model.sums()
+                assert st[k][a:b].tobytes() == rows[k][a:b].tobytes(), f"step {t} root copy {g}: {k}"
+            assert np.all(st["expiry_ns"][:a] == W.RELEASED) and np.all(st["expiry_ns"][b:] == W.RELEASED), \
+                f"step {t} root copy {g} decided resources outside its range"
             for k in ("count", "sum_has", "sum_wants"):
-                assert res[k].tobytes() == sums[k].tobytes(), f"step {t} root copy {g}: running {k}"
+                assert res[k][a:b].tobytes() == sums[k][a:b].tobytes(), f"step {t} root copy {g}: running {k}"
         new = [tpl[g] if reqs[g] is None else _shard_templates(tpl[g], g, resp, model.cfg, lo) for g in range(G)]
         tpl = new
         if pipelined:

@@ -41,10 +41,7 @@ def main():
             var, _, val = kv.partition("=")
             os.environ[var] = val
         path, _, mode = p.partition(":")
-        os.environ["DM_FUSED_G"] = "256" if mode.endswith("256") else "512"
         e = Engine(0, os.path.abspath(path))
-        if mode.startswith("fused"):
-            e.set_large_path(fused=True)
         e.load(snap)
         for _ in range(5):
             e.apportion(W.NOW_NS, writeback=True)
