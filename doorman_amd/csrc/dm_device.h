@@ -225,7 +225,7 @@ struct DevParams {
 // decision's Assign before the next request is decided
 struct ReqItem {
   int32_t seg;
-  int32_t pad;
+  int32_t fast;  // 1 + its slot of the fast path (FastItem), 0: decided by k_decide only
   int64_t qlo, qhi;
   int64_t scr;
 };
@@ -240,6 +240,64 @@ struct ReqArgs {
   double* sc_has;
   double* sc_wants;
   int32_t* sc_sub;  // subclients of a live row, -1 for a row absent after Clean
+  const struct FastRes* fast;  // the fast path's verdict per slot (k_decide skips items it decided)
+};
+
+// dm_decide's fast path (dm_decide_fast.hip) for a resource with many requests in a
+// round whose requests keep every count (each requester a live row asking with the
+// subclients every live row holds): equalShare is then constant through the round,
+// FairShare round 1 / ProportionalShare's sums move by each Assign's own row only
+// (prefix scans over the requests), FairShare round 2 at each request's threshold is
+// a count / sum of the wants between deservedShare and T over the store as the earlier
+// Assigns left it (sorted wants + sorted per-block Assign events), and only
+// sumHas's recurrence (and ProportionalShare's sumWants test) stays sequential.
+constexpr int kFdMin = 64;       // requests on one resource before the fast path is tried
+constexpr int kFdBlock = 2048;   // requests per Assign-event block (2 events each)
+constexpr double kFdMaxAbs = 1e300;  // |wants| and |capacity| bound: no overflow in the sums
+constexpr int kFdChunk = 1024;   // scan elements per workgroup (4 per thread)
+struct FastItem {
+  int32_t item;  // index of the resource's ReqItem
+  int32_t nblk;  // event blocks: ceil(K / kFdBlock)
+  int64_t k0, K; // its requests [k0, k0 + K) of the round (grouped order)
+  int64_t m0;    // offset of its sorted-wants area (n + 1 entries)
+  int64_t e0;    // offset of its events (2 K)
+  int64_t b0;    // first event block (global block index)
+  int64_t n;     // rows of the resource
+};
+struct FdScan {  // one scanned element: double-double sums and an integer count
+  double xh, xl;  // FairShare: extra (sum of d - w for w < d); ProportionalShare: extraCapacity
+  double yh, yl;  // ProportionalShare: extraNeed
+  long long i;    // FairShare: wantExtra (subclients of rows with w > d)
+};
+struct FastRes {
+  int32_t ok;    // 1: the fast path decides this resource's requests
+  int32_t kind;
+  int32_t s0;    // the one subclients count
+  int32_t pad;
+  double C, eq, d;
+  long long count, nlive;
+  double sum_has, sum_wants;  // after Clean
+  FdScan init;                // the totals over the live rows before the round
+  int64_t exp_out;
+};
+struct FastArgs {
+  const FastItem* fi;
+  FastRes* fr;
+  const int64_t* prev;  // [n requests] the previous request of the round on the same row, or -1
+  double* pw;           // [n requests] the row's wants before the request
+  double* v;            // [n requests] the request's grant before the avail cap (FS), or PS's round-1 grant
+  FdScan* sc;           // [n requests] per-request deltas -> exclusive prefix (running totals)
+  double* keys;         // [sum n + 1] live wants (+inf for absent rows) -> sorted into keys_s
+  double* keys_s;
+  FdScan* ps;           // [sum n + 1] exclusive prefix sums of the sorted wants
+  double* ev_in;        // [sum 2K] Assign events: wants inserted (+1) / replaced (-1)
+  int32_t* evs_in;
+  double* ev;           // sorted within each block
+  int32_t* evs;
+  int32_t* ecnt;        // [blocks * (2 kFdBlock + 1)] exclusive prefix of the signs
+  double2* esum;        // ... and of sign * wants (double-double)
+  int32_t* bdc;         // [blocks] signed count / sum of the block's events <= d
+  double2* bds;
 };
 
 // dm_hier_root_tick: one exchange round of the hierarchy's root (k_hier_tick)

@@ -36,6 +36,7 @@ namespace dm {
 __global__ __launch_bounds__(256) void k_decide(DevParams p, const ReqItem* __restrict__ items, ReqArgs q) {
   __shared__ Lds<256> lds;
   const ReqItem it = items[blockIdx.x];
+  if (it.fast > 0 && q.fast[it.fast - 1].ok) return;  // decided by the fast path (dm_decide_fast.hip)
   const int seg = it.seg;
   const int64_t lo = p.seg_off[seg], hi = p.seg_off[seg + 1];
   const int64_t n = hi - lo;

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/doorman_hip.h"
@@ -53,6 +54,17 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
 hipError_t launch_decide(const DevParams& p, const ReqItem* items, int nitems, const ReqArgs& q, hipStream_t st);
+hipError_t fd_prep(const DevParams& p, const ReqItem* items, const ReqArgs& q, const FastArgs& fa, int nfast,
+                   hipStream_t st);
+hipError_t fd_item(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
+                   const FastArgs& fa, FdScan* part, hipStream_t st);
+hipError_t fd_item_sorted(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
+                          const FastArgs& fa, FdScan* part, hipStream_t st);
+hipError_t fd_sort_keys(void* temp, size_t* bytes, const double* in, double* out, int64_t n, int nseg,
+                        const int64_t* begin, const int64_t* end, hipStream_t st);
+hipError_t fd_sort_pairs(void* temp, size_t* bytes, const double* kin, double* kout, const int32_t* vin,
+                         int32_t* vout, int64_t n, int nseg, const int64_t* begin, const int64_t* end,
+                         hipStream_t st);
 hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t st);
 }  // namespace dm
 
@@ -89,6 +101,7 @@ enum KClass {
   KC_LARGE_CH,  // bucket partials,
   KC_LARGE_E,   // bucket totals,
   KC_LARGE_MH,  // the map
+  KC_DECIDE,    // dm_decide: the round's device work (fast path + k_decide)
   KC_COUNT
 };
 // bin 6 (2049-4096 rows) runs on 256 x 16 or 512 x 8 workgroups (kBin6Wide):
@@ -101,7 +114,7 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "block128x8_dense", "block256x8_dense", "block2k4k_dense",
                                      "block128x4_rest", "block128x8_rest", "block256x8_rest", "block2k4k_rest",
                                      "hier_publish",
-                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het"};
+                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het", "decide"};
 
 template <typename T>
 struct DBuf {
@@ -330,6 +343,16 @@ struct dm_ctx {
   DBuf<ReqItem> rq_items;
   DBuf<double> rq_sc_has, rq_sc_wants;  // the round's working copy of the requested resources' rows
   DBuf<int32_t> rq_sc_sub;
+  // dm_decide's fast path (dm_decide_fast.hip); DM_DECIDE_FAST=0 turns it off
+  bool decide_fast = true;
+  DBuf<FastItem> fd_items;
+  DBuf<FastRes> fd_res;
+  DBuf<int64_t> fd_prev, fd_bounds;
+  DBuf<double> fd_pw, fd_v, fd_keys, fd_keys_s, fd_ev_in, fd_ev;
+  DBuf<FdScan> fd_sc, fd_ps, fd_part;
+  DBuf<int32_t> fd_evs_in, fd_evs, fd_ecnt, fd_bdc;
+  DBuf<double2> fd_esum, fd_bds;
+  DBuf<uint8_t> fd_tmp;
   // dm_publish_totals: the workgroups' validation flags and their arrival counter
   // (k_publish; both return to zero after each launch)
   DBuf<uint32_t> pub_sync;
@@ -440,6 +463,10 @@ struct dm_ctx {
     }
     rq_rows.release(); rq_sub.release(); rq_exp.release(); rq_has.release(); rq_wants.release(); rq_gets.release();
     rq_items.release(); rq_sc_has.release(); rq_sc_wants.release(); rq_sc_sub.release();
+    fd_items.release(); fd_res.release(); fd_prev.release(); fd_bounds.release(); fd_pw.release(); fd_v.release();
+    fd_keys.release(); fd_keys_s.release(); fd_ev_in.release(); fd_ev.release(); fd_sc.release(); fd_ps.release();
+    fd_part.release(); fd_evs_in.release(); fd_evs.release(); fd_ecnt.release(); fd_bdc.release(); fd_esum.release();
+    fd_bds.release(); fd_tmp.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
   }
@@ -691,6 +718,7 @@ int dm_create(int device, dm_ctx** out) {
   dm_ctx* c = new dm_ctx();
   c->device = device;
   if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
+  if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1257,6 +1285,40 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
     }
     items.back().qhi = i + 1;
   }
+  // Resources with many requests try the fast path (dm_decide_fast.hip): per request
+  // the previous request of the round on the same row (its Assign is what the row
+  // holds then), per resource its scan / sort areas.  The device decides whether the
+  // round qualifies (FastRes::ok); k_decide takes every item it does not.
+  std::vector<FastItem> fitems;
+  std::vector<int64_t> prev;
+  int64_t m_off = 0, e_off = 0, b_off = 0;
+  for (size_t ii = 0; c->decide_fast && ii < items.size(); ++ii) {
+    ReqItem& itm = items[ii];
+    const int64_t K = itm.qhi - itm.qlo;
+    if (K < kFdMin) continue;
+    if (prev.empty()) prev.assign((size_t)n, -1);
+    FastItem f{};
+    f.item = (int32_t)ii;
+    f.k0 = itm.qlo;
+    f.K = K;
+    f.n = c->h_seg_off[itm.seg + 1] - c->h_seg_off[itm.seg];
+    f.nblk = (int32_t)((K + kFdBlock - 1) / kFdBlock);
+    f.m0 = m_off;
+    f.e0 = e_off;
+    f.b0 = b_off;
+    m_off += f.n + 1;
+    e_off += 2 * K;
+    b_off += f.nblk;
+    itm.fast = (int32_t)fitems.size() + 1;
+    fitems.push_back(f);
+    std::unordered_map<int64_t, int64_t> last;
+    last.reserve((size_t)(2 * K));
+    for (int64_t k = itm.qlo; k < itm.qhi; ++k) {
+      auto f2 = last.find(srows[(size_t)k]);
+      if (f2 != last.end()) prev[(size_t)k] = f2->second;
+      last[srows[(size_t)k]] = k;
+    }
+  }
   hipStream_t st = c->stream;
   DM_HIP(c, upload(c->rq_rows, srows.data(), (size_t)n, st), "stage requests");
   DM_HIP(c, upload(c->rq_has, shas.data(), (size_t)n, st), "stage requests");
@@ -1279,9 +1341,88 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   p.expl = c->expl.p;
   p.now = now_ns;
   p.recompute = 0;
+  const int nfast = (int)fitems.size();
+  FastArgs fa{};
+  const int64_t* d_kb = nullptr;
+  const int64_t *d_ke = nullptr, *d_eb = nullptr, *d_ee = nullptr;
+  int neb = 0;
+  size_t need = 0, need2 = 0;
+  if (nfast > 0) {
+    DM_HIP(c, upload(c->fd_items, fitems.data(), fitems.size(), st), "fast path");
+    DM_HIP(c, upload(c->fd_prev, prev.data(), prev.size(), st), "fast path");
+    DM_HIP(c, c->fd_res.ensure((size_t)nfast), "fast path");
+    DM_HIP(c, c->fd_pw.ensure((size_t)n), "fast path");
+    DM_HIP(c, c->fd_v.ensure((size_t)n), "fast path");
+    DM_HIP(c, c->fd_sc.ensure((size_t)n), "fast path");
+    DM_HIP(c, c->fd_keys.ensure((size_t)m_off), "fast path");
+    DM_HIP(c, c->fd_keys_s.ensure((size_t)m_off), "fast path");
+    DM_HIP(c, c->fd_ps.ensure((size_t)m_off), "fast path");
+    DM_HIP(c, c->fd_ev_in.ensure((size_t)e_off), "fast path");
+    DM_HIP(c, c->fd_evs_in.ensure((size_t)e_off), "fast path");
+    DM_HIP(c, c->fd_ev.ensure((size_t)e_off), "fast path");
+    DM_HIP(c, c->fd_evs.ensure((size_t)e_off), "fast path");
+    DM_HIP(c, c->fd_ecnt.ensure((size_t)(b_off * (2 * kFdBlock + 1))), "fast path");
+    DM_HIP(c, c->fd_esum.ensure((size_t)(b_off * (2 * kFdBlock + 1))), "fast path");
+    DM_HIP(c, c->fd_bdc.ensure((size_t)b_off), "fast path");
+    DM_HIP(c, c->fd_bds.ensure((size_t)b_off), "fast path");
+    int64_t most = 1;
+    for (const FastItem& f : fitems) most = std::max(most, std::max(f.K, f.n + 1));
+    DM_HIP(c, c->fd_part.ensure((size_t)((most + kFdChunk - 1) / kFdChunk)), "fast path");
+    // segment bounds of the sorts: each item's wants, each event block
+    std::vector<int64_t> kb, ke, eb, ee;
+    for (const FastItem& f : fitems) {
+      kb.push_back(f.m0);
+      ke.push_back(f.m0 + f.n);
+      for (int64_t b = 0; b < f.nblk; ++b) {
+        eb.push_back(f.e0 + 2 * b * kFdBlock);
+        ee.push_back(f.e0 + 2 * std::min<int64_t>(f.K, (b + 1) * kFdBlock));
+      }
+    }
+    neb = (int)eb.size();
+    std::vector<int64_t> bounds(kb);
+    bounds.insert(bounds.end(), ke.begin(), ke.end());
+    bounds.insert(bounds.end(), eb.begin(), eb.end());
+    bounds.insert(bounds.end(), ee.begin(), ee.end());
+    DM_HIP(c, upload(c->fd_bounds, bounds.data(), bounds.size(), st), "fast path");
+    d_kb = c->fd_bounds.p;
+    d_ke = d_kb + kb.size();
+    d_eb = d_ke + ke.size();
+    d_ee = d_eb + eb.size();
+    fa = FastArgs{c->fd_items.p, c->fd_res.p,    c->fd_prev.p, c->fd_pw.p,    c->fd_v.p,      c->fd_sc.p,
+                  c->fd_keys.p,  c->fd_keys_s.p, c->fd_ps.p,   c->fd_ev_in.p, c->fd_evs_in.p, c->fd_ev.p,
+                  c->fd_evs.p,   c->fd_ecnt.p,   c->fd_esum.p, c->fd_bdc.p,   c->fd_bds.p};
+    DM_HIP(c, fd_sort_keys(nullptr, &need, c->fd_keys.p, c->fd_keys_s.p, m_off, nfast, d_kb, d_ke, st), "fast path");
+    DM_HIP(c, fd_sort_pairs(nullptr, &need2, c->fd_ev_in.p, c->fd_ev.p, c->fd_evs_in.p, c->fd_evs.p, e_off, neb, d_eb,
+                            d_ee, st),
+           "fast path");
+    DM_HIP(c, c->fd_tmp.ensure(std::max<size_t>(std::max(need, need2), 1)), "fast path");
+  }
   const ReqArgs q{c->rq_rows.p, c->rq_has.p,     c->rq_wants.p,    c->rq_sub.p,   c->rq_gets.p,
-                  c->rq_exp.p,  c->rq_sc_has.p,  c->rq_sc_wants.p, c->rq_sc_sub.p};
-  DM_HIP(c, launch_decide(p, c->rq_items.p, (int)items.size(), q, st), "decide requests");
+                  c->rq_exp.p,  c->rq_sc_has.p,  c->rq_sc_wants.p, c->rq_sc_sub.p, nfast ? c->fd_res.p : nullptr};
+  // the device work of the round (one profiling class: dm_kernel_times "decide")
+  auto launches = [&]() -> hipError_t {
+    hipError_t e = hipSuccess;
+    if (nfast > 0) {
+      if ((e = fd_prep(p, c->rq_items.p, q, fa, nfast, st)) != hipSuccess) return e;
+      for (int s2 = 0; s2 < nfast; ++s2)
+        if ((e = fd_item(p, items[(size_t)fitems[(size_t)s2].item], fitems[(size_t)s2], s2, q, fa, c->fd_part.p,
+                         st)) != hipSuccess)
+          return e;
+      size_t t1 = c->fd_tmp.n, t2 = c->fd_tmp.n;
+      if ((e = fd_sort_keys(c->fd_tmp.p, &t1, c->fd_keys.p, c->fd_keys_s.p, m_off, nfast, d_kb, d_ke, st)) !=
+          hipSuccess)
+        return e;
+      if ((e = fd_sort_pairs(c->fd_tmp.p, &t2, c->fd_ev_in.p, c->fd_ev.p, c->fd_evs_in.p, c->fd_evs.p, e_off, neb,
+                             d_eb, d_ee, st)) != hipSuccess)
+        return e;
+      for (int s2 = 0; s2 < nfast; ++s2)
+        if ((e = fd_item_sorted(p, items[(size_t)fitems[(size_t)s2].item], fitems[(size_t)s2], s2, q, fa,
+                                c->fd_part.p, st)) != hipSuccess)
+          return e;
+    }
+    return launch_decide(p, c->rq_items.p, (int)items.size(), q, st);
+  };
+  DM_HIP(c, c->timed(KC_DECIDE, st, launches), "decide requests");
   DM_HIP(c, download(shas.data(), (const double*)c->rq_gets.p, 0, n, st), "read decisions");
   DM_HIP(c, download(ssub.data(), (const int64_t*)c->rq_exp.p, 0, n, st), "read decisions");
   DM_HIP(c, hipStreamSynchronize(st), "decide requests");

@@ -395,3 +395,158 @@ def test_decide_matches_sequential_oracle_decides(seed):
     np.testing.assert_array_equal(exp, ref_e)
     ok = float_close(gets, ref_g, cap_row[rows])
     assert ok.all(), (np.flatnonzero(~ok)[:8], gets[~ok][:4], ref_g[~ok][:4])
+
+
+def _oracle_round(snap, rows, has, wants, sub, now, limit=None):
+    """The oracle's literal Resource.Decide replayed request by request on each
+    resource's store, each ending with its Assign (resource.go:100-113); the first
+    `limit` requests only when given (a prefix of a round is decided exactly as in the
+    whole round)."""
+    so = snap["seg_off"]
+    cfg = O.make_cfg(len(so) - 1)
+    for f in O.CFG_DTYPE.names:
+        cfg[f] = snap[f]
+    n = len(rows) if limit is None else min(limit, len(rows))
+    stores = {}
+    ref_g, ref_e = np.empty(n), np.empty(n, np.int64)
+    for k in range(n):
+        row = rows[k]
+        r = int(np.searchsorted(so, row, side="right")) - 1
+        if r not in stores:
+            st = O.Store(int(so[r + 1] - so[r]))
+            for j in range(so[r], so[r + 1]):
+                if snap["expiry_ns"][j] != W.RELEASED:
+                    st.put(int(j - so[r]), int(snap["expiry_ns"][j]), snap["has"][j], snap["wants"][j],
+                           int(snap["subclients"][j]))
+            st.set_sums(int(snap["agg_count"][r]), snap["agg_sum_has"][r], snap["agg_sum_wants"][r])
+            stores[r] = st
+        lease = O.decide(stores[r], cfg[r], int(row - so[r]), has[k], wants[k], int(sub[k]), now)
+        ref_g[k], ref_e[k] = lease.has, lease.expiry_ns
+    return ref_g, ref_e
+
+
+def _fast_round_snapshot(rng, sizes, kinds, s0):
+    """Resources whose live rows all hold one subclients count (per resource), every
+    row live: rounds of existing clients refreshing with that count take the fast path."""
+    N = int(np.sum(sizes))
+    R = len(sizes)
+    cap = rng.choice([100.0, 1000.0, 12345.678], R)
+    cap_row = np.repeat(cap, sizes)
+    sub = np.repeat(np.asarray(s0), sizes).astype(np.int64)
+    wants = rng.uniform(0.0, 3.0, N) * cap_row / np.repeat(np.maximum(sizes, 1), sizes) * sub
+    tie = rng.random(N) < 0.1
+    wants[tie] = np.round(wants[tie])
+    has = rng.uniform(0.0, 1.2, N) * cap_row / np.repeat(np.maximum(sizes, 1), sizes)
+    snap = W.make_snapshot(sizes, wants, has, sub, NOW + 600 * W.NS, np.asarray(kinds, np.int32), cap, 20, 5)
+    return W.add_store_sums(snap)
+
+
+def _decide_engine(fast=True):
+    from doorman_amd.engine import Engine
+    old = os.environ.get("DM_DECIDE_FAST")
+    os.environ["DM_DECIDE_FAST"] = "1" if fast else "0"
+    try:
+        return Engine(0)
+    finally:
+        if old is None:
+            os.environ.pop("DM_DECIDE_FAST")
+        else:
+            os.environ["DM_DECIDE_FAST"] = old
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_decide_fast_path_matches_sequential_oracle(seed):
+    """dm_decide's fast path (dm_decide_fast.hip: resources with >= 64 requests whose
+    requests keep every count) against the oracle's literal replay of the whole round,
+    and against the one-workgroup replay (DM_DECIDE_FAST=0): FairShare and
+    ProportionalShare resources of several sizes, rounds of 1-3 requests per client
+    (clients asking twice see their own earlier Assign), wants unchanged, new, tied,
+    subclient counts 1 and 3, rounds longer than one event block (2048 requests);
+    one resource gets a request with another count (the fast path declines it) and
+    one holds released rows asked for again (declined too)."""
+    rng = np.random.default_rng(31 + seed)
+    sizes = np.array([3000, 700, 1500, 90, 40, 2600], dtype=np.int64)
+    kinds = [W.FAIR_SHARE, W.FAIR_SHARE, W.PROPORTIONAL_SHARE, W.FAIR_SHARE, W.PROPORTIONAL_SHARE, W.FAIR_SHARE]
+    s0 = [1, 3, 1, 3, 1, 1]
+    snap = _fast_round_snapshot(rng, sizes, kinds, s0)
+    so = snap["seg_off"]
+    # resource 5: a tenth of its rows released (requests for them are new clients: declined)
+    rel = so[5] + rng.choice(sizes[5], sizes[5] // 10, replace=False)
+    snap["expiry_ns"][rel] = W.RELEASED
+    snap["has"][rel] = 0.0
+    snap["wants"][rel] = 0.0
+    snap["subclients"][rel] = 0
+    W.add_store_sums(snap)
+    rows, wants, sub = [], [], []
+    for r, n in enumerate(sizes):
+        K = int(n * rng.choice([1.0, 1.5, 2.5]))
+        rr = so[r] + rng.integers(0, n, K)
+        cw = snap["wants"][rr]
+        fresh = rng.uniform(0.0, 3.0, K) * snap["capacity"][r] / n * s0[r]
+        w = np.where(rng.random(K) < 0.4, cw, fresh)
+        t = rng.random(K) < 0.1
+        w[t] = np.round(w[t])
+        rows.append(rr)
+        wants.append(w)
+        sub.append(np.full(K, s0[r], np.int64))
+    rows, wants, sub = np.concatenate(rows), np.concatenate(wants), np.concatenate(sub)
+    odd = np.flatnonzero((rows >= so[1]) & (rows < so[2]))[5]
+    sub[odd] = 2  # resource 1: one request changes its count -> k_decide
+    order = rng.permutation(len(rows))  # interleave the resources' requests
+    rows, wants, sub = rows[order], wants[order], sub[order]
+    has = rng.uniform(0, 1, len(rows))
+    fast, slow = _decide_engine(True), _decide_engine(False)
+    try:
+        fast.load(snap)
+        slow.load(snap)
+        gets, exp = fast.decide(NOW, rows, has, wants, sub)
+        again, _ = fast.decide(NOW, rows, has, wants, sub)
+        sg, se = slow.decide(NOW, rows, has, wants, sub)
+    finally:
+        fast.close()
+        slow.close()
+    assert gets.tobytes() == again.tobytes(), "the fast path is deterministic"
+    ref_g, ref_e = _oracle_round(snap, rows, has, wants, sub, NOW)
+    cap_row = np.repeat(snap["capacity"], np.diff(so))
+    np.testing.assert_array_equal(exp, ref_e)
+    np.testing.assert_array_equal(se, ref_e)
+    for got, label in ((gets, "fast"), (sg, "one-workgroup replay")):
+        ok = float_close(got, ref_g, cap_row[rows])
+        assert ok.all(), (label, np.flatnonzero(~ok)[:8], got[~ok][:4], ref_g[~ok][:4])
+    e = np.max(np.abs(gets - ref_g) / np.maximum(np.abs(ref_g), cap_row[rows]))
+    print(f"\nfast-path decide: {len(rows)} requests, max |got-ref|/max(|ref|, C) = {e:.3e} (bar 1e-9)")
+
+
+def test_decide_100k_requests_on_a_100k_client_resource():
+    """every client of a 100k-client FairShare resource refreshes in
+    one round (new wants, same subclients), so the round is 100k requests on one
+    resource -- 10^10 row visits for a request-by-request replay.  The fast path's
+    device time (dm_kernel_times "decide") is reported and must stay under 10 ms; the
+    first 3000 requests are checked against the oracle's literal replay (a prefix of a
+    sequential round is decided exactly as in the whole round), the whole round's
+    capacity bookkeeping by the grants' sum."""
+    rng = np.random.default_rng(5)
+    n = 100_000
+    snap = _fast_round_snapshot(rng, np.array([n], np.int64), [W.FAIR_SHARE], [1])
+    rows = rng.permutation(n).astype(np.int64)
+    wants = rng.uniform(0.0, 3.0, n) * snap["capacity"][0] / n
+    sub = np.ones(n, np.int64)
+    has = np.zeros(n)
+    e = _decide_engine(True)
+    try:
+        e.load(snap)
+        e.decide(NOW, rows[:100], has[:100], wants[:100], sub[:100])  # warm-up (allocations, code objects)
+        e.set_profiling(True)
+        e.reset_kernel_times()
+        gets, exp = e.decide(NOW, rows, has, wants, sub)
+        launches, ms = e.kernel_times()["decide"]
+        e.set_profiling(False)
+    finally:
+        e.close()
+    ref_g, ref_e = _oracle_round(snap, rows, has, wants, sub, NOW, limit=3000)
+    cap = snap["capacity"][0]
+    assert float_close(gets[:3000], ref_g, np.full(3000, cap)).all()
+    np.testing.assert_array_equal(exp[:3000], ref_e)
+    print(f"\n100k requests on a 100k-client resource: {ms:.2f} ms of device time (bar 10 ms); "
+          f"sum of grants {gets.sum():.6f} of capacity {cap}")
+    assert launches == 1 and ms < 10.0, ms
