@@ -31,9 +31,12 @@ def test_every_header_symbol_has_a_binding():
 
 
 def test_code_object_targets_gfx950():
+    """Every offload bundle in the library is a gfx950 code object (host code may name
+    other targets: rocPRIM's architecture table, pulled in by hipCUB's sorts)."""
+    import re
     data = open(_lib.LIB_PATH, "rb").read()
-    assert b"amdgcn-amd-amdhsa--gfx950" in data
-    assert b"gfx942" not in data and b"gfx90a" not in data
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", data))
+    assert targets == {b"gfx950"}, targets
 
 
 def test_version_string():
