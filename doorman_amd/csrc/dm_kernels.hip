@@ -638,25 +638,23 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   const int64_t* __restrict__ eb = p.expiry + ch.row0;
   r.valid = r.live = r.expl = r.rel = 0;
   int sr[kLR];
+  // the wants loads leave first, whichever form follows: they wait only for the chunk
+  // record, not for the per-chunk count (uni) that picks the form (one memory latency
+  // less per workgroup in the steady state)
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    const int i = k * 256 + threadIdx.x;
+    r.w[k] = wb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
+    r.h[k] = 0.0;
+  }
   if (uni >= 0) {
 #pragma unroll
-    for (int k = 0; k < kLR; ++k) {
-      const int i = k * 256 + threadIdx.x;
-      r.w[k] = wb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
-      sr[k] = (prev_live >> k & 1) ? uni : (int32_t)kSubReleased;
-      r.h[k] = 0.0;
-      if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    }
+    for (int k = 0; k < kLR; ++k) sr[k] = (prev_live >> k & 1) ? uni : (int32_t)kSubReleased;
   } else {
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
       const int i = k * 256 + threadIdx.x;
-      const unsigned u = (unsigned)(i < ch.nrows ? i : ch.nrows - 1);
-      r.w[k] = wb[u];
-      sr[k] = sb[u];
-      r.h[k] = 0.0;
-      // two round trips of half the rows (C2 tick 163 -> 157 us, tools/ab.py)
-      if (k == kLR / 2 - 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      sr[k] = sb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
     }
   }
   int64_t e[kLR];
@@ -810,7 +808,8 @@ __global__ __launch_bounds__(256) void k_large_a(DevParams p, const Chunk* __res
   ChunkRows rw;
   {
     const int uni = P.s_live ? __builtin_amdgcn_readfirstlane(P.uni[blockIdx.x]) : -1;
-    load_chunk(p, ch, rw, rs, uni, uni >= 0 ? P.live[(size_t)blockIdx.x * 256 + threadIdx.x] : 0u);
+    const uint32_t prev_live = P.s_live ? P.live[(size_t)blockIdx.x * 256 + threadIdx.x] : 0u;
+    load_chunk(p, ch, rw, rs, uni, prev_live);
   }
   AggA a = zeroA();
 #pragma unroll

@@ -1784,6 +1784,8 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     return c->fail(DM_E_INVAL, "bad upsert");
   if (nu > 0 && !b->upsert_expiry_ns && !c->cfg_loaded)
     return c->fail(DM_E_STATE, "arrivals without expiries take the resource's lease length: load a configuration");
+  if (nu > 0 && !b->upsert_expiry_ns && b->upsert_now_ns <= 0)  // an unset clock would insert lapsed leases
+    return c->fail(DM_E_INVAL, "arrivals without expiries need upsert_now_ns (> 0): their expiry is now + lease length");
   if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
   if (nu > 0) c->expl_rows = true;  // arrivals take explicit expiries
   if (nu > 0 || nr > 0) c->chain_live_ok = false;  // subclients words written, rows released

@@ -158,11 +158,13 @@ class Engine:
                                                      _ptr(wants)))
 
     def apply(self, wants_mask=None, wants=None, release_rows=None, upsert=None, wants_first_row: int = 0,
-              now_ns: int = 0):
+              now_ns: int | None = None):
         """dm_store_apply: one round's refresh (row mask + packed wants), departures and
         arrivals (upsert = (rows, has, wants, subclients, expiry_ns)) in one call.
         Narrow arrivals: has None (= 0), subclients as int32 (sent as 4 B), expiry_ns None
-        (= now_ns + the resource's lease length)."""
+        (= now_ns + the resource's lease length: now_ns is then required)."""
+        if upsert is not None and upsert[4] is None and now_ns is None:
+            raise ValueError("arrivals without expiries need now_ns (their expiry is now_ns + lease length)")
         keep = []
 
         def col(a, dt):
@@ -189,7 +191,7 @@ class Engine:
             else:
                 b.upsert_subclients = _ptr(col(sub, np.int64))
             b.upsert_expiry_ns = None if exp is None else _ptr(col(exp, np.int64))
-            b.upsert_now_ns = int(now_ns)
+            b.upsert_now_ns = int(now_ns or 0)
         self._chk(self._L.dm_store_apply(self._ctx, ctypes.byref(b)))
 
     def release(self, rows):

@@ -128,7 +128,7 @@ typedef struct {
   /* narrow arrivals: 4-B subclients instead of upsert_subclients (C4's arrivals: 20 B per
      row over PCIe with has and expiry NULL, instead of 40) */
   const int32_t* upsert_subclients32;
-  int64_t upsert_now_ns;
+  int64_t upsert_now_ns;             /* required (> 0, else DM_E_INVAL) when upsert_expiry_ns is NULL */
 } dm_store_batch;
 
 typedef struct {

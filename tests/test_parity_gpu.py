@@ -1064,3 +1064,37 @@ def test_dense_split_queues_undecided_items():
     finally:
         a.close()
         b.close()
+
+
+def test_arrivals_without_expiry_need_a_clock():
+    """arrivals whose expiry is implied (now + the resource's lease length)
+    need the caller's now: Engine.apply refuses to default it, and dm_store_apply
+    rejects upsert_now_ns <= 0 with DM_E_INVAL before anything is written."""
+    import ctypes
+    from doorman_amd import _lib
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(5)
+    snap = snapshot_with_sizes(rng, np.array([300, 20, 5000], np.int64), expired_frac=0.0)
+    free = np.array([3, 310, 400], np.int64)
+    for k, v in (("wants", 0.0), ("has", 0.0), ("subclients", 0), ("expiry_ns", W.RELEASED)):
+        snap[k][free] = v
+    W.add_store_sums(snap)
+    with Engine(0) as e:
+        e.load(snap)
+        before = e.read_store()
+        arrivals = (free, None, np.ones(3), np.ones(3, np.int32), None)
+        with pytest.raises(ValueError):
+            e.apply(upsert=arrivals)
+        b = _lib.StoreBatch()
+        rows, w, s32 = free.copy(), np.ones(3), np.ones(3, np.int32)
+        b.upsert_n, b.upsert_rows, b.upsert_wants = 3, rows.ctypes.data, w.ctypes.data
+        b.upsert_subclients32 = s32.ctypes.data
+        b.upsert_now_ns = 0
+        assert e._L.dm_store_apply(e._ctx, ctypes.byref(b)) == _lib.DM_E_INVAL
+        after = e.read_store()
+        for k in before:
+            assert before[k].tobytes() == after[k].tobytes(), k
+        e.apply(upsert=arrivals, now_ns=W.NOW_NS)  # with the clock: the leases expire now + lease length
+        got = e.read_store()
+        np.testing.assert_array_equal(got["expiry_ns"][free],
+                                      W.NOW_NS + np.repeat(snap["lease_length_s"], np.diff(snap["seg_off"]))[free] * W.NS)
