@@ -84,11 +84,9 @@ __device__ __forceinline__ FdScan block_exclusive(FdScan v, FdScan* lds, FdScan*
     if (t >= off) lds[t] = fd_add(a, lds[t]);
     __syncthreads();
   }
-  const FdScan incl = lds[t];
   *total = lds[255];
   const FdScan ex = t > 0 ? lds[t - 1] : fd_zero();
   __syncthreads();
-  (void)incl;
   return ex;
 }
 
@@ -317,6 +315,7 @@ __global__ __launch_bounds__(256) void k_fd_ev_prefix(FastItem fi, int slot, Fas
     }
     carry = fd_add(carry, tot);
   }
+  __syncthreads();  // every prefix written before thread 0 reads them
   if (threadIdx.x == 0) {
     if (len % kFdChunk == 0) {  // the total at index len (no thread's slot reached it)
       fa.ecnt[po + len] = (int32_t)carry.i;
