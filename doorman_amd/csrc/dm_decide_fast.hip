@@ -59,12 +59,34 @@ __device__ __forceinline__ double dd_val(DD a) { return a.hi + a.lo; }
 __device__ __forceinline__ FdScan fd_add(const FdScan& a, const FdScan& b) {
   const DD x = dd_add(DD{a.xh, a.xl}, DD{b.xh, b.xl});
   const DD y = dd_add(DD{a.yh, a.yl}, DD{b.yh, b.yl});
-  return FdScan{x.hi, x.lo, y.hi, y.lo, a.i + b.i};
+  const DD z = dd_add(DD{a.zh, a.zl}, DD{b.zh, b.zl});
+  return FdScan{x.hi, x.lo, y.hi, y.lo, z.hi, z.lo, a.i + b.i};
 }
+__device__ __forceinline__ FdScan fd_zero() { return FdScan{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0}; }
 struct OpFd {
   __device__ FdScan operator()(FdScan a, FdScan b) const { return fd_add(a, b); }
+  __device__ static FdScan zero() { return fd_zero(); }
 };
-__device__ __forceinline__ FdScan fd_zero() { return FdScan{0.0, 0.0, 0.0, 0.0, 0}; }
+
+// The available capacity a = C - sumHas before each request follows
+//   a' = C - (sumHas + g - has) = max(a + has - v, 0)     with g = minF(v, a + has)
+// (algorithm.go:120,131,179,204 then store.go:156), a map x -> max(x + c, 0); maps of
+// the form x -> max(x + A, B) compose into the same form, so every request's a is an
+// exclusive scan of them (x -> max(x, -inf) is the identity; -inf as kFdNone, kept finite
+// for the double-double sums).
+constexpr double kFdNone = -1e307;
+__device__ __forceinline__ bool dd_lt(DD a, DD b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+__device__ __forceinline__ FdLind ld_compose(const FdLind& f, const FdLind& g) {  // f first, then g
+  const DD a = dd_add(DD{f.ah, f.al}, DD{g.ah, g.al});
+  const DD fb = dd_add(DD{f.bh, f.bl}, DD{g.ah, g.al});
+  const DD gb = DD{g.bh, g.bl};
+  const DD b = dd_lt(fb, gb) ? gb : fb;
+  return FdLind{a.hi, a.lo, b.hi, b.lo};
+}
+struct OpLd {
+  __device__ FdLind operator()(FdLind a, FdLind b) const { return ld_compose(a, b); }
+  __device__ static FdLind zero() { return FdLind{0.0, 0.0, kFdNone, 0.0}; }
+};
 
 // FairShare round 1's per-row terms (algorithm.go:160-169) at d = s0 * equalShare
 __device__ __forceinline__ double fs_t(double w, double d) { return w < d ? d - w : 0.0; }
@@ -73,103 +95,104 @@ __device__ __forceinline__ long long fs_c(double w, double d, int s0) { return w
 __device__ __forceinline__ double ps_x(double w, double e) { return w < e ? e - w : 0.0; }
 __device__ __forceinline__ double ps_y(double w, double e) { return w < e ? 0.0 : w - e; }
 
-// ---- block-wide exclusive scan of FdScan (256 threads; Hillis-Steele in LDS) ----
-__device__ __forceinline__ FdScan block_exclusive(FdScan v, FdScan* lds, FdScan* total) {
+// ---- deterministic exclusive scans (256 threads; Hillis-Steele in LDS) ----
+template <typename T, typename Op>
+__device__ __forceinline__ T block_exclusive(T v, T* lds, T* total) {
+  Op op;
   const int t = threadIdx.x;
   lds[t] = v;
   __syncthreads();
   for (int off = 1; off < 256; off <<= 1) {
-    const FdScan a = t >= off ? lds[t - off] : fd_zero();
+    const T a = t >= off ? lds[t - off] : Op::zero();
     __syncthreads();
-    if (t >= off) lds[t] = fd_add(a, lds[t]);
+    if (t >= off) lds[t] = op(a, lds[t]);
     __syncthreads();
   }
   *total = lds[255];
-  const FdScan ex = t > 0 ? lds[t - 1] : fd_zero();
+  const T ex = t > 0 ? lds[t - 1] : Op::zero();
   __syncthreads();
   return ex;
 }
 
-
 // phase 1: each chunk's total (fixed order: 4 per thread, then the thread totals in order)
-__global__ __launch_bounds__(256) void k_fd_scan_part(const FdScan* __restrict__ a, int64_t n, FdScan* part,
-                                                      const FastRes* fr) {
-  __shared__ FdScan lds[256];
+template <typename T, typename Op>
+__global__ __launch_bounds__(256) void k_fd_scan_part(const T* __restrict__ a, int64_t n, T* part, const FastRes* fr) {
+  __shared__ T lds[256];
   if (fr && !fr->ok) return;
+  Op op;
   const int64_t base = (int64_t)blockIdx.x * kFdChunk + 4 * threadIdx.x;
-  FdScan s = fd_zero();
+  T s = Op::zero();
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (base + i < n) s = fd_add(s, a[base + i]);
-  FdScan tot;
-  (void)block_exclusive(s, lds, &tot);
+    if (base + i < n) s = op(s, a[base + i]);
+  T tot;
+  (void)block_exclusive<T, Op>(s, lds, &tot);
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
 // phase 2: exclusive scan of the chunk totals, starting at init (one workgroup)
-__global__ __launch_bounds__(256) void k_fd_scan_top(FdScan* part, int64_t nparts, const FdScan* init,
-                                                     const FastRes* fr) {
-  __shared__ FdScan lds[256];
+template <typename T, typename Op>
+__global__ __launch_bounds__(256) void k_fd_scan_top(T* part, int64_t nparts, const T* init, const FastRes* fr) {
+  __shared__ T lds[256];
   if (fr && !fr->ok) return;
-  FdScan carry = init ? *init : fd_zero();
+  Op op;
+  T carry = init ? *init : Op::zero();
   for (int64_t b = 0; b < nparts; b += 256) {
     const int64_t i = b + threadIdx.x;
-    const FdScan v = i < nparts ? part[i] : fd_zero();
-    FdScan tot;
-    const FdScan ex = block_exclusive(v, lds, &tot);
-    if (i < nparts) part[i] = fd_add(carry, ex);
-    carry = fd_add(carry, tot);
+    const T v = i < nparts ? part[i] : Op::zero();
+    T tot;
+    const T ex = block_exclusive<T, Op>(v, lds, &tot);
+    if (i < nparts) part[i] = op(carry, ex);
+    carry = op(carry, tot);
   }
 }
 
 // phase 3: every element's exclusive prefix, in place
-__global__ __launch_bounds__(256) void k_fd_scan_apply(FdScan* a, int64_t n, const FdScan* part, const FastRes* fr) {
-  __shared__ FdScan lds[256];
+template <typename T, typename Op>
+__global__ __launch_bounds__(256) void k_fd_scan_apply(T* a, int64_t n, const T* part, const FastRes* fr) {
+  __shared__ T lds[256];
   if (fr && !fr->ok) return;
+  Op op;
   const int64_t base = (int64_t)blockIdx.x * kFdChunk + 4 * threadIdx.x;
-  FdScan v[4];
-  FdScan s = fd_zero();
+  T v[4];
+  T s = Op::zero();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    v[i] = base + i < n ? a[base + i] : fd_zero();
-    s = fd_add(s, v[i]);
+    v[i] = base + i < n ? a[base + i] : Op::zero();
+    s = op(s, v[i]);
   }
-  FdScan tot;
-  FdScan run = fd_add(part[blockIdx.x], block_exclusive(s, lds, &tot));
+  T tot;
+  T run = op(part[blockIdx.x], block_exclusive<T, Op>(s, lds, &tot));
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (base + i < n) a[base + i] = run;
-    run = fd_add(run, v[i]);
+    run = op(run, v[i]);
   }
 }
 
-static hipError_t fd_scan(FdScan* a, int64_t n, const FdScan* init, FdScan* part, const FastRes* fr,
-                          hipStream_t st) {
+template <typename T, typename Op>
+static hipError_t fd_scan(T* a, int64_t n, const T* init, T* part, const FastRes* fr, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t np = (n + kFdChunk - 1) / kFdChunk;
-  k_fd_scan_part<<<(unsigned)np, 256, 0, st>>>(a, n, part, fr);
-  k_fd_scan_top<<<1, 256, 0, st>>>(part, np, init, fr);
-  k_fd_scan_apply<<<(unsigned)np, 256, 0, st>>>(a, n, part, fr);
+  k_fd_scan_part<T, Op><<<(unsigned)np, 256, 0, st>>>(a, n, part, fr);
+  k_fd_scan_top<T, Op><<<1, 256, 0, st>>>(part, np, init, fr);
+  k_fd_scan_apply<T, Op><<<(unsigned)np, 256, 0, st>>>(a, n, part, fr);
   return hipGetLastError();
 }
 
 // ---- the round ----
-// Clean into the round's scratch copy (as k_decide), the eligibility test, and the
-// totals over the live rows before the first request.  One workgroup per fast item.
-__global__ __launch_bounds__(256) void k_fd_prep(DevParams p, const ReqItem* __restrict__ items, ReqArgs q,
-                                                 FastArgs fa) {
+// Clean (store.go:169-181) of one chunk of the resource's rows into the round's scratch
+// copy (as k_decide), with the chunk's partials: released subclients / has / wants,
+// the live rows' subclients range, wants the fast path cannot take.
+__global__ __launch_bounds__(256) void k_fd_clean(DevParams p, ReqItem it, FastItem fi, ReqArgs q, FastArgs fa) {
   __shared__ Lds<256> lds;
-  __shared__ FdScan red[4];
-  const FastItem fi = fa.fi[blockIdx.x];
-  const ReqItem it = items[fi.item];
   const int seg = it.seg;
-  const int64_t lo = p.seg_off[seg], n = p.seg_off[seg + 1] - lo;
-  double* sh_ = q.sc_has + it.scr;
-  double* sw_ = q.sc_wants + it.scr;
-  int32_t* ss_ = q.sc_sub + it.scr;
+  const int64_t lo = p.seg_off[seg], n = fi.n;
   const Res rs = load_res(p, seg);
   AggA a = zeroA();
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
+  const int64_t j0 = (int64_t)blockIdx.x * kFdRows;
+  const int64_t j1 = j0 + kFdRows < n ? j0 + kFdRows : n;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
     const int32_t raw = p.sub[lo + j];
     const double hj = p.has[lo + j], wj = p.wants[lo + j];
     const bool gone = p.now > row_expiry(p, lo + j, raw, rs.follow_exp);
@@ -184,56 +207,115 @@ __global__ __launch_bounds__(256) void k_fd_prep(DevParams p, const ReqItem* __r
       a.nan |= !(__builtin_fabs(wj) <= kFdMaxAbs) ? 1 : 0;  // NaN, infinite or huge wants
       a.nlive += 1;
     }
-    sh_[j] = hj;
-    sw_[j] = wj;
-    ss_[j] = gone ? -1 : sv;
+    q.sc_has[it.scr + j] = hj;
+    q.sc_wants[it.scr + j] = wj;
+    q.sc_sub[it.scr + j] = gone ? -1 : sv;
   }
-  a = group_reduce<256>(a, OpA(), lds.a);  // its barriers also order the scratch writes
+  a = group_reduce_t0<256>(a, OpA(), lds.a);
+  if (threadIdx.x == 0) fa.pc[fi.c0 + blockIdx.x] = FdClean{a.cnt, a.h, a.w, a.smin, a.smax, a.nan, a.nlive};
+}
+
+// The resource's Clean from the chunks' partials (fixed order), the rows' verdict and
+// the round's constants.  One workgroup.
+__global__ __launch_bounds__(256) void k_fd_check(DevParams p, ReqItem it, FastItem fi, int slot, FastArgs fa) {
+  __shared__ Lds<256> lds;
+  const Res rs = load_res(p, it.seg);
+  AggA a = zeroA();
+  for (int c = threadIdx.x; c < fi.nch; c += 256) {
+    const FdClean x = fa.pc[fi.c0 + c];
+    AggA y = zeroA();
+    y.cnt = x.cnt;
+    y.h = x.h;
+    y.w = x.w;
+    y.smin = x.smin;
+    y.smax = x.smax;
+    y.nan = x.bad;
+    y.nlive = x.nlive;
+    a = OpA()(a, y);
+  }
+  a = group_reduce_t0<256>(a, OpA(), lds.a);
+  if (threadIdx.x != 0) return;
   const Clean cl = clean_from(p, rs, a);
   const double C = rs.C;
   const int s0 = a.smin;
-  bool ok = !rs.learning && (rs.kind == 2 || rs.kind == 3) && a.nlive > 0 && a.smin == a.smax && s0 >= 1 &&
-            !a.nan && cl.count >= 1 && __builtin_fabs(C) <= kFdMaxAbs;
-  int bad = ok ? 0 : 1;
-  for (int64_t k = it.qlo + threadIdx.x; ok && k < it.qhi; k += 256) {
-    const int64_t row = q.rows[k] - lo;
-    if (q.sub[k] != s0 || ss_[row] < 0 || !(__builtin_fabs(q.wants[k]) <= kFdMaxAbs)) bad = 1;
+  const bool ok = !rs.learning && (rs.kind == 2 || rs.kind == 3) && a.nlive > 0 && a.smin == a.smax && s0 >= 1 &&
+                  !a.nan && cl.count >= 1 && __builtin_fabs(C) <= kFdMaxAbs;
+  FastRes r;
+  r.ok = 0;
+  r.kind = rs.kind;
+  r.s0 = s0;
+  r.ok0 = ok ? 1 : 0;
+  r.bad = 0;
+  r.pad = 0;
+  r.C = C;
+  r.eq = C / (double)cl.count;  // algorithm.go:123,229
+  r.d = (double)s0 * r.eq;      // :160 (eq * s0 at :233,273: the same product)
+  r.count = cl.count;
+  r.nlive = a.nlive;
+  r.sum_has = cl.sum_has;
+  r.sum_wants = cl.sum_wants;
+  r.init = fd_zero();
+  r.exp_out = rs.exp_out;
+  fa.fr[slot] = r;
+}
+
+// Every request asks from a live row with the resource's count and finite wants.
+__global__ __launch_bounds__(256) void k_fd_reqcheck(DevParams p, ReqItem it, FastItem fi, int slot, ReqArgs q,
+                                                     FastArgs fa) {
+  FastRes* fr = fa.fr + slot;
+  if (!fr->ok0) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool bad = false;
+  if (j < fi.K) {
+    const int64_t k = fi.k0 + j;
+    const int64_t row = q.rows[k] - p.seg_off[it.seg];
+    bad = q.sub[k] != fr->s0 || q.sc_sub[it.scr + row] < 0 || !(__builtin_fabs(q.wants[k]) <= kFdMaxAbs);
   }
-  ok = !__syncthreads_or(bad);
-  const double eq = C / (double)cl.count;  // algorithm.go:123,229
-  const double d = (double)s0 * eq;        // :160 (eq * s0 at :233,273: the same product)
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&fr->bad, 1);
+}
+
+// The totals over the live rows before the first request (one chunk's partial), and
+// (FairShare) the live rows' wants as sort keys (+inf for absent rows).
+__global__ __launch_bounds__(256) void k_fd_totals(ReqItem it, FastItem fi, int slot, ReqArgs q, FastArgs fa) {
+  __shared__ FdScan red[4];
+  const FastRes& frr = fa.fr[slot];
+  if (!frr.ok0 || frr.bad) return;
+  const double d = frr.d;
+  const int s0 = frr.s0;
+  const bool fs = frr.kind == 3;
+  const int64_t j0 = (int64_t)blockIdx.x * kFdRows;
+  const int64_t j1 = j0 + kFdRows < fi.n ? j0 + kFdRows : fi.n;
   FdScan tot = fd_zero();
-  if (ok) {
-    for (int64_t j = threadIdx.x; j < n; j += 256) {
-      const bool live = ss_[j] >= 0;
-      const double w = sw_[j];
-      if (live) {
-        if (rs.kind == 3) {
-          tot = fd_add(tot, FdScan{fs_t(w, d), 0.0, 0.0, 0.0, fs_c(w, d, s0)});
-        } else {
-          tot = fd_add(tot, FdScan{ps_x(w, d), 0.0, ps_y(w, d), 0.0, 0});
-        }
-      }
-      if (rs.kind == 3) fa.keys[fi.m0 + j] = live ? w : __builtin_inf();
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+    const bool live = q.sc_sub[it.scr + j] >= 0;
+    const double w = q.sc_wants[it.scr + j];
+    if (live) {
+      if (fs) tot = fd_add(tot, FdScan{fs_t(w, d), 0.0, 0.0, 0.0, 0.0, 0.0, fs_c(w, d, s0)});
+      else tot = fd_add(tot, FdScan{ps_x(w, d), 0.0, ps_y(w, d), 0.0, 0.0, 0.0, 0});
     }
-    tot = group_reduce<256>(tot, OpFd(), red);
+    if (fs) fa.keys[fi.m0 + j] = live ? w : __builtin_inf();
   }
+  tot = group_reduce_t0<256>(tot, OpFd(), red);
+  if (threadIdx.x == 0) fa.pt[fi.c0 + blockIdx.x] = tot;
+}
+
+// The verdict, and the totals from the chunks' partials (fixed order).
+__global__ __launch_bounds__(256) void k_fd_final(FastItem fi, int slot, FastArgs fa) {
+  __shared__ FdScan red[4];
+  FastRes* fr = fa.fr + slot;
+  const bool ok = fr->ok0 && !fr->bad;
+  if (!ok) {
+    if (threadIdx.x == 0) fr->ok = 0;
+    return;
+  }
+  FdScan tot = fd_zero();
+  for (int c = threadIdx.x; c < fi.nch; c += 256) tot = fd_add(tot, fa.pt[fi.c0 + c]);
+  tot = group_reduce_t0<256>(tot, OpFd(), red);
   if (threadIdx.x == 0) {
-    FastRes r;
-    r.ok = ok ? 1 : 0;
-    r.kind = rs.kind;
-    r.s0 = s0;
-    r.pad = 0;
-    r.C = C;
-    r.eq = eq;
-    r.d = d;
-    r.count = cl.count;
-    r.nlive = a.nlive;
-    r.sum_has = cl.sum_has;
-    r.sum_wants = cl.sum_wants;
-    r.init = tot;
-    r.exp_out = rs.exp_out;
-    fa.fr[blockIdx.x] = r;
+    tot.zh = fr->sum_wants;  // ProportionalShare's sumWants starts at the cleaned store's
+    tot.zl = 0.0;
+    fr->init = tot;
+    fr->ok = 1;
   }
 }
 
@@ -255,7 +337,7 @@ __global__ __launch_bounds__(256) void k_fd_delta(DevParams p, ReqItem it, FastI
   FdScan e;
   if (fr.kind == 3) {
     const DD x = dd_two_sum(fs_t(rw, d), -fs_t(pw, d));
-    e = FdScan{x.hi, x.lo, 0.0, 0.0, fs_c(rw, d, fr.s0) - fs_c(pw, d, fr.s0)};
+    e = FdScan{x.hi, x.lo, 0.0, 0.0, 0.0, 0.0, fs_c(rw, d, fr.s0) - fs_c(pw, d, fr.s0)};
     fa.ev_in[fi.e0 + 2 * j] = rw;
     fa.evs_in[fi.e0 + 2 * j] = 1;
     fa.ev_in[fi.e0 + 2 * j + 1] = pw;
@@ -263,7 +345,8 @@ __global__ __launch_bounds__(256) void k_fd_delta(DevParams p, ReqItem it, FastI
   } else {
     const DD x = dd_two_sum(ps_x(rw, d), -ps_x(pw, d));
     const DD y = dd_two_sum(ps_y(rw, d), -ps_y(pw, d));
-    e = FdScan{x.hi, x.lo, y.hi, y.lo, 0};
+    const DD z = dd_two_sum(rw, -pw);  // sumWants moves by the request's wants (store.go:157)
+    e = FdScan{x.hi, x.lo, y.hi, y.lo, z.hi, z.lo, 0};
   }
   fa.sc[k] = e;
 }
@@ -276,7 +359,7 @@ __global__ __launch_bounds__(256) void k_fd_m0_fill(FastItem fi, int slot, FastA
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j > fi.n) return;
   const double v = j < fr.nlive ? fa.keys_s[fi.m0 + j] : 0.0;
-  fa.ps[fi.m0 + j] = FdScan{v, 0.0, 0.0, 0.0, 0};
+  fa.ps[fi.m0 + j] = FdScan{v, 0.0, 0.0, 0.0, 0.0, 0.0, 0};
 }
 
 // Per event block: exclusive prefix counts / sums of its sorted events, and its
@@ -299,12 +382,12 @@ __global__ __launch_bounds__(256) void k_fd_ev_prefix(FastItem fi, int slot, Fas
       v[i] = fd_zero();
       if (base + i < len) {
         const DD x = dd_of(es[base + i] > 0 ? ev[base + i] : -ev[base + i]);
-        v[i] = FdScan{x.hi, x.lo, 0.0, 0.0, es[base + i]};
+        v[i] = FdScan{x.hi, x.lo, 0.0, 0.0, 0.0, 0.0, es[base + i]};
       }
       s = fd_add(s, v[i]);
     }
     FdScan tot;
-    FdScan run = fd_add(carry, block_exclusive(s, lds, &tot));
+    FdScan run = fd_add(carry, block_exclusive<FdScan, OpFd>(s, lds, &tot));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (base + i <= len) {
@@ -353,8 +436,9 @@ __device__ __forceinline__ int64_t upper_bound_d(const double* a, int64_t n, dou
 
 // Per request: its grant before the available-capacity cap.  FairShare: rw when it
 // is within deservedShare (algorithm.go:131) or deservedShare + deservedExtra
-// (:179), else round 2 at T (:189-204); ProportionalShare: its round-1 grant
-// (:283), used only when sumWants > C (the recurrence decides).
+// (:179), else round 2 at T (:189-204); ProportionalShare: rw when the store's
+// sumWants (the earlier Assigns' included) is within C or rw within its equal share
+// (:245), else its round-1 grant (:283).
 __global__ __launch_bounds__(256) void k_fd_query(ReqItem it, FastItem fi, int slot, ReqArgs q, FastArgs fa) {
   const FastRes& frr = fa.fr[slot];
   if (!frr.ok) return;
@@ -372,7 +456,8 @@ __global__ __launch_bounds__(256) void k_fd_query(ReqItem it, FastItem fi, int s
     const double x = dd_val(dd_add(dd_add(DD{e.xh, e.xl}, dd_of(-ps_x(pw, d))), dd_of(ps_x(rw, d))));
     const double y = dd_val(dd_add(dd_add(DD{e.yh, e.yl}, dd_of(-ps_y(pw, d))), dd_of(ps_y(rw, d))));
     const double epc = eq * rsub;                 // :233
-    v = epc + (rw - epc) * (x / y);               // :283
+    const double sw = dd_val(DD{e.zh, e.zl});     // sumWants before request k
+    v = (sw <= fr.C || rw <= epc) ? rw : epc + (rw - epc) * (x / y);  // :245, :283
   } else {
     const double ds = eq * rsub;  // :126
     if (rw <= ds) {
@@ -445,10 +530,10 @@ __global__ __launch_bounds__(256) void k_fd_query(ReqItem it, FastItem fi, int s
   fa.v[k] = v;
 }
 
-// The round in order (one wave per fast item): the available capacity after the
-// earlier grants (algorithm.go:120,239), ProportionalShare's sumWants test (:245),
-// the Assigns' running sums (store.go:156-158).  Lanes hold 64 requests' inputs;
-// the recurrence walks them with readlanes.
+// Rounds in which some client asks twice: the grant of its earlier request is the has
+// its later one sees, so the available capacity (algorithm.go:120,239) after the
+// earlier grants (store.go:156) runs in order, on one wave per fast item.  Lanes hold
+// 64 requests' inputs; the recurrence walks them with readlanes.
 __global__ __launch_bounds__(64) void k_fd_seq(DevParams p, ReqItem it, FastItem fi, int slot, ReqArgs q,
                                                FastArgs fa) {
   __shared__ double gl[64];
@@ -458,15 +543,13 @@ __global__ __launch_bounds__(64) void k_fd_seq(DevParams p, ReqItem it, FastItem
   const int lane = threadIdx.x;
   const int64_t lo = p.seg_off[it.seg];
   const double C = fr.C;
-  const bool ps = fr.kind == 2;
-  const double epc = fr.eq * (double)fr.s0;
-  double sh = fr.sum_has, sw = fr.sum_wants;
+  double sh = fr.sum_has;
   const int64_t end = fi.k0 + fi.K;
   for (int64_t base = fi.k0; base < end; base += 64) {
     const int64_t k = base + lane;
     const bool in = k < end;
     const int64_t kc = in ? k : base;
-    const double v = fa.v[kc], rw = q.wants[kc], pw = fa.pw[kc];
+    const double v = fa.v[kc];
     const int64_t prev = fa.prev[kc];
     const double oh0 = prev < 0 ? q.sc_has[it.scr + (q.rows[kc] - lo)] : 0.0;
     const int m = (int)std::min<int64_t>(64, end - base);
@@ -478,15 +561,7 @@ __global__ __launch_bounds__(64) void k_fd_seq(DevParams p, ReqItem it, FastItem
       else oh = ld_wt(q.gets + pv);
       const double vi = readlane_any(v, i);
       const double avail = C - sh + oh;
-      double g;
-      if (ps) {
-        const double rwi = readlane_any(rw, i);
-        g = (sw <= C || rwi <= epc) ? minF(rwi, avail) : minF(vi, avail);
-        sw += rwi - readlane_any(pw, i);
-      } else {
-        g = minF(vi, avail);
-        // (sumWants moves too, store.go:157, but nothing in FairShare reads it)
-      }
+      const double g = minF(vi, avail);
       sh += g - oh;
       if (lane == 0) gl[i] = g;
     }
@@ -499,42 +574,84 @@ __global__ __launch_bounds__(64) void k_fd_seq(DevParams p, ReqItem it, FastItem
   }
 }
 
+// Rounds in which every client asks once: the available capacity before each request
+// from the exclusive composition of the maps x -> max(x + has - v, 0) (OpLd).
+__global__ __launch_bounds__(256) void k_fd_lind_fill(DevParams p, ReqItem it, FastItem fi, int slot, ReqArgs q,
+                                                      FastArgs fa) {
+  if (!fa.fr[slot].ok) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= fi.K) return;
+  const int64_t k = fi.k0 + j;
+  const double oh = q.sc_has[it.scr + (q.rows[k] - p.seg_off[it.seg])];  // store.Get(self).Has
+  const DD c = dd_two_sum(oh, -fa.v[k]);
+  fa.ld[k] = FdLind{c.hi, c.lo, 0.0, 0.0};
+}
+
+__global__ __launch_bounds__(256) void k_fd_lind_final(DevParams p, ReqItem it, FastItem fi, int slot, ReqArgs q,
+                                                       FastArgs fa) {
+  const FastRes& fr = fa.fr[slot];
+  if (!fr.ok) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= fi.K) return;
+  const int64_t k = fi.k0 + j;
+  const double oh = q.sc_has[it.scr + (q.rows[k] - p.seg_off[it.seg])];
+  const FdLind f = fa.ld[k];
+  const DD a0 = dd_two_sum(fr.C, -fr.sum_has);  // C - sumHas before the round
+  const DD x = dd_add(a0, DD{f.ah, f.al});
+  const DD b = DD{f.bh, f.bl};
+  const DD a = dd_lt(x, b) ? b : x;                  // C - sumHas before request k
+  const double avail = dd_val(dd_add(a, dd_of(oh)));  // algorithm.go:120,239
+  q.gets[k] = minF(fa.v[k], avail);                   // :131,179,204,245,290
+  q.expiry[k] = fr.exp_out;                           // now + lease length (store.go:161)
+}
+
 // ---- host side ----
-hipError_t fd_prep(const DevParams& p, const ReqItem* items, const ReqArgs& q, const FastArgs& fa, int nfast,
-                   hipStream_t st) {
-  if (nfast <= 0) return hipSuccess;
-  k_fd_prep<<<nfast, 256, 0, st>>>(p, items, q, fa);
+// Clean, the verdict and the round's totals of one fast item.
+hipError_t fd_rows(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
+                   const FastArgs& fa, hipStream_t st) {
+  const unsigned gk = (unsigned)((fi.K + 255) / 256);
+  k_fd_clean<<<(unsigned)fi.nch, 256, 0, st>>>(p, it, fi, q, fa);
+  k_fd_check<<<1, 256, 0, st>>>(p, it, fi, slot, fa);
+  k_fd_reqcheck<<<gk, 256, 0, st>>>(p, it, fi, slot, q, fa);
+  k_fd_totals<<<(unsigned)fi.nch, 256, 0, st>>>(it, fi, slot, q, fa);
+  k_fd_final<<<1, 256, 0, st>>>(fi, slot, fa);
   return hipGetLastError();
 }
 
+// Each request's Assign delta and the running totals before it (a scan).
 hipError_t fd_item(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
                    const FastArgs& fa, FdScan* part, hipStream_t st) {
   const unsigned gk = (unsigned)((fi.K + 255) / 256);
   k_fd_delta<<<gk, 256, 0, st>>>(p, it, fi, slot, q, fa);
-  hipError_t e = fd_scan(fa.sc + fi.k0, fi.K, &fa.fr[slot].init, part, fa.fr + slot, st);
-  if (e != hipSuccess) return e;
-  return hipGetLastError();
+  return fd_scan<FdScan, OpFd>(fa.sc + fi.k0, fi.K, &fa.fr[slot].init, part, fa.fr + slot, st);
 }
 
+// After the sorts: FairShare's round-2 structures (the kernels return at once for
+// ProportionalShare), every request's grant before the cap, then the cap itself.
 hipError_t fd_item_sorted(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
                           const FastArgs& fa, FdScan* part, hipStream_t st) {
   const unsigned gk = (unsigned)((fi.K + 255) / 256);
-  // FairShare's round-2 structures (the kernels return at once for ProportionalShare)
   k_fd_m0_fill<<<(unsigned)((fi.n + 1 + 255) / 256), 256, 0, st>>>(fi, slot, fa);
-  hipError_t e = fd_scan(fa.ps + fi.m0, fi.n + 1, nullptr, part, fa.fr + slot, st);
+  hipError_t e = fd_scan<FdScan, OpFd>(fa.ps + fi.m0, fi.n + 1, nullptr, part, fa.fr + slot, st);
   if (e != hipSuccess) return e;
   k_fd_ev_prefix<<<(unsigned)fi.nblk, 256, 0, st>>>(fi, slot, fa);
   k_fd_query<<<gk, 256, 0, st>>>(it, fi, slot, q, fa);
-  k_fd_seq<<<1, 64, 0, st>>>(p, it, fi, slot, q, fa);
+  if (fi.repeats) {
+    k_fd_seq<<<1, 64, 0, st>>>(p, it, fi, slot, q, fa);
+    return hipGetLastError();
+  }
+  k_fd_lind_fill<<<gk, 256, 0, st>>>(p, it, fi, slot, q, fa);
+  e = fd_scan<FdLind, OpLd>(fa.ld + fi.k0, fi.K, nullptr, reinterpret_cast<FdLind*>(part), fa.fr + slot, st);
+  if (e != hipSuccess) return e;
+  k_fd_lind_final<<<gk, 256, 0, st>>>(p, it, fi, slot, q, fa);
   return hipGetLastError();
 }
 
-// Segmented sorts (hipCUB radix sorts: stable, deterministic): the items' initial
-// wants, and every event block.  temp == nullptr: *bytes = the storage needed.
-hipError_t fd_sort_keys(void* temp, size_t* bytes, const double* in, double* out, int64_t n, int nseg,
-                        const int64_t* begin, const int64_t* end, hipStream_t st) {
-  return hipcub::DeviceSegmentedRadixSort::SortKeys(temp, *bytes, in, out, (int)n, nseg, begin, end, 0,
-                                                    (int)(8 * sizeof(double)), st);
+// The items' initial wants (one radix sort each: a segmented sort gives a segment one
+// workgroup), and every event block (segmented: 4096 events each).  hipCUB radix
+// sorts are stable and deterministic.  temp == nullptr: *bytes = the storage needed.
+hipError_t fd_sort_keys(void* temp, size_t* bytes, const double* in, double* out, int64_t n, hipStream_t st) {
+  return hipcub::DeviceRadixSort::SortKeys(temp, *bytes, in, out, (int)n, 0, (int)(8 * sizeof(double)), st);
 }
 hipError_t fd_sort_pairs(void* temp, size_t* bytes, const double* kin, double* kout, const int32_t* vin,
                          int32_t* vout, int64_t n, int nseg, const int64_t* begin, const int64_t* end,

@@ -253,6 +253,7 @@ struct ReqArgs {
 // sumHas's recurrence (and ProportionalShare's sumWants test) stays sequential.
 constexpr int kFdMin = 64;       // requests on one resource before the fast path is tried
 constexpr int kFdBlock = 2048;   // requests per Assign-event block (2 events each)
+constexpr int kFdRows = 4096;    // rows per workgroup of the fast path's row passes
 constexpr double kFdMaxAbs = 1e300;  // |wants| and |capacity| bound: no overflow in the sums
 constexpr int kFdChunk = 1024;   // scan elements per workgroup (4 per thread)
 struct FastItem {
@@ -263,22 +264,39 @@ struct FastItem {
   int64_t e0;    // offset of its events (2 K)
   int64_t b0;    // first event block (global block index)
   int64_t n;     // rows of the resource
+  int64_t c0;    // first row chunk (kFdRows rows each; global chunk index)
+  int32_t nch;   // row chunks
+  int32_t repeats;  // 1: some row is requested twice (the grants then need the sequential recurrence)
 };
 struct FdScan {  // one scanned element: double-double sums and an integer count
   double xh, xl;  // FairShare: extra (sum of d - w for w < d); ProportionalShare: extraCapacity
   double yh, yl;  // ProportionalShare: extraNeed
+  double zh, zl;  // ProportionalShare: sumWants
   long long i;    // FairShare: wantExtra (subclients of rows with w > d)
+};
+struct FdClean {  // one row chunk's Clean partials
+  long long cnt;  // subclients Clean releases
+  double h, w;    // their has / wants
+  int smin, smax; // live rows' subclients range
+  int bad;        // some live row's wants NaN, infinite or beyond kFdMaxAbs
+  int nlive;
 };
 struct FastRes {
   int32_t ok;    // 1: the fast path decides this resource's requests
   int32_t kind;
   int32_t s0;    // the one subclients count
+  int32_t ok0;   // the rows qualify (before the requests are checked)
+  int32_t bad;   // some request does not qualify (atomic OR)
   int32_t pad;
   double C, eq, d;
   long long count, nlive;
   double sum_has, sum_wants;  // after Clean
   FdScan init;                // the totals over the live rows before the round
   int64_t exp_out;
+};
+struct FdLind {  // the available-capacity recurrence a' = max(a + c, 0) composed: x -> max(x + A, B)
+  double ah, al;
+  double bh, bl;
 };
 struct FastArgs {
   const FastItem* fi;
@@ -298,6 +316,9 @@ struct FastArgs {
   double2* esum;        // ... and of sign * wants (double-double)
   int32_t* bdc;         // [blocks] signed count / sum of the block's events <= d
   double2* bds;
+  FdClean* pc;          // [row chunks] Clean partials
+  FdScan* pt;           // [row chunks] totals partials
+  FdLind* ld;           // [n requests] the recurrence's steps -> exclusive compositions
 };
 
 // dm_hier_root_tick: one exchange round of the hierarchy's root (k_hier_tick)

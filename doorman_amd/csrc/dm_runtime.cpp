@@ -54,14 +54,13 @@ hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_
                                     hipStream_t st);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
 hipError_t launch_decide(const DevParams& p, const ReqItem* items, int nitems, const ReqArgs& q, hipStream_t st);
-hipError_t fd_prep(const DevParams& p, const ReqItem* items, const ReqArgs& q, const FastArgs& fa, int nfast,
-                   hipStream_t st);
+hipError_t fd_rows(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
+                   const FastArgs& fa, hipStream_t st);
 hipError_t fd_item(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
                    const FastArgs& fa, FdScan* part, hipStream_t st);
 hipError_t fd_item_sorted(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
                           const FastArgs& fa, FdScan* part, hipStream_t st);
-hipError_t fd_sort_keys(void* temp, size_t* bytes, const double* in, double* out, int64_t n, int nseg,
-                        const int64_t* begin, const int64_t* end, hipStream_t st);
+hipError_t fd_sort_keys(void* temp, size_t* bytes, const double* in, double* out, int64_t n, hipStream_t st);
 hipError_t fd_sort_pairs(void* temp, size_t* bytes, const double* kin, double* kout, const int32_t* vin,
                          int32_t* vout, int64_t n, int nseg, const int64_t* begin, const int64_t* end,
                          hipStream_t st);
@@ -352,6 +351,9 @@ struct dm_ctx {
   DBuf<FdScan> fd_sc, fd_ps, fd_part;
   DBuf<int32_t> fd_evs_in, fd_evs, fd_ecnt, fd_bdc;
   DBuf<double2> fd_esum, fd_bds;
+  DBuf<FdClean> fd_pc;
+  DBuf<FdScan> fd_pt;
+  DBuf<FdLind> fd_ld;
   DBuf<uint8_t> fd_tmp;
   // dm_publish_totals: the workgroups' validation flags and their arrival counter
   // (k_publish; both return to zero after each launch)
@@ -466,7 +468,7 @@ struct dm_ctx {
     fd_items.release(); fd_res.release(); fd_prev.release(); fd_bounds.release(); fd_pw.release(); fd_v.release();
     fd_keys.release(); fd_keys_s.release(); fd_ev_in.release(); fd_ev.release(); fd_sc.release(); fd_ps.release();
     fd_part.release(); fd_evs_in.release(); fd_evs.release(); fd_ecnt.release(); fd_bdc.release(); fd_esum.release();
-    fd_bds.release(); fd_tmp.release();
+    fd_bds.release(); fd_tmp.release(); fd_pc.release(); fd_pt.release(); fd_ld.release();
     if (h_flags) (void)hipHostFree(h_flags);
     h_flags = nullptr;
   }
@@ -1291,7 +1293,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   // round qualifies (FastRes::ok); k_decide takes every item it does not.
   std::vector<FastItem> fitems;
   std::vector<int64_t> prev;
-  int64_t m_off = 0, e_off = 0, b_off = 0;
+  int64_t m_off = 0, e_off = 0, b_off = 0, c_off = 0;
   for (size_t ii = 0; c->decide_fast && ii < items.size(); ++ii) {
     ReqItem& itm = items[ii];
     const int64_t K = itm.qhi - itm.qlo;
@@ -1306,16 +1308,22 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
     f.m0 = m_off;
     f.e0 = e_off;
     f.b0 = b_off;
+    f.c0 = c_off;
+    f.nch = (int32_t)std::max<int64_t>(1, (f.n + kFdRows - 1) / kFdRows);
     m_off += f.n + 1;
     e_off += 2 * K;
     b_off += f.nblk;
+    c_off += f.nch;
     itm.fast = (int32_t)fitems.size() + 1;
     fitems.push_back(f);
     std::unordered_map<int64_t, int64_t> last;
     last.reserve((size_t)(2 * K));
     for (int64_t k = itm.qlo; k < itm.qhi; ++k) {
       auto f2 = last.find(srows[(size_t)k]);
-      if (f2 != last.end()) prev[(size_t)k] = f2->second;
+      if (f2 != last.end()) {
+        prev[(size_t)k] = f2->second;
+        fitems.back().repeats = 1;
+      }
       last[srows[(size_t)k]] = k;
     }
   }
@@ -1343,8 +1351,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   p.recompute = 0;
   const int nfast = (int)fitems.size();
   FastArgs fa{};
-  const int64_t* d_kb = nullptr;
-  const int64_t *d_ke = nullptr, *d_eb = nullptr, *d_ee = nullptr;
+  const int64_t *d_eb = nullptr, *d_ee = nullptr;
   int neb = 0;
   size_t need = 0, need2 = 0;
   if (nfast > 0) {
@@ -1365,33 +1372,34 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
     DM_HIP(c, c->fd_esum.ensure((size_t)(b_off * (2 * kFdBlock + 1))), "fast path");
     DM_HIP(c, c->fd_bdc.ensure((size_t)b_off), "fast path");
     DM_HIP(c, c->fd_bds.ensure((size_t)b_off), "fast path");
+    DM_HIP(c, c->fd_pc.ensure((size_t)c_off), "fast path");
+    DM_HIP(c, c->fd_pt.ensure((size_t)c_off), "fast path");
+    DM_HIP(c, c->fd_ld.ensure((size_t)n), "fast path");
     int64_t most = 1;
     for (const FastItem& f : fitems) most = std::max(most, std::max(f.K, f.n + 1));
     DM_HIP(c, c->fd_part.ensure((size_t)((most + kFdChunk - 1) / kFdChunk)), "fast path");
-    // segment bounds of the sorts: each item's wants, each event block
-    std::vector<int64_t> kb, ke, eb, ee;
-    for (const FastItem& f : fitems) {
-      kb.push_back(f.m0);
-      ke.push_back(f.m0 + f.n);
+    // segment bounds of the event blocks' sort
+    std::vector<int64_t> eb, ee;
+    for (const FastItem& f : fitems)
       for (int64_t b = 0; b < f.nblk; ++b) {
         eb.push_back(f.e0 + 2 * b * kFdBlock);
         ee.push_back(f.e0 + 2 * std::min<int64_t>(f.K, (b + 1) * kFdBlock));
       }
-    }
     neb = (int)eb.size();
-    std::vector<int64_t> bounds(kb);
-    bounds.insert(bounds.end(), ke.begin(), ke.end());
-    bounds.insert(bounds.end(), eb.begin(), eb.end());
+    std::vector<int64_t> bounds(eb);
     bounds.insert(bounds.end(), ee.begin(), ee.end());
     DM_HIP(c, upload(c->fd_bounds, bounds.data(), bounds.size(), st), "fast path");
-    d_kb = c->fd_bounds.p;
-    d_ke = d_kb + kb.size();
-    d_eb = d_ke + ke.size();
+    d_eb = c->fd_bounds.p;
     d_ee = d_eb + eb.size();
     fa = FastArgs{c->fd_items.p, c->fd_res.p,    c->fd_prev.p, c->fd_pw.p,    c->fd_v.p,      c->fd_sc.p,
                   c->fd_keys.p,  c->fd_keys_s.p, c->fd_ps.p,   c->fd_ev_in.p, c->fd_evs_in.p, c->fd_ev.p,
-                  c->fd_evs.p,   c->fd_ecnt.p,   c->fd_esum.p, c->fd_bdc.p,   c->fd_bds.p};
-    DM_HIP(c, fd_sort_keys(nullptr, &need, c->fd_keys.p, c->fd_keys_s.p, m_off, nfast, d_kb, d_ke, st), "fast path");
+                  c->fd_evs.p,   c->fd_ecnt.p,   c->fd_esum.p, c->fd_bdc.p,   c->fd_bds.p,    c->fd_pc.p,
+                  c->fd_pt.p,    c->fd_ld.p};
+    for (const FastItem& f : fitems) {
+      size_t b1 = 0;
+      DM_HIP(c, fd_sort_keys(nullptr, &b1, c->fd_keys.p + f.m0, c->fd_keys_s.p + f.m0, f.n, st), "fast path");
+      need = std::max(need, b1);
+    }
     DM_HIP(c, fd_sort_pairs(nullptr, &need2, c->fd_ev_in.p, c->fd_ev.p, c->fd_evs_in.p, c->fd_evs.p, e_off, neb, d_eb,
                             d_ee, st),
            "fast path");
@@ -1403,15 +1411,15 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   auto launches = [&]() -> hipError_t {
     hipError_t e = hipSuccess;
     if (nfast > 0) {
-      if ((e = fd_prep(p, c->rq_items.p, q, fa, nfast, st)) != hipSuccess) return e;
-      for (int s2 = 0; s2 < nfast; ++s2)
-        if ((e = fd_item(p, items[(size_t)fitems[(size_t)s2].item], fitems[(size_t)s2], s2, q, fa, c->fd_part.p,
-                         st)) != hipSuccess)
+      for (int s2 = 0; s2 < nfast; ++s2) {
+        const FastItem& f = fitems[(size_t)s2];
+        if ((e = fd_rows(p, items[(size_t)f.item], f, s2, q, fa, st)) != hipSuccess) return e;
+        if ((e = fd_item(p, items[(size_t)f.item], f, s2, q, fa, c->fd_part.p, st)) != hipSuccess) return e;
+        size_t t1 = c->fd_tmp.n;
+        if ((e = fd_sort_keys(c->fd_tmp.p, &t1, c->fd_keys.p + f.m0, c->fd_keys_s.p + f.m0, f.n, st)) != hipSuccess)
           return e;
-      size_t t1 = c->fd_tmp.n, t2 = c->fd_tmp.n;
-      if ((e = fd_sort_keys(c->fd_tmp.p, &t1, c->fd_keys.p, c->fd_keys_s.p, m_off, nfast, d_kb, d_ke, st)) !=
-          hipSuccess)
-        return e;
+      }
+      size_t t2 = c->fd_tmp.n;
       if ((e = fd_sort_pairs(c->fd_tmp.p, &t2, c->fd_ev_in.p, c->fd_ev.p, c->fd_evs_in.p, c->fd_evs.p, e_off, neb,
                              d_eb, d_ee, st)) != hipSuccess)
         return e;

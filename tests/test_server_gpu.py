@@ -459,7 +459,8 @@ def test_decide_fast_path_matches_sequential_oracle(seed):
     """dm_decide's fast path (dm_decide_fast.hip: resources with >= 64 requests whose
     requests keep every count) against the oracle's literal replay of the whole round,
     and against the one-workgroup replay (DM_DECIDE_FAST=0): FairShare and
-    ProportionalShare resources of several sizes, rounds of 1-3 requests per client
+    ProportionalShare resources of several sizes, rounds of one request per client
+    (the grants' recurrence as a scan of max-plus maps) and of 1-3 requests per client
     (clients asking twice see their own earlier Assign), wants unchanged, new, tied,
     subclient counts 1 and 3, rounds longer than one event block (2048 requests);
     one resource gets a request with another count (the fast path declines it) and
@@ -479,8 +480,12 @@ def test_decide_fast_path_matches_sequential_oracle(seed):
     W.add_store_sums(snap)
     rows, wants, sub = [], [], []
     for r, n in enumerate(sizes):
-        K = int(n * rng.choice([1.0, 1.5, 2.5]))
-        rr = so[r] + rng.integers(0, n, K)
+        if r % 2 == 0:  # every client once (the grants' recurrence as a scan)
+            rr = so[r] + rng.permutation(n)
+            K = n
+        else:  # some clients two or three times (the recurrence in order)
+            K = int(n * rng.choice([1.0, 1.5, 2.5]))
+            rr = so[r] + rng.integers(0, n, K)
         cw = snap["wants"][rr]
         fresh = rng.uniform(0.0, 3.0, K) * snap["capacity"][r] / n * s0[r]
         w = np.where(rng.random(K) < 0.4, cw, fresh)
