@@ -343,6 +343,7 @@ def timed_steps(torch, eng, step, steps, warmup, sync_ranks, extra_warm=True, al
     ev0.record(ext)
     for _ in range(steps):
         step()
+    t_enq = time.perf_counter() - t0  # host time to enqueue the steps (the GPU runs behind it)
     eng.join()  # every class stream's work before the closing event
     ev1.record(ext)
     eng.sync()
@@ -362,7 +363,8 @@ def timed_steps(torch, eng, step, steps, warmup, sync_ranks, extra_warm=True, al
         e.sync()
         ktimes.update(e.kernel_times())
         e.set_profiling(False)
-    return {"elapsed": elapsed, "stream_ms": stream_ms, "ktimes": ktimes, "warm_run": max(warmup, 1) + extra}
+    return {"elapsed": elapsed, "stream_ms": stream_ms, "ktimes": ktimes, "warm_run": max(warmup, 1) + extra,
+            "host_enqueue_s": t_enq}
 
 
 def roofline_of(workload, snap, run, steps, single_kernel_tick):
@@ -538,6 +540,9 @@ def exchange_self_check(torch, dist, ht, leaf, root, bounds, rank, world, g, now
     finally:
         ht.gather = gather0
     k = (ht.step - 1) % len(ht.totals)
+    if corrupt and rank == world - 1 and ht.native is not None:  # (the library gathered it: corrupt the copy)
+        ht.gathered[k][1, 0] += 1.0
+        torch.cuda.synchronize()
     gathered = ht.gathered[k].cpu().numpy().copy()
     S = ht.stride
     own = ht.totals[k].cpu().numpy()
@@ -634,6 +639,10 @@ def main():
                          "copied in place of the RCCL all-gather -- and the root round), on the exchange's own stream "
                          "as at N > 1; prints the rank's step time (not a whole-node measurement)")
     ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--exchange", default="native", choices=["native", "python"],
+                    help="native: each step is one library call (dm_hier_step: the leaf tick, then the block "
+                         "gathered by the library's own RCCL communicator and the root round on the exchange "
+                         "stream); python: the same sequence from Python (torch.distributed all-gather)")
     ap.add_argument("--check-corrupt", action="store_true",
                     help="test only: the exchange self-check's step corrupts one rank's gathered copy (expect "
                          "dist.consistent false)")
@@ -725,6 +734,26 @@ def main():
             dst[s_rank * stride:(s_rank + 1) * stride].copy_(src)
         return gather
 
+    exchange_used = {"mode": None}
+
+    def exchange_mode(stride):
+        """How the exchange runs: (native mode, RCCL id) for HierarchicalTick."""
+        if args.exchange == "python" or args.no_pipeline:
+            exchange_used["mode"] = "python"
+            return None, None
+        if world > 1 and gloo:  # the rehearsal of N ranks on one GPU: through host memory, from Python
+            exchange_used["mode"] = "python (gloo)"
+            return None, None
+        if world > 1:  # one RCCL communicator of the library's own, its id from rank 0
+            from doorman_amd.hierarchy import rccl_unique_id
+            obj = [rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            exchange_used["mode"] = "native (dm_hier_step, library RCCL all-gather over xGMI)"
+            return "rccl", obj[0]
+        exchange_used["mode"] = "native (dm_hier_step" + (", rehearsal: local copy of this rank's block)"
+                                                          if args.rehearse_shard else ")")
+        return "local", None
+
     def measure(layout):
         """Load this rank's store (and root copy), run the timed steps; returns the run,
         the snapshot and the engines (closed by the caller)."""
@@ -745,9 +774,12 @@ def main():
                 bounds = c3_bounds(s_world)
                 root.load(root_snapshot(C3_R, 1, W.FAIR_SHARE, 1000.0, lease_length_s=20))
                 stride = 1 + int(np.diff(bounds).max())
-                ht = HierarchicalTick(torch, eng, root, C3_R, s_world, s_rank,
-                                      rehearsal_gather(stride) if args.rehearse_shard else gather,
-                                      shard_lo=bounds, pipelined=not args.no_pipeline)
+                native, comm_id = exchange_mode(stride)
+                gfn = rehearsal_gather(stride) if args.rehearse_shard else gather
+                ht = HierarchicalTick(torch, eng, root, C3_R, s_world, s_rank, gfn, shard_lo=bounds,
+                                      pipelined=not args.no_pipeline, native=native, comm_id=comm_id)
+                if native == "local" and args.rehearse_shard:  # the other ranks' blocks, synthesized once
+                    gfn(ht.totals[0], ht.gathered[0])
             else:
                 root.load(root_snapshot(R, world, W.FAIR_SHARE, np.asarray(snap["capacity"]) * world,
                                         lease_length_s=20))
@@ -845,11 +877,13 @@ def main():
                        "parallelism": (f"intermediate-server hierarchy x{world}, {layout}" if hier
                                        else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
+            "exchange": exchange_used["mode"] if hier else None,
             "dist": (((dist_info or {}) | {"consistent": run["self_check"]["consistent"],
                                           "check_sample": run["self_check"]["sample"],
                                           "exchange_check": run["self_check"]})
                      if run.get("self_check") else dist_info),
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "host_enqueue_us_per_step": round(run["host_enqueue_s"] / args.steps * 1e6, 2),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
                         for k, v in run["ktimes"].items()},
             "roofline": roofline,

@@ -16,6 +16,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "doorman_hip.h")
 
 DM_OK, DM_E_INVAL, DM_E_HIP, DM_E_STATE, DM_E_KIND, DM_E_RANGE, DM_E_ARGUMENT = 0, -1, -2, -3, -4, -5, -6
 DM_HIER_INVALID, DM_HIER_COUNT_RANGE = 1, 2
+DM_RCCL_ID_BYTES = 128
 DM_WRITEBACK, DM_AGG_RECOMPUTE, DM_ASYNC, DM_WB_INPLACE, DM_WB_ALTERNATE, DM_DEFER_JOIN = 1, 2, 4, 8, 16, 32
 
 
@@ -110,6 +111,11 @@ _SIGS = {
     "dm_hier_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64]),
     "dm_hier_pipeline": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_publish_ring": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "dm_hier_attach": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_hier_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "dm_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "dm_hier_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),

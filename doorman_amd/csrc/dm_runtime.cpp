@@ -3,7 +3,9 @@
 // Owns the device-resident columnar lease store (one context per GPU), builds
 // the size-binned dispatch plan from the segment offsets, launches a tick on the
 // context's HIP stream and reads results back.  See DESIGN.md §3-§5.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl is loaded when the first communicator is made
 
 #include <algorithm>
 #include <cmath>
@@ -370,6 +372,14 @@ struct dm_ctx {
   int64_t hier_stride = 0;
   DBuf<uint32_t> hier_status;
   int hier_servers = 0;
+  // dm_hier_attach / dm_hier_step (root side): the leaf it serves, its ring and gathered
+  // buffer, its server index; the exchange's RCCL communicator (dm_hier_comm_init)
+  dm_ctx* hs_leaf = nullptr;
+  int hs_server = 0;
+  std::vector<void*> hs_ring;
+  void* hs_gathered = nullptr;
+  ncclComm_t nccl_comm = nullptr;
+  bool hs_ordered = false;  // dm_hier_step already ordered the exchange stream after the tick
   // leaf side: pipelined templates (dm_hier_pipeline).  An exchange stages this
   // leaf's new templates in a free slot; the leaf's ticks take the staged templates
   // of the exchanges enqueued before the previous tick (one tick of lag).
@@ -795,9 +805,17 @@ int dm_create(int device, dm_ctx** out) {
   return DM_OK;
 }
 
+struct RcclApi;
+static const RcclApi* rccl_api();
+static void rccl_destroy(const RcclApi* r, ncclComm_t comm);
+
 void dm_destroy(dm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->nccl_comm) {
+    rccl_destroy(rccl_api(), c->nccl_comm);
+    c->nccl_comm = nullptr;
+  }
   // deferred tick work (DM_DEFER_JOIN) and update copies may still run on the
   // auxiliary streams: drain every stream before any buffer is freed
   for (int i = 0; i < dm_ctx::kAux; ++i)
@@ -2038,7 +2056,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   DM_HIP(root, root->hier_status.ensure((size_t)kHierMaxServers), "hierarchy status");
   root->hier_servers = n_servers;
   const bool same = root->stream == leaf->stream;
-  if (!same) {  // the root round after the leaf's prior work (its publish)
+  if (!same && !root->hs_ordered) {  // the root round after the leaf's prior work (its publish)
     DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->root order");
   }
   ResCfg* tcfg = leaf->cfg.p;
@@ -2116,6 +2134,125 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   root->last_writeback = true;
   root->have_result = true;
   return DM_OK;
+}
+
+// librccl, loaded on first use: the copy torch already mapped if there is one (one
+// RCCL per process), else ROCm's
+struct RcclApi {
+  void* h = nullptr;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+static const RcclApi* rccl_api() {
+  static RcclApi api;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    for (const char* n : names)
+      if ((api.h = dlopen(n, RTLD_NOW | RTLD_NOLOAD))) break;
+    for (int i = 0; !api.h && i < 3; ++i) api.h = dlopen(names[i], RTLD_NOW);
+    if (api.h) {
+      api.get_unique_id = (decltype(api.get_unique_id))dlsym(api.h, "ncclGetUniqueId");
+      api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(api.h, "ncclCommInitRank");
+      api.all_gather = (decltype(api.all_gather))dlsym(api.h, "ncclAllGather");
+      api.comm_destroy = (decltype(api.comm_destroy))dlsym(api.h, "ncclCommDestroy");
+      api.error_string = (decltype(api.error_string))dlsym(api.h, "ncclGetErrorString");
+      if (!api.get_unique_id || !api.comm_init_rank || !api.all_gather || !api.comm_destroy || !api.error_string)
+        api.h = nullptr;
+    }
+  }
+  return api.h ? &api : nullptr;
+}
+static void rccl_destroy(const RcclApi* r, ncclComm_t comm) {
+  if (r && comm) (void)r->comm_destroy(comm);
+}
+
+int dm_rccl_unique_id(void* id_out) {
+  if (!id_out) return DM_E_INVAL;
+  const RcclApi* r = rccl_api();
+  if (!r) {
+    g_last_error = "librccl not found";
+    return DM_E_STATE;
+  }
+  ncclUniqueId id;
+  const ncclResult_t e = r->get_unique_id(&id);
+  if (e != ncclSuccess) {
+    g_last_error = std::string("ncclGetUniqueId: ") + r->error_string(e);
+    return DM_E_HIP;
+  }
+  memcpy(id_out, &id, sizeof id);
+  return DM_OK;
+}
+
+int dm_hier_comm_init(dm_ctx* root, const void* id, int nranks, int rank) {
+  DM_ENTER(root);
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) return root->fail(DM_E_INVAL, "bad communicator arguments");
+  if (root->nccl_comm) return root->fail(DM_E_STATE, "the exchange already has a communicator");
+  const RcclApi* r = rccl_api();
+  if (!r) return root->fail(DM_E_STATE, "librccl not found");
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  const ncclResult_t e = r->comm_init_rank(&root->nccl_comm, nranks, uid, rank);
+  if (e != ncclSuccess) {
+    root->nccl_comm = nullptr;
+    return root->fail(DM_E_HIP, std::string("ncclCommInitRank: ") + r->error_string(e));
+  }
+  return DM_OK;
+}
+
+int dm_hier_attach(dm_ctx* leaf, dm_ctx* root, int server, void* const* ring, int nring, void* gathered,
+                   void* exchange_stream) {
+  DM_ENTER(root);
+  if (!leaf || leaf->device != root->device) return root->fail(DM_E_INVAL, "the leaf must share the root's device");
+  if (root->hier_G == 0) return root->fail(DM_E_STATE, "set the exchange's layout first (dm_hier_layout)");
+  if (server < 0 || server >= root->hier_G) return root->fail(DM_E_RANGE, "server index out of range");
+  if (nring < 3 || !ring) return root->fail(DM_E_INVAL, "the publish ring needs at least 3 blocks");
+  if (root->hier_G > 1 && !gathered) return root->fail(DM_E_INVAL, "several servers need a gathered buffer");
+  int rc = dm_publish_ring(leaf, nring, ring);
+  if (rc) return rc;
+  if ((rc = dm_hier_pipeline(leaf, 1))) return rc;
+  if ((rc = dm_set_stream(root, exchange_stream ? exchange_stream : leaf->stream))) return rc;
+  root->hs_leaf = leaf;
+  root->hs_server = server;
+  root->hs_ring.assign(ring, ring + nring);
+  root->hs_gathered = gathered;
+  return DM_OK;
+}
+
+int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
+  DM_CHECK_CTX(root);
+  if (!leaf || root->hs_leaf != leaf) return root->fail(DM_E_STATE, "dm_hier_attach this leaf to the root first");
+  int rc = dm_apportion(leaf, now_ns, DM_WRITEBACK | DM_ASYNC | DM_DEFER_JOIN);
+  if (rc) return rc;
+  const int64_t n = (int64_t)root->hs_ring.size();
+  void* block = root->hs_ring[(size_t)((leaf->pub_k - 1) % n)];  // what this tick published
+  const int G = root->hier_G;
+  const void* gathered = block;
+  if (G > 1) {
+    DM_HIP(root, leaf->join_aux(), "join leaf streams");
+    // the exchange stream after the tick that wrote the block
+    DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->exchange order");
+    const size_t bytes = (size_t)root->hier_stride * 16;
+    if (root->nccl_comm) {  // every server's block, in server order, over xGMI
+      const RcclApi* r = rccl_api();
+      const ncclResult_t e = r->all_gather(block, root->hs_gathered, (size_t)root->hier_stride * 2, ncclFloat64,
+                                           root->nccl_comm, root->stream);
+      if (e != ncclSuccess) return root->fail(DM_E_HIP, std::string("ncclAllGather: ") + r->error_string(e));
+    } else {  // a rehearsal: this server's slot only
+      DM_HIP(root, hipMemcpyAsync((char*)root->hs_gathered + (size_t)root->hs_server * bytes, block, bytes,
+                                  hipMemcpyDeviceToDevice, root->stream),
+             "gather (local)");
+    }
+    gathered = root->hs_gathered;
+  }
+  root->hs_ordered = G > 1;
+  rc = dm_hier_root_tick(root, gathered, G, now_ns, leaf, root->hs_server);
+  root->hs_ordered = false;
+  return rc;
 }
 
 int dm_hier_status(dm_ctx* root, uint32_t* status, int n) {

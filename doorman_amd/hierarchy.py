@@ -29,6 +29,15 @@ import numpy as np
 from . import workloads as W
 
 
+def rccl_unique_id() -> bytes:
+    """dm_rccl_unique_id: a new id for the exchange's RCCL communicator (rank 0)."""
+    from . import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(_lib.DM_RCCL_ID_BYTES)
+    _lib.check(L.dm_rccl_unique_id(buf), None, L)
+    return buf.raw
+
+
 def partition(seg_sizes, world: int) -> np.ndarray:
     """Contiguous resource ranges balanced by lease count: boundaries b[0..world]
     with shard k = resources [b[k], b[k+1])."""
@@ -91,12 +100,20 @@ class HierarchicalTick:
     Otherwise every tick first runs its exchange, stream-ordered on one stream."""
 
     def __init__(self, torch, leaf, root, n_resources: int, n_servers: int, server: int, gather, shard_lo=None,
-                 pipelined: bool = False):
+                 pipelined: bool = False, native: str | None = None, comm_id: bytes | None = None):
+        """native: the whole pipelined step in one library call (dm_hier_step) instead of
+        the Python sequence below -- "rccl": the blocks gathered by the library's own RCCL
+        communicator (comm_id: rank 0's dm_rccl_unique_id, the same bytes on every rank;
+        dm_hier_comm_init is collective), "local": without a collective (one server, or one
+        rank's rehearsal: its block copied into its slot of `gather`-less gathered buffer)."""
         from . import _lib
         self.torch = torch
         self.leaf, self.root = leaf, root
         self.R, self.G, self.g = n_resources, n_servers, server
         self.gather = gather
+        self.native = native
+        if native is not None:
+            assert native in ("rccl", "local") and pipelined, "dm_hier_step is the pipelined step"
         self.pipelined = pipelined
         L = root._L
         if shard_lo is None:
@@ -139,7 +156,16 @@ class HierarchicalTick:
         root.set_stream(self.xstream.cuda_stream)
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1 if pipelined else 0), leaf._ctx, leaf._L)
         ring = (ctypes.c_void_p * nbuf)(*[t.data_ptr() for t in self.totals])
-        _lib.check(leaf._L.dm_publish_ring(leaf._ctx, nbuf if pipelined else 0, ring), leaf._ctx, leaf._L)
+        if native is None:
+            _lib.check(leaf._L.dm_publish_ring(leaf._ctx, nbuf if pipelined else 0, ring), leaf._ctx, leaf._L)
+            return
+        if native == "rccl":
+            assert comm_id is not None and len(comm_id) == _lib.DM_RCCL_ID_BYTES
+            idb = ctypes.create_string_buffer(bytes(comm_id), _lib.DM_RCCL_ID_BYTES)
+            _lib.check(L.dm_hier_comm_init(root._ctx, idb, self.G, self.g), root._ctx, L)
+        gp = self.gathered[0].data_ptr() if self.G > 1 else None
+        _lib.check(L.dm_hier_attach(leaf._ctx, root._ctx, self.g, ring, nbuf, gp, self.xstream.cuda_stream),
+                   root._ctx, L)
 
     def exchange(self, now_ns: int):
         """publish -> all-gather -> the root's round -> this server's new templates
@@ -178,6 +204,14 @@ class HierarchicalTick:
                                                    f"(flags {st[bad].tolist()}: 1 = num_clients < 1, 2 = Count >= 2^31)")
 
     def tick(self, now_ns: int, asynchronous: bool = False):
+        if self.native is not None:  # the leaf tick + the exchange in one library call
+            from . import _lib
+            self.step += 1
+            _lib.check(self.root._L.dm_hier_step(self.leaf._ctx, self.root._ctx, int(now_ns)), self.root._ctx,
+                       self.root._L)
+            if not asynchronous:
+                self.sync()
+            return
         if self.pipelined:  # the tick (templates staged one exchange ago; it publishes its block), then
             # this step's exchange of that block
             self.leaf.apportion(now_ns, writeback=True, asynchronous=True)

@@ -318,6 +318,35 @@ int dm_hier_pipeline(dm_ctx* leaf, int on);
 #define DM_HIER_COUNT_RANGE 2u
 int dm_hier_status(dm_ctx* root, uint32_t* status, int n_servers);
 
+/* ---- one intermediate server's whole step in one call ----
+ * The reference's intermediate serves its clients and refreshes its own lease upstream
+ * on a loop of its own (server.go:227-323).  dm_hier_step does both for one step with no
+ * host round trip in between: the leaf's writeback tick (dm_apportion, its block
+ * published into the ring), then on the exchange stream the block gathered from every
+ * server and the root's round (dm_hier_root_tick) staging this server's templates for the
+ * leaf's next-but-one tick (dm_hier_pipeline).  The blocks are gathered by
+ *   - the RCCL communicator of dm_hier_comm_init: one ncclAllGather over xGMI of every
+ *     server's block (stride records each) into the gathered buffer;
+ *   - without one, with one server: nothing (the root reads the ring block in place);
+ *   - without one, with several servers (a rehearsal of one rank of a node on one GPU):
+ *     this server's block copied into its slot, the other slots as the caller left them.
+ * dm_hier_attach binds the pair once: the ring (nring >= 3 device blocks of `stride`
+ * double2 records, as dm_publish_ring), the gathered buffer (n_servers x stride records;
+ * unused with one server), the exchange stream (NULL: the leaf's), the server index; it
+ * needs dm_hier_layout on the root and turns dm_hier_pipeline on for the leaf.  The
+ * per-step host work is then a handful of stream operations: a step of a small shard
+ * stays device-bound instead of host-bound. */
+int dm_hier_attach(dm_ctx* leaf, dm_ctx* root, int server, void* const* ring, int nring, void* gathered,
+                   void* exchange_stream);
+int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns);
+/* RCCL communicator of the exchange (librccl, loaded when first needed): rank 0 creates
+ * the id (id_out: DM_RCCL_ID_BYTES bytes), every rank passes it to dm_hier_comm_init with
+ * the node's rank count and its rank (collective: every rank must call it).  One rank
+ * per GPU; the root context keeps the communicator until dm_destroy. */
+#define DM_RCCL_ID_BYTES 128
+int dm_rccl_unique_id(void* id_out);
+int dm_hier_comm_init(dm_ctx* root, const void* id, int nranks, int rank);
+
 /* Large resources (more than 4096 rows) run on 2048-row chunks in stream-ordered
  * launches (Clean + speculative round 1, round 1 again only where Clean released
  * subclients, FairShare round 2, the map, whose last-arriving chunk per resource writes

@@ -615,3 +615,59 @@ def test_stream_wait_orders_a_foreign_stream_after_the_tick():
     for k, (s, v) in enumerate(zip(shots, vals)):
         got = s.cpu().numpy()[1:, 0]
         assert np.array_equal(got, sizes * v), f"tick {k}: block of another tick"
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_native_step_matches_the_python_step(G):
+    """dm_hier_step (the leaf tick and the exchange in one library call, dm_hier_attach)
+    against the same pipelined sequence run from Python (HierarchicalTick without
+    `native`): server 0 of G, sharded, the other servers' blocks synthesized from their
+    shards' totals (as bench.py --rehearse-shard), its own block copied into its slot
+    each step.  Leases, templates in use, root rows and running sums, bit for bit, over
+    steps whose templates change; and against the reference model for the root rows."""
+    import torch
+    from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import HierarchicalTick, partition, root_snapshot
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(404 + G)
+    sizes = rng.integers(5, 900, 40)
+    R = len(sizes)
+    lo = partition(sizes, G)
+    S = 1 + int(np.diff(lo).max())
+    rcfg = root_config(R, rng)
+    full = W.make_snapshot(sizes, rng.uniform(0.2, 3.0, int(sizes.sum())) * 1000.0 / np.repeat(sizes, sizes),
+                           0.0, 1, NOW + 60 * W.NS, W.FAIR_SHARE, 1000.0)
+    others = np.zeros((G * S, 2))
+    for j in range(1, G):
+        sj = W.subset(full, np.arange(lo[j], lo[j + 1]))
+        n = int(lo[j + 1] - lo[j])
+        others[j * S + 1:j * S + 1 + n, 0] = sj["agg_sum_wants"]
+        others[j * S + 1:j * S + 1 + n, 1] = np.asarray(sj["agg_count"], np.int64).view(np.float64)
+    shard = W.subset(full, np.arange(lo[0], lo[1]))
+    runs = []
+    for native in ("local", None):
+        leaf, root = Engine(0), Engine(0)
+        leaf.load(M.with_config(shard, M.default_config(int(lo[1] - lo[0]))))
+        root.load(M.with_config(root_snapshot(R, 1, W.FAIR_SHARE, 1.0), rcfg))
+
+        def gather(src, dst):
+            dst[0:S].copy_(src)
+        ht = HierarchicalTick(torch, leaf, root, R, G, 0, gather, shard_lo=lo, pipelined=True, native=native)
+        if G > 1:
+            ht.gathered[0].copy_(torch.from_numpy(others).to(ht.gathered[0].device))
+        out = []
+        for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 14 * W.NS, NOW + 19 * W.NS]):
+            ht.tick(now)
+            ht.sync()
+            out.append((leaf.leases(), leaf.config(), root.read_store(), root.resources(safe=False)))
+        runs.append(out)
+        leaf.close()
+        root.close()
+    for t, (a, b) in enumerate(zip(*runs)):
+        for x, y in zip(a[0], b[0]):
+            assert x.tobytes() == y.tobytes(), f"step {t}: leases"
+        assert_cfg_equal(a[1], b[1], f"step {t}: templates")
+        for k in ("has", "wants", "subclients", "expiry_ns"):
+            assert a[2][k].tobytes() == b[2][k].tobytes(), f"step {t}: root {k}"
+        for k in ("count", "sum_has", "sum_wants"):
+            assert a[3][k].tobytes() == b[3][k].tobytes(), f"step {t}: root running {k}"

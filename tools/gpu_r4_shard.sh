@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4shard
 rm -rf $OUT; mkdir -p $OUT
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-timeout -k 10 600 python -u -m pytest -x -q -s --timeout 300 --timeout-method thread tests/test_server_gpu.py tests/test_hierarchy_gpu.py tests/test_hierarchy_dist_gpu.py tests/test_large_gpu.py tests/test_c3_full_gpu.py tests/test_parity_gpu.py::test_arrivals_without_expiry_need_a_clock > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q -s --timeout 300 --timeout-method thread tests/test_hierarchy_gpu.py tests/test_hierarchy_dist_gpu.py tests/test_large_gpu.py tests/test_c3_full_gpu.py tests/test_parity_gpu.py::test_arrivals_without_expiry_need_a_clock > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 fi
 for n in ${SHARDS:-8 4 2}; do
