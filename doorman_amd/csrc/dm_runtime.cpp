@@ -187,6 +187,12 @@ struct dm_ctx {
     bool val = false;         // a stream-memory signal (else an event)
   };
   bool xs_values = false;      // every token as stream memory (DM_XS_VALUES=1)
+  // A pipelined leaf's staged templates from another stream: the host waits for the
+  // exchange that made them and the leaf's stream gets no barrier (a queue waiting on
+  // another queue here costs ~12-16 us even when the signal is long set -- the step of
+  // an N = 8 shard idled that long every tick, tools/step_trace.py); the host stays at
+  // most ~one step ahead, the device never waits.  DM_TPL_HOSTWAIT=0: the barrier.
+  bool tpl_hostwait = true;
   bool xs_can_value = false;   // signal words allocated
   // the staged templates' hop -- the only one a pipelined leaf tick waits on -- as
   // stream memory (DM_XS_READY_VALUE=1).  Off: with the exchange on a second stream the
@@ -731,6 +737,7 @@ int dm_create(int device, dm_ctx** out) {
   c->device = device;
   if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
   if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
+  if (const char* hw = getenv("DM_TPL_HOSTWAIT")) c->tpl_hostwait = atoi(hw) != 0;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1030,7 +1037,14 @@ static int commit_templates(dm_ctx* c) {
   c->tpl_pending.erase(c->tpl_pending.begin(), c->tpl_pending.begin() + (ptrdiff_t)n);
   if (take < 0) return DM_OK;
   DM_HIP(c, c->join_aux(), "join");  // deferred class work also read the old templates
-  DM_HIP(c, c->xs_wait(c->tpl_ready[take], c->stream), "staged templates");
+  const dm_ctx::XsTok& rt = c->tpl_ready[take];
+  if (c->tpl_hostwait && rt.rec && !rt.val && rt.s && rt.s != c->stream) {
+    const hipError_t q = hipEventQuery(c->xs_ev[rt.w]);
+    if (q == hipErrorNotReady) DM_HIP(c, hipEventSynchronize(c->xs_ev[rt.w]), "staged templates (host wait)");
+    else if (q != hipSuccess) return c->hip_fail(q, "staged templates");
+  } else {
+    DM_HIP(c, c->xs_wait(rt, c->stream), "staged templates");
+  }
   c->main_dirty = true;  // the class streams fork after the wait
   std::swap(c->cfg, c->tpl_cfg[take]);
   std::swap(c->cold, c->tpl_cold[take]);
