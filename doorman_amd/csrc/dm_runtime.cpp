@@ -1039,9 +1039,11 @@ static int commit_templates(dm_ctx* c) {
   DM_HIP(c, c->join_aux(), "join");  // deferred class work also read the old templates
   const dm_ctx::XsTok& rt = c->tpl_ready[take];
   if (c->tpl_hostwait && rt.rec && !rt.val && rt.s && rt.s != c->stream) {
-    const hipError_t q = hipEventQuery(c->xs_ev[rt.w]);
-    if (q == hipErrorNotReady) DM_HIP(c, hipEventSynchronize(c->xs_ev[rt.w]), "staged templates (host wait)");
-    else if (q != hipSuccess) return c->hip_fail(q, "staged templates");
+    hipError_t q = hipEventQuery(c->xs_ev[rt.w]);
+    for (int spin = 0; q == hipErrorNotReady && spin < (1 << 20); ++spin) q = hipEventQuery(c->xs_ev[rt.w]);  // poll:
+    // the wake-up of a blocking wait comes too late for the next launch to be queued in time
+    if (q == hipErrorNotReady) q = hipEventSynchronize(c->xs_ev[rt.w]);
+    if (q != hipSuccess) return c->hip_fail(q, "staged templates");
   } else {
     DM_HIP(c, c->xs_wait(rt, c->stream), "staged templates");
   }

@@ -151,7 +151,11 @@ class HierarchicalTick:
         # (DM_HIER_XSTREAM=1: a second stream at G = 1 too -- tests and A/B runs of the
         # cross-stream form on one GPU)
         own = self.G > 1 or os.environ.get("DM_HIER_XSTREAM", "0") == "1"
-        self.xstream = torch.cuda.Stream(device=dev) if pipelined and own else self.stream
+        # the exchange's kernels (gather, root round) are few and short, but beside a leaf tick
+        # that fills every CU they wait for slots: a high-priority queue lets them in first
+        # (DM_XPRIO=0: normal priority)
+        prio = -1 if os.environ.get("DM_XPRIO", "1") != "0" else 0
+        self.xstream = torch.cuda.Stream(device=dev, priority=prio) if pipelined and own else self.stream
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1 if pipelined else 0), leaf._ctx, leaf._L)
