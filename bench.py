@@ -553,7 +553,7 @@ def exchange_self_check(torch, dist, ht, leaf, root, bounds, rank, world, g, now
               == lr["count"].astype(np.int64).tobytes())
     if ht.pipelined:  # take the staged templates of this exchange
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 0), leaf._ctx, leaf._L)
-        _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, 1), leaf._ctx, leaf._L)
+        _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, ht.lag), leaf._ctx, leaf._L)
     tpl = leaf.config()
     samples = [(lo + int(i), (pre["wants"][i], pre["has"][i], int(pre["subclients"][i]), int(pre["expiry_ns"][i])),
                 (int(pres["count"][i]), pres["sum_has"][i], pres["sum_wants"][i]),
@@ -776,8 +776,11 @@ def main():
                 stride = 1 + int(np.diff(bounds).max())
                 native, comm_id = exchange_mode(stride)
                 gfn = rehearsal_gather(stride) if args.rehearse_shard else gather
+                # an exchange on a stream of its own (several servers) gets a whole tick to finish
+                # before the leaf takes its templates (two ticks of lag): the leaf never waits
                 ht = HierarchicalTick(torch, eng, root, C3_R, s_world, s_rank, gfn, shard_lo=bounds,
-                                      pipelined=not args.no_pipeline, native=native, comm_id=comm_id)
+                                      pipelined=not args.no_pipeline, native=native, comm_id=comm_id,
+                                      lag=2 if s_world > 1 else 1)
                 if native == "local" and args.rehearse_shard:  # the other ranks' blocks, synthesized once
                     gfn(ht.totals[0], ht.gathered[0])
             else:

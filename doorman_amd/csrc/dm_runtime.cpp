@@ -168,7 +168,7 @@ struct dm_ctx {
   // DM_XS_VALUES=1 every hop as values, DM_XS_READY_VALUE=1 only the staged templates'
   // hop.  A wait on a token signalled on the waiting stream itself is skipped (stream
   // order).
-  static constexpr int kTplSlots = 3;
+  static constexpr int kTplSlots = 4;  // staged templates: in use + pending (lag 2) + the one being written
   enum : int {
     XS_FORK = 0,
     XS_JOIN0 = 1,                       // + aux stream
@@ -390,6 +390,7 @@ struct dm_ctx {
   // leaf's new templates in a free slot; the leaf's ticks take the staged templates
   // of the exchanges enqueued before the previous tick (one tick of lag).
   bool tpl_pipe = false;
+  int tpl_lag = 1;  // ticks between an exchange and the first tick that takes its templates, minus one
   DBuf<ResCfg> tpl_cfg[kTplSlots];
   DBuf<ResCold> tpl_cold[kTplSlots];
   XsTok tpl_ready[kTplSlots];        // root stream: the slot's templates are written
@@ -1032,7 +1033,8 @@ static int ready(dm_ctx* c) {
 static int commit_templates(dm_ctx* c) {
   int take = -1;
   size_t n = 0;
-  while (n < c->tpl_pending.size() && c->tpl_pending[n].tag < c->ticks_issued) take = c->tpl_pending[n++].slot;
+  while (n < c->tpl_pending.size() && c->tpl_pending[n].tag + (c->tpl_lag - 1) < c->ticks_issued)
+    take = c->tpl_pending[n++].slot;
   for (size_t i = 0; i + 1 < n; ++i) c->tpl_free_slots.push_back(c->tpl_pending[i].slot);  // superseded
   c->tpl_pending.erase(c->tpl_pending.begin(), c->tpl_pending.begin() + (ptrdiff_t)n);
   if (take < 0) return DM_OK;
@@ -2020,6 +2022,7 @@ int dm_hier_layout(dm_ctx* root, int n_servers, const int64_t* shard_lo, int64_t
 int dm_hier_pipeline(dm_ctx* leaf, int on) {
   DM_ENTER(leaf);
   if (!leaf->cfg_loaded) return leaf->fail(DM_E_STATE, "load the leaf's configuration first");
+  if (on < 0 || on > dm_ctx::kTplSlots - 1) return leaf->fail(DM_E_INVAL, "pipeline lag must be 0..3");
   if (!on && leaf->tpl_pipe && !leaf->tpl_pending.empty()) {  // take the newest staged templates now
     const int take = leaf->tpl_pending.back().slot;
     DM_HIP(leaf, leaf->xs_wait(leaf->tpl_ready[take], leaf->stream), "staged templates");
@@ -2034,6 +2037,7 @@ int dm_hier_pipeline(dm_ctx* leaf, int on) {
   }
   if (on) DM_HIP(leaf, hipStreamSynchronize(leaf->stream), "template slots");  // no tick still reads a slot
   leaf->tpl_pipe = on != 0;
+  leaf->tpl_lag = on > 1 ? on : 1;
   return DM_OK;
 }
 
@@ -2230,7 +2234,7 @@ int dm_hier_attach(dm_ctx* leaf, dm_ctx* root, int server, void* const* ring, in
   if (root->hier_G > 1 && !gathered) return root->fail(DM_E_INVAL, "several servers need a gathered buffer");
   int rc = dm_publish_ring(leaf, nring, ring);
   if (rc) return rc;
-  if ((rc = dm_hier_pipeline(leaf, 1))) return rc;
+  if ((rc = dm_hier_pipeline(leaf, leaf->tpl_pipe ? leaf->tpl_lag : 1))) return rc;
   if ((rc = dm_set_stream(root, exchange_stream ? exchange_stream : leaf->stream))) return rc;
   root->hs_leaf = leaf;
   root->hs_server = server;

@@ -307,7 +307,9 @@ int dm_hier_root_tick(dm_ctx* root, const void* dev_gathered, int n_servers, int
  * tick of lag, as the reference's intermediate refreshes upstream on its own loop
  * (server.go:227-323) while it keeps serving clients -- so the exchange (publish,
  * all-gather, root round) can run on a stream of its own beside the next leaf tick.
- * At most 3 staged exchanges; off (default) takes the newest staged templates. */
+ * on = 2 or 3: one or two ticks more (an exchange on its own stream then has a whole
+ * tick to finish before the leaf needs it: the leaf never waits for it).  Off (0,
+ * default) takes the newest staged templates. */
 int dm_hier_pipeline(dm_ctx* leaf, int on);
 
 /* Per-server outcome of the last dm_hier_root_tick (waits for it): status[g] = 0 when

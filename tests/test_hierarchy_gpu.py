@@ -434,13 +434,14 @@ def _shard_templates(prev, g, resp, root_cfg, lo):
 CFG_FIELDS_ALL = W.CFG_FIELDS
 
 
-@pytest.mark.parametrize("pipelined,large", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("pipelined,large", [(False, False), (1, False), (1, True), (2, False)])
 def test_sharded_exchange_matches_the_reference_model(pipelined, large):
     """configs[3]'s layout: resources sharded by id over G servers,
     each server an intermediate of its own range; the root (one row per resource,
     its owner's) evaluated redundantly by every server from the gathered blocks.
     Pipelined (dm_hier_pipeline): each leaf tick takes the templates of the exchange
-    enqueued before the previous tick (one tick of lag).  Every step: root copies
+    enqueued before the previous tick (one tick of lag), or (pipelined = 2) one tick
+    later still (the lag bench.py uses when the exchange has a stream of its own).  Every step: root copies
     bit for bit against the model, every leaf's templates bit for bit, leaf leases
     against the oracle on the leaf's store under the templates the model says that
     tick used.  `large`: some leaf resources above 4096 rows, so the leaves' ticks run
@@ -470,7 +471,7 @@ def test_sharded_exchange_matches_the_reference_model(pipelined, large):
         e = Engine(0)
         e.load(M.with_config(shard, cfg))
         if pipelined:
-            _lib.check(L.dm_hier_pipeline(e._ctx, 1), e._ctx)
+            _lib.check(L.dm_hier_pipeline(e._ctx, int(pipelined)), e._ctx)
         leaves.append(e)
         tpl.append(cfg)
         root = Engine(0)
@@ -481,8 +482,9 @@ def test_sharded_exchange_matches_the_reference_model(pipelined, large):
     gathered = torch.zeros((G * S, 2), dtype=torch.float64, device="cuda")
     staged = []  # templates after each exchange, oldest first (pipelined)
     for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 30 * W.NS, NOW + 31 * W.NS]):
-        used = tpl if not pipelined else (staged[t - 2] if t >= 2 else [M.default_config(int(lo[g + 1] - lo[g]))
-                                                                         for g in range(G)])
+        lag = int(pipelined)
+        used = tpl if not pipelined else (staged[t - 1 - lag] if t >= 1 + lag else
+                                          [M.default_config(int(lo[g + 1] - lo[g])) for g in range(G)])
         if pipelined:  # tick first (it takes the exchange of two steps ago), then this step's exchange
             for g in range(G):
                 pre = leaf_snapshot(leaves[g], used[g])
