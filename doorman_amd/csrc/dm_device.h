@@ -145,6 +145,16 @@ struct HetRes {
   int64_t bc[kHetBuckets];  // count of the wantExtra clients
 };
 
+// The tick-done word (dm_apportion): the rest kernel of a one-class split tick -- the
+// tick's last kernel -- stores the tick's sequence number once every workgroup of it has
+// finished, so another queue can wait for the tick on the word (a stream wait on a value)
+// and the tick's own queue gets no marker packet.
+struct TickDone {
+  uint64_t* word;  // signal memory; nullptr: none
+  uint32_t* ctr;   // arrival counter (its last arriver resets it)
+  uint64_t seq;
+};
+
 // row -> resource lookup for store updates: seg_off plus, for every block of
 // 2^kRowBlkShift rows, the resource holding its first row
 constexpr int kRowBlkShift = 12;

@@ -297,7 +297,8 @@ __global__ __launch_bounds__(G) void k_block_dense(DevParams p, WorkItem* __rest
 template <int G, int R>
 __global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restrict__ items,
                                                   const int32_t* __restrict__ queue, int32_t* qcnt, int par,
-                                                  int32_t* host_count, int32_t* general_list, int32_t* general_count) {
+                                                  int32_t* host_count, int32_t* general_list, int32_t* general_count,
+                                                  TickDone td) {
   __shared__ Lds<G> lds;
   const int count = qcnt[par];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -311,6 +312,17 @@ __global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restr
     const int idx = queue[q];
     group_segment<G, R, kRest>(p, items[idx], items + idx, threadIdx.x, lds, general_list, general_count);
     __syncthreads();  // the next item reuses the single-use LDS slots
+  }
+  if (td.word) {  // the tick is done once every workgroup of this, its last kernel, is
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this workgroup's stores, seen from every XCD
+      const uint32_t old = __hip_atomic_fetch_add(td.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        __hip_atomic_store(td.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(td.word, td.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -2464,16 +2476,17 @@ hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, 
 }
 
 hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipStream_t st) {
+                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, const TickDone& td,
+                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const unsigned rg = (unsigned)std::max(1, std::min(n, rest_grid));
   switch (bin) {
-    case 3: k_block_rest<128, 4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
-    case 4: k_block_rest<128, 8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
-    case 5: k_block_rest<256, 8><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
-    case 6: k_block_rest<256, 16><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount); break;
+    case 3: k_block_rest<128, 4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
+    case 4: k_block_rest<128, 8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
+    case 5: k_block_rest<256, 8><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
+    case 6: k_block_rest<256, 16><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
     case kBin6Wide:
-      k_block_rest<512, 8><<<rg, 512, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount);
+      k_block_rest<512, 8><<<rg, 512, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td);
       break;
     default: return hipErrorInvalidValue;
   }

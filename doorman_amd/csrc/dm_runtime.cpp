@@ -27,7 +27,8 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
                             int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipStream_t st);
+                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, const TickDone& td,
+                           hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
@@ -403,6 +404,16 @@ struct dm_ctx {
   std::vector<Staged> tpl_pending;          // oldest first
   std::vector<int> tpl_free_slots;
   int64_t ticks_issued = 0;
+  // The tick-done word (TickDone): ticks numbered by tick_seq (never reset); a one-class
+  // split tick's rest kernel stores its number when the tick is done.  Another queue
+  // waits on the word (hipStreamWaitValue64) instead of an event recorded on this queue
+  // (each marker on the leaf's queue cost a ~10-us bubble per N = 8 shard step).
+  // DM_TICK_FLAG=0: events only.
+  uint64_t* tick_word = nullptr;
+  uint32_t* tick_ctr = nullptr;
+  uint64_t tick_seq = 0;          // the last tick's number
+  bool tick_flagged = false;      // ... and whether it stores it
+  uint64_t tpl_free_seq[kTplSlots] = {};  // a slot is free once the word reaches this (0: use tpl_free)
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
   bool profiling = false;
@@ -803,6 +814,22 @@ int dm_create(int device, dm_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
+  if (e == hipSuccess && (!getenv("DM_TICK_FLAG") || atoi(getenv("DM_TICK_FLAG")) != 0)) {
+    int can = 0;
+    if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && can &&
+        hipExtMallocWithFlags((void**)&c->tick_word, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess &&
+        hipMalloc((void**)&c->tick_ctr, sizeof(uint32_t)) == hipSuccess &&
+        hipMemset(c->tick_word, 0, sizeof(uint64_t)) == hipSuccess &&
+        hipMemset(c->tick_ctr, 0, sizeof(uint32_t)) == hipSuccess) {
+      e = hipDeviceSynchronize();
+    } else {  // events only
+      (void)hipGetLastError();
+      if (c->tick_word) (void)hipFree(c->tick_word);
+      if (c->tick_ctr) (void)hipFree(c->tick_ctr);
+      c->tick_word = nullptr;
+      c->tick_ctr = nullptr;
+    }
+  }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
@@ -852,6 +879,8 @@ void dm_destroy(dm_ctx* c) {
   for (auto ev : c->ev_bat)
     if (ev) (void)hipEventDestroy(ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->tick_word) (void)hipFree(c->tick_word);
+  if (c->tick_ctr) (void)hipFree(c->tick_ctr);
   delete c;
 }
 
@@ -1053,7 +1082,10 @@ static int commit_templates(dm_ctx* c) {
   std::swap(c->cfg, c->tpl_cfg[take]);
   std::swap(c->cold, c->tpl_cold[take]);
   // the old templates (now in slot `take`) are free after the ticks already enqueued
-  c->xs_signal_lazy(dm_ctx::XS_FREE0 + take, c->stream, &c->tpl_free[take]);  // the next exchange into it waits
+  // the next exchange into it waits for the ticks enqueued so far: on the tick-done word
+  // when the last of them stores it, else on a (lazy) event
+  c->tpl_free_seq[take] = c->tick_flagged ? c->tick_seq : 0;
+  c->xs_signal_lazy(dm_ctx::XS_FREE0 + take, c->stream, &c->tpl_free[take]);
   c->tpl_free_rec[take] = true;
   c->tpl_free_slots.push_back(take);
   return DM_OK;
@@ -1065,6 +1097,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (rc) return rc;
   if (c->tpl_pipe && (rc = commit_templates(c))) return rc;
   c->ticks_issued += 1;
+  c->tick_seq += 1;
+  c->tick_flagged = false;
   const bool wb = flags & DM_WRITEBACK;
   DevParams p{};
   p.seg_off = c->seg_off.p;
@@ -1147,6 +1181,11 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (!c->h_packs.empty()) used |= 1u << c->class_stream[kNumBins];
   if (nch > 0) used |= 1u << c->class_stream[kNumBins + 1];
   const bool fork = __builtin_popcount(used) > 1;
+  int nonempty_bins = 0;
+  for (int b = 0; b < kNumBins; ++b) nonempty_bins += c->h_bins[b].empty() ? 0 : 1;
+  // one work class on the context stream, no kernel after its split bin's rest kernel:
+  // that kernel can store the tick-done word
+  const bool one_class = !fork && nch == 0 && c->h_packs.empty() && !general && nonempty_bins == 1;
   auto cls_stream = [&](int cls) { return fork ? c->aux[c->class_stream[cls]] : st; };
   hipStream_t s_large = cls_stream(kNumBins + 1), s_small = cls_stream(kNumBins);
   if (!fork) {  // everything on the context stream, after any deferred class work
@@ -1244,9 +1283,14 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                  return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc, s);
                }),
                "group kernel (dense split)");
+        TickDone td{nullptr, nullptr, 0};
+        if (one_class && c->tick_word) {
+          td = TickDone{c->tick_word, c->tick_ctr, c->tick_seq};
+          c->tick_flagged = true;
+        }
         DM_HIP(c, timed(KC_REST3 + i, s, [&] {
                  return launch_bin_rest(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
-                                        rest_grid, gl, gc, s);
+                                        rest_grid, gl, gc, td, s);
                }),
                "group kernel (dense split)");
         c->dq_par[i] ^= 1;
@@ -2090,7 +2134,11 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     slot = leaf->tpl_free_slots.front();
     DM_HIP(root, leaf->tpl_cfg[slot].ensure((size_t)leaf->R), "template slot");
     DM_HIP(root, leaf->tpl_cold[slot].ensure((size_t)leaf->R), "template slot");
-    if (leaf->tpl_free_rec[slot])  // the ticks that read the slot's old templates are done
+    if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0)  // the ticks that read the slot's old
+      DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tpl_free_seq[slot],  // templates
+                                        hipStreamWaitValueGte, ~0ull),                           // are done
+             "template slot");
+    else if (leaf->tpl_free_rec[slot])
       DM_HIP(root, leaf->xs_wait(leaf->tpl_free[slot], root->stream), "template slot");
     tcfg = leaf->tpl_cfg[slot].p;
     tcold = leaf->tpl_cold[slot].p;
@@ -2254,8 +2302,13 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
   const void* gathered = block;
   if (G > 1) {
     DM_HIP(root, leaf->join_aux(), "join leaf streams");
-    // the exchange stream after the tick that wrote the block
-    DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->exchange order");
+    // the exchange stream after the tick that wrote the block: on the tick-done word when
+    // the tick stores it (no marker on the leaf's queue), else an event
+    if (leaf->tick_flagged)
+      DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tick_seq, hipStreamWaitValueGte, ~0ull),
+             "leaf->exchange order");
+    else
+      DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->exchange order");
     const size_t bytes = (size_t)root->hier_stride * 16;
     if (root->nccl_comm) {  // every server's block, in server order, over xGMI
       const RcclApi* r = rccl_api();
