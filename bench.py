@@ -776,11 +776,10 @@ def main():
                 stride = 1 + int(np.diff(bounds).max())
                 native, comm_id = exchange_mode(stride)
                 gfn = rehearsal_gather(stride) if args.rehearse_shard else gather
-                # an exchange on a stream of its own (several servers) gets a whole tick to finish
-                # before the leaf takes its templates (two ticks of lag): the leaf never waits
+                # an exchange on a stream of its own gets a whole tick to finish before the leaf
+                # takes its templates (two ticks of lag: HierarchicalTick's default then)
                 ht = HierarchicalTick(torch, eng, root, C3_R, s_world, s_rank, gfn, shard_lo=bounds,
-                                      pipelined=not args.no_pipeline, native=native, comm_id=comm_id,
-                                      lag=2 if s_world > 1 else 1)
+                                      pipelined=not args.no_pipeline, native=native, comm_id=comm_id)
                 if native == "local" and args.rehearse_shard:  # the other ranks' blocks, synthesized once
                     gfn(ht.totals[0], ht.gathered[0])
             else:

@@ -100,7 +100,8 @@ class HierarchicalTick:
     Otherwise every tick first runs its exchange, stream-ordered on one stream."""
 
     def __init__(self, torch, leaf, root, n_resources: int, n_servers: int, server: int, gather, shard_lo=None,
-                 pipelined: bool = False, native: str | None = None, comm_id: bytes | None = None, lag: int = 1):
+                 pipelined: bool = False, native: str | None = None, comm_id: bytes | None = None,
+                 lag: int | None = None):
         """native: the whole pipelined step in one library call (dm_hier_step) instead of
         the Python sequence below -- "rccl": the blocks gathered by the library's own RCCL
         communicator (comm_id: rank 0's dm_rccl_unique_id, the same bytes on every rank;
@@ -158,8 +159,11 @@ class HierarchicalTick:
         self.xstream = torch.cuda.Stream(device=dev, priority=prio) if pipelined and own else self.stream
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
-        # lag: ticks of lag of the pipelined templates (dm_hier_pipeline): 1, or 2 so that an
-        # exchange on its own stream has a whole tick to finish before the leaf takes it
+        # lag: ticks of lag of the pipelined templates (dm_hier_pipeline): default 1 with the
+        # exchange on the leaf's stream, 2 with a stream of its own (the exchange then has a
+        # whole tick to finish before the leaf takes its templates: the leaf never waits)
+        if lag is None:
+            lag = 2 if self.xstream is not self.stream else 1
         self.lag = lag if pipelined else 0
         _lib.check(leaf._L.dm_hier_pipeline(leaf._ctx, self.lag), leaf._ctx, leaf._L)
         ring = (ctypes.c_void_p * nbuf)(*[t.data_ptr() for t in self.totals])

@@ -124,7 +124,7 @@ def test_hierarchical_tick_two_processes_matches_the_reference_model():
 # ---- configs[3]'s layout: one snapshot sharded by resource id, pipelined exchange ----
 RS = 50
 SIZES = np.random.default_rng(21).integers(5, 400, RS)
-STEPS = [NOW, NOW + 4 * W.NS, NOW + 8 * W.NS, NOW + 30 * W.NS]
+STEPS = [NOW, NOW + 4 * W.NS, NOW + 8 * W.NS, NOW + 30 * W.NS, NOW + 34 * W.NS]
 
 
 def _full_snap():
@@ -133,16 +133,16 @@ def _full_snap():
     return s
 
 
-def _rank_sharded(rank, world, port, q):
+def _rank_sharded(rank, world, port, q, lag):
     import traceback
     try:
-        _rank_sharded_body(rank, world, port, q)
+        _rank_sharded_body(rank, world, port, q, lag)
     except Exception:  # report to the parent instead of leaving it waiting
         q.put((rank, "error: " + traceback.format_exc()))
         raise
 
 
-def _rank_sharded_body(rank, world, port, q):
+def _rank_sharded_body(rank, world, port, q, lag):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -161,7 +161,7 @@ def _rank_sharded_body(rank, world, port, q):
         dist.all_gather(parts, src.cpu())
         dst.copy_(torch.cat(parts).to(dst.device))
 
-    ht = HierarchicalTick(torch, leaf, root, RS, world, rank, gather, shard_lo=lo, pipelined=True)
+    ht = HierarchicalTick(torch, leaf, root, RS, world, rank, gather, shard_lo=lo, pipelined=True, lag=lag)
     assert ht.stream.cuda_stream != ht.xstream.cuda_stream
     out = []
     for now in STEPS:
@@ -184,7 +184,8 @@ def _root_cfg_s():
             "safe_capacity": np.where(np.arange(RS) % 3 == 0, 4.5, np.nan)}
 
 
-def test_sharded_pipelined_hierarchical_tick_two_processes():
+@pytest.mark.parametrize("lag", [1, 2])
+def test_sharded_pipelined_hierarchical_tick_two_processes(lag):
     """bench.py's configs[3] path across processes: the resources of one snapshot
     sharded by id over two ranks, each an intermediate server of its range; every
     step a leaf tick, then the pipelined exchange (publish, all-gather, the root's
@@ -198,7 +199,7 @@ def test_sharded_pipelined_hierarchical_tick_two_processes():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_sharded, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_sharded, args=(r, world, port, q, lag)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -218,7 +219,8 @@ def test_sharded_pipelined_hierarchical_tick_two_processes():
     staged = []
     owner = np.searchsorted(lo, np.arange(RS), side="right") - 1
     for t, now in enumerate(STEPS):
-        used = staged[t - 2] if t >= 2 else [M.default_config(int(lo[g + 1] - lo[g])) for g in range(world)]
+        used = (staged[t - 1 - lag] if t >= 1 + lag else
+                [M.default_config(int(lo[g + 1] - lo[g])) for g in range(world)])
         reqs = []
         for g in range(world):
             got = res[g][t]
