@@ -101,7 +101,7 @@ class HierarchicalTick:
 
     def __init__(self, torch, leaf, root, n_resources: int, n_servers: int, server: int, gather, shard_lo=None,
                  pipelined: bool = False, native: str | None = None, comm_id: bytes | None = None,
-                 lag: int | None = None):
+                 lag: int | None = None, comm_ranks: int | None = None):
         """native: the whole pipelined step in one library call (dm_hier_step) instead of
         the Python sequence below -- "rccl": the blocks gathered by the library's own RCCL
         communicator (comm_id: rank 0's dm_rccl_unique_id, the same bytes on every rank;
@@ -173,7 +173,8 @@ class HierarchicalTick:
         if native == "rccl":
             assert comm_id is not None and len(comm_id) == _lib.DM_RCCL_ID_BYTES
             idb = ctypes.create_string_buffer(bytes(comm_id), _lib.DM_RCCL_ID_BYTES)
-            _lib.check(L.dm_hier_comm_init(root._ctx, idb, self.G, self.g), root._ctx, L)
+            nr = self.G if comm_ranks is None else comm_ranks  # (tests: a one-rank communicator on one GPU)
+            _lib.check(L.dm_hier_comm_init(root._ctx, idb, nr, self.g if nr == self.G else 0), root._ctx, L)
         gp = self.gathered[0].data_ptr() if self.G > 1 else None
         _lib.check(L.dm_hier_attach(leaf._ctx, root._ctx, self.g, ring, nbuf, gp, self.xstream.cuda_stream),
                    root._ctx, L)

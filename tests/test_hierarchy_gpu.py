@@ -619,17 +619,19 @@ def test_stream_wait_orders_a_foreign_stream_after_the_tick():
         assert np.array_equal(got, sizes * v), f"tick {k}: block of another tick"
 
 
-@pytest.mark.parametrize("G", [1, 3])
-def test_native_step_matches_the_python_step(G):
+@pytest.mark.parametrize("G,native", [(1, "local"), (3, "local"), (3, "rccl")])
+def test_native_step_matches_the_python_step(G, native):
     """dm_hier_step (the leaf tick and the exchange in one library call, dm_hier_attach)
     against the same pipelined sequence run from Python (HierarchicalTick without
-    `native`): server 0 of G, sharded, the other servers' blocks synthesized from their
+    `native`), with the block gathered in place / copied into its slot ("local") or by
+    ncclAllGather over a one-rank communicator of the library's own ("rccl": dlopen'd
+    librccl, dm_rccl_unique_id, dm_hier_comm_init): server 0 of G, sharded, the other servers' blocks synthesized from their
     shards' totals (as bench.py --rehearse-shard), its own block copied into its slot
     each step.  Leases, templates in use, root rows and running sums, bit for bit, over
     steps whose templates change; and against the reference model for the root rows."""
     import torch
     from doorman_amd.engine import Engine
-    from doorman_amd.hierarchy import HierarchicalTick, partition, root_snapshot
+    from doorman_amd.hierarchy import HierarchicalTick, partition, rccl_unique_id, root_snapshot
     torch.cuda.set_device(0)
     rng = np.random.default_rng(404 + G)
     sizes = rng.integers(5, 900, 40)
@@ -647,14 +649,17 @@ def test_native_step_matches_the_python_step(G):
         others[j * S + 1:j * S + 1 + n, 1] = np.asarray(sj["agg_count"], np.int64).view(np.float64)
     shard = W.subset(full, np.arange(lo[0], lo[1]))
     runs = []
-    for native in ("local", None):
+    for mode in (native, None):
         leaf, root = Engine(0), Engine(0)
         leaf.load(M.with_config(shard, M.default_config(int(lo[1] - lo[0]))))
         root.load(M.with_config(root_snapshot(R, 1, W.FAIR_SHARE, 1.0), rcfg))
 
         def gather(src, dst):
             dst[0:S].copy_(src)
-        ht = HierarchicalTick(torch, leaf, root, R, G, 0, gather, shard_lo=lo, pipelined=True, native=native)
+        # "rccl": the library's own communicator, here of one rank (server 0's block lands in
+        # slot 0 through ncclAllGather): the RCCL leg's plumbing on one GPU
+        kw = {"comm_id": rccl_unique_id(), "comm_ranks": 1} if mode == "rccl" else {}
+        ht = HierarchicalTick(torch, leaf, root, R, G, 0, gather, shard_lo=lo, pipelined=True, native=mode, **kw)
         if G > 1:
             ht.gathered[0].copy_(torch.from_numpy(others).to(ht.gathered[0].device))
         out = []
