@@ -54,7 +54,8 @@ struct Pack {  // a run of consecutive small resources covering <= 64 rows
 struct WorkItem {  // one resource of a size bin: no dependent load before its rows
   int32_t seg;
   int32_t n;   // rows (<= 4096) in bits 0-15; bits 16-23: the dense hint written by
-               // writeback ticks (s0 > 0 when expl[seg] == s0 + 1, below), else 0
+               // writeback ticks (s0 > 0 when expl[seg] == s0 + 1, below), else 0;
+               // bit 24: the resource also holds released rows (DevParams::rmask)
   int64_t lo;
 };
 
@@ -220,6 +221,10 @@ struct DevParams {
                       // read the subclients column (set by writeback ticks of the
                       // 128-thread group kernels, 257-1024 rows; upserts set 1, releases
                       // reset it to 0)
+  // Released-row masks of the dense resources of the workgroup bins (257-4096 rows):
+  // the resource starting at row lo owns the bytes from rel_mask_offset(lo), one
+  // RelMask<R> entry per lane (bit k: row k*G + lane is released).  N/2 + 64 bytes.
+  uint8_t* rmask;
   int64_t now;
   int32_t recompute;
   int32_t writeback;  // rows become followers / released in the store; out_expiry unused
@@ -233,6 +238,13 @@ struct DevParams {
 // dm_decide: one resource and its requests [qlo, qhi) in the caller's order; the
 // resource's rows are copied to scratch rows [scr, scr + n) that take each
 // decision's Assign before the next request is decided
+template <int R> struct RelMask { using T = uint8_t; };   // R <= 8 rows per lane
+template <> struct RelMask<16> { using T = uint16_t; };
+// 4-aligned, lo/2 - 4 < offset <= lo/2: a resource of n rows owns at least
+// 4 * floor(n / 8) bytes before the next one's, enough for G entries of R/8 bytes
+// in every workgroup bin (n > G * R / 2, R >= 4)
+constexpr int64_t rel_mask_offset(int64_t lo) { return (lo >> 3) << 2; }
+
 struct ReqItem {
   int32_t seg;
   int32_t fast;  // 1 + its slot of the fast path (FastItem), 0: decided by k_decide only

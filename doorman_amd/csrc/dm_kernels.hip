@@ -51,6 +51,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   int s[R];   // subclients in [0, kSubMax]
   int sr[R];  // the raw subclients words: where each row's expiry lives (dm_device.h)
   unsigned valid = 0, live = 0;
+  unsigned relm = 0;  // rows a dense resource's mask says are released (bit k: row k*G + t)
   // Every load is issued before any is consumed: lanes past the segment end
   // re-read row n-1 (same cache line, n >= 1 in every bin) instead of branching
   // around the load, which made the compiler wait on each row's expiry before
@@ -65,7 +66,14 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // rows) only track the state and write the hints (the extra branch costs
   // registers they do not have: spills at 5 waves per SIMD, C2 +3.5 %), and their
   // dense-only kernels skip the column.
-  const int hint = (kHintLoad) ? wi.n >> 16 : 0;
+  // A dense resource may also hold released rows (C2: loaded leases that had lapsed):
+  // its hint word carries "has released rows" (bit 8) and the tick that set it wrote
+  // which rows they are, one mask entry of R bits per lane (RelMask), read here in
+  // place of the column: 1-2 B per lane instead of 4 B per row.
+  const int hw = kDense ? wi.n >> 16 : 0;  // hint word: s0 in bits 0-7, released rows in bit 8
+  const int hint = (kHintLoad) ? hw & 0xFF : 0;
+  using MaskT = typename RelMask<R>::T;
+  MaskT* const mrow = reinterpret_cast<MaskT*>(p.rmask + rel_mask_offset(lo));
   if (MODE != kDenseOnly && !hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -77,13 +85,14 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       sr[k] = *col_at(sb, u);
     }
   } else {
+    if (hw >> 8 & 1) relm = mrow[t];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
       const unsigned u = (unsigned)(i < n ? i : n - 1);
       w[k] = *col_at(wb, u);
       h[k] = *col_at(hb, u);
-      sr[k] = hint;
+      sr[k] = hint;  // uniform: the mask's rows are taken out below (one register, not R)
     }
   }
   const Res rs = load_res(p, seg);
@@ -93,6 +102,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       return;
     }
   } else if (kHintLoad && hint && dense_subclients(rs) != hint) {
+    relm = 0;  // the column says which rows are released now
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -122,6 +132,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;  // store.go:174 when.After(expiry)
     s[k] = sub_value(sr[k]);
   }
+  live &= ~relm;
 
   // ---- pass A: Clean ----
   AggA a = zeroA();
@@ -129,13 +140,14 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   for (int k = 0; k < R; ++k) {
     if (!(valid >> k & 1)) continue;
     const bool lv = live >> k & 1;
+    const int sk = (relm >> k & 1) ? 0 : s[k];  // a released row counts nothing (its wants and has are 0)
     if (!lv) {
-      a.cnt += s[k];
+      a.cnt += sk;
       a.h += h[k];
       a.w += w[k];
     }
     if (p.recompute) {
-      a.all.cnt += s[k];
+      a.all.cnt += sk;
       a.all.h += h[k];
       a.all.w += w[k];
     }
@@ -218,7 +230,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      put_released(p, lo, u, sr[k]);
+      put_released(p, lo, u, (relm >> k & 1) ? (int)kSubReleased : sr[k]);
       continue;
     }
     double g;
@@ -240,15 +252,19 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     delta.v += g - h[k];
   }
 
-  const int nlive = a.nlive;  // live rows of the resource (the dense state needs all n)
+  // After a writeback tick every live row follows the resource and every other row
+  // is released: live rows with one subclient count s0 (1..254) make the resource
+  // dense.  Released rows among them go into its mask (written by the tick that sets
+  // the state; a dense tick leaves the state as it found it or, when the followers
+  // lapse together, ends it).
+  const int nlive = a.nlive;
+  const int dn = (kDense && p.writeback && nlive >= 1 && a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
+  const int hw_next = dn ? (dn | (nlive < n ? 1 << 8 : 0)) : 0;
   delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
+  if (MODE != kDenseOnly && (hw_next >> 8)) mrow[t] = (MaskT)(valid & ~live);
   if (t == 0) {
-    // after a writeback tick every live row follows the resource; all n rows live
-    // with one subclient count s0 (1..254) makes the resource dense
-    const int dn =
-        (kDense && p.writeback && nlive == n && a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
     write_resource(p, seg, rs, cl, delta.v, dn);
-    if (p.writeback && (wi.n >> 16) != dn) item->n = n | dn << 16;
+    if (p.writeback && hw != hw_next) item->n = n | hw_next << 16;
   }
 }
 

@@ -259,6 +259,7 @@ struct dm_ctx {
   // running sums + the followers' expiry, AoS (32 B)
   DBuf<ResAgg> agg;
   DBuf<uint8_t> expl;  // per resource: rows may carry explicit expiries (DevParams::expl)
+  DBuf<uint8_t> rmask;  // released-row masks of dense workgroup-bin resources (DevParams::rmask)
   // config, AoS: what every tick reads (32 B), and the rest (safe capacity, refresh)
   DBuf<ResCfg> cfg;
   DBuf<ResCold> cold;
@@ -996,6 +997,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_HIP(c, upload(c->agg, agg.data(), (size_t)R, st), "upload running sums");
   const std::vector<uint8_t> expl((size_t)std::max<int64_t>(R, 1), 1);  // loaded rows carry explicit expiries
   DM_HIP(c, upload(c->expl, expl.data(), expl.size(), st), "upload explicit flags");
+  DM_HIP(c, c->rmask.ensure((size_t)(N / 2 + 64)), "alloc released-row masks");  // written before read
   build_plan(c);
   int rc = upload_plan(c);
   if (rc) return rc;
@@ -1109,6 +1111,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   p.cfg = c->cfg.p;
   p.agg = c->agg.p;
   p.expl = c->expl.p;
+  p.rmask = c->rmask.p;
   // Every tick writes every row's lease (released rows included).  On a store
   // beyond the Infinity Cache a writeback tick writes its gets/expiry into the
   // alternate pair of columns and the pairs swap afterwards: separate output

@@ -795,25 +795,33 @@ def test_config_limits_and_cold_fields_round_trip(eng):
     assert e.value.code == DM_E_INVAL
 
 
+@pytest.mark.parametrize("expired", [0.0, 0.03])
 @pytest.mark.parametrize("split", ["1", "0", "3"])
 @pytest.mark.parametrize("cols", ["inplace", "alternate"])
-def test_dense_subclients_state(monkeypatch, cols, split):
-    """A writeback tick marks a group-kernel resource dense when every row is a live
-    follower with one subclient count; the next ticks skip its subclients column.
-    Releases, upserts (other subclient counts, explicit expiries) and lapsed
-    followers end the state, wants refreshes keep it; every tick matches the oracle
-    on a host copy, and dm_store_stats counts the dense resources.  split=1: after a
+def test_dense_subclients_state(monkeypatch, cols, split, expired):
+    """A writeback tick marks a group-kernel resource dense when every live row is a
+    follower with one subclient count (every other row is released then: its rows go
+    into the resource's released-row mask); the next ticks skip its subclients
+    column.  Releases and upserts (other subclient counts, explicit expiries, a
+    released slot taken again) end the state until the next writeback tick, lapsed
+    followers end it, wants refreshes keep it; every tick matches the oracle on a
+    host copy, and dm_store_stats counts the dense resources.  split=1: after a
     writeback tick the workgroup bins (128x4, 128x8, 256x8, 512x8) run as
     k_block_dense + k_block_rest (stale hints queued); split=0 (DM_DENSE_SPLIT=0):
-    the one-kernel form; split=3: only the 128-thread bins split."""
+    the one-kernel form; split=3: only the 128-thread bins split.  expired > 0:
+    loaded rows already past their expiry, released by the first tick (C2's shape),
+    so most resources carry a mask from the start."""
     from doorman_amd.engine import Engine
     monkeypatch.setenv("DM_DENSE_SPLIT", split)  # read when the context is created
     eng = Engine(0)
     rng = np.random.default_rng(5150)
     sizes = np.array([12, 30, 60, 100, 200, 400, 900, 1000, 1500, 3000, 5, 0, 9000, 20, 700])
-    snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=0.0, learning_frac=0.0,
+    snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=expired, learning_frac=0.0,
                                parent_expired_frac=0.0)
     snap["lease_length_s"] = np.full(len(sizes), 20, np.int64)
+    free = np.flatnonzero(rng.random(len(snap["wants"])) < expired)  # free slots too
+    snap["expiry_ns"][free], snap["subclients"][free], snap["has"][free], snap["wants"][free] = W.RELEASED, 0, 0.0, 0.0
+    W.add_store_sums(snap)
     group = (sizes >= 257) & (sizes <= 4096)  # the workgroup kernels keep the state
     eng.load(snap)
     assert eng.store_stats()["dense_resources"] == 0  # loaded rows carry explicit expiries
@@ -835,9 +843,9 @@ def test_dense_subclients_state(monkeypatch, cols, split):
             host["wants"][rows] = np.where(host["expiry_ns"][rows] == W.RELEASED, host["wants"][rows], nw)
             W.add_store_sums(host)
         if rnd == 4:  # upserts with another subclient count: explicit rows, non-uniform resources
-            rows = np.array([off[2] + 5, off[7] + 2, off[9] + 7, off[1] + 3])
+            rows = np.array([off[2] + 5, off[7] + 2, off[9] + 7, off[1] + 3, off[6] + 10])
             ne = now + 100 * W.NS
-            eng.upsert(rows, np.zeros(4), np.ones(4), np.full(4, 3, np.int64), np.full(4, ne))
+            eng.upsert(rows, np.zeros(5), np.ones(5), np.full(5, 3, np.int64), np.full(5, ne))
             host["wants"][rows], host["has"][rows], host["subclients"][rows], host["expiry_ns"][rows] = 1.0, 0.0, 3, ne
             W.add_store_sums(host)
         eng.apportion(now, writeback=True, wb_columns=cols)
@@ -853,12 +861,13 @@ def test_dense_subclients_state(monkeypatch, cols, split):
         st = eng.read_store()
         np.testing.assert_array_equal(st["subclients"], host["subclients"], err_msg=f"tick {rnd}")
         np.testing.assert_array_equal(st["expiry_ns"], host["expiry_ns"], err_msg=f"tick {rnd}")
-        # expected dense resources: 257-4096 rows, every row live with one subclient count >= 1
+        # expected dense resources: 257-4096 rows, every live row with one subclient
+        # count in 1..254 (released rows beside them), at least one live row
         want = 0
         for r in np.flatnonzero(group):
-            s = host["subclients"][off[r]:off[r + 1]]
             lv = host["expiry_ns"][off[r]:off[r + 1]] != W.RELEASED
-            want += int(lv.all() and s.min() == s.max() and 1 <= s[0] <= 254)
+            s = host["subclients"][off[r]:off[r + 1]][lv]
+            want += int(lv.any() and s.min() == s.max() and 1 <= s[0] <= 254)
         assert eng.store_stats()["dense_resources"] == want, f"tick {rnd}"
     assert eng.store_stats()["dense_resources"] == 0  # every follower lapsed at the last tick
     eng.close()
