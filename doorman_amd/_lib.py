@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdoorman_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "doorman_hip.h")
 
-DM_OK, DM_E_INVAL, DM_E_HIP, DM_E_STATE, DM_E_KIND, DM_E_RANGE, DM_E_ARGUMENT = 0, -1, -2, -3, -4, -5, -6
+DM_OK, DM_E_INVAL, DM_E_HIP, DM_E_STATE, DM_E_KIND, DM_E_RANGE, DM_E_ARGUMENT, DM_E_INTERNAL = 0, -1, -2, -3, -4, -5, -6, -7
 DM_HIER_INVALID, DM_HIER_COUNT_RANGE = 1, 2
 DM_RCCL_ID_BYTES = 128
 DM_WRITEBACK, DM_AGG_RECOMPUTE, DM_ASYNC, DM_WB_INPLACE, DM_WB_ALTERNATE, DM_DEFER_JOIN = 1, 2, 4, 8, 16, 32

@@ -33,7 +33,7 @@ template <int G, int R, int MODE = kMixed>
 __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, WorkItem* item, int t,
                                               Lds<G>& lds, int32_t* general_list, int32_t* general_count,
                                               int32_t* queue = nullptr, int32_t* qcount = nullptr,
-                                              int32_t qidx = 0) {
+                                              int32_t qidx = 0, int32_t* guard = nullptr, int qcap = 0) {
   // the dense state (below): every workgroup kernel tracks it and writes the hints;
   // only the 128-thread mixed kernel and the dense-only kernels load by the hint
   constexpr bool kDense = G >= 128;
@@ -98,7 +98,11 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   const Res rs = load_res(p, seg);
   if constexpr (MODE == kDenseOnly) {
     if (dense_subclients(rs) != hint) {  // stale hint: k_block_rest reads the column
-      if (t == 0) queue[atomicAdd(qcount, 1)] = qidx;
+      if (t == 0) {
+        const int q = atomicAdd(qcount, 1);
+        if (q < qcap) queue[q] = qidx;  // at most one entry per item and tick (a guarded tick's count may grow)
+        if (guard) __hip_atomic_store(guard, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       return;
     }
   } else if (kHintLoad && hint && dense_subclients(rs) != hint) {
@@ -257,11 +261,18 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // dense.  Released rows among them go into its mask (written by the tick that sets
   // the state; a dense tick leaves the state as it found it or, when the followers
   // lapse together, ends it).
+  // A resource with no live row left (its followers lapsed together) stays dense,
+  // every row in its mask, so that a dense tick always leaves a dense resource dense
+  // (the host's skip of the rest kernel rests on it: dm_runtime.cpp).
   const int nlive = a.nlive;
-  const int dn = (kDense && p.writeback && nlive >= 1 && a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
+  const int s_keep = (hw & 0xFF) ? (hw & 0xFF) : 1;
+  const int dn = !(kDense && p.writeback) ? 0
+                 : nlive == 0              ? s_keep
+                 : (a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
   const int hw_next = dn ? (dn | (nlive < n ? 1 << 8 : 0)) : 0;
   delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
-  if (MODE != kDenseOnly && (hw_next >> 8)) mrow[t] = (MaskT)(valid & ~live);
+  if (MODE == kDenseOnly ? nlive == 0 : (hw_next >> 8) != 0)  // a dense tick changes the mask only by a lapse
+    mrow[t] = (MaskT)(valid & ~live);
   if (t == 0) {
     write_resource(p, seg, rs, cl, delta.v, dn);
     if (p.writeback && hw != hw_next) item->n = n | hw_next << 16;
@@ -295,19 +306,49 @@ __global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevPa
 // split or mixed), written only when the count differs from the last one written
 // (qcnt[2]): a system-scope store to host memory keeps an otherwise empty launch
 // alive ~2 us longer, every tick of a dense store.
+// When the host skips k_block_rest (every item of the bin verified dense in this row
+// epoch, dm_runtime.cpp), `guard` (host-mapped) is set should the dense kernel queue
+// an item after all, which the host reports as DM_E_INTERNAL instead of leaving the
+// item undecided unnoticed; the tick-done word then comes from k_tick_done (one wave
+// after the dense kernel: 10^5 workgroups on one counter took 8 ms).
+__device__ __forceinline__ void tick_done_signal(const TickDone& td) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this workgroup's stores, seen from every XCD
+    const uint32_t old = __hip_atomic_fetch_add(td.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(td.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(td.word, td.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <int G, int R>
 __global__ __launch_bounds__(G) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
                                                    int32_t* queue, int32_t* qcnt, int par,
-                                                   int32_t* general_list, int32_t* general_count) {
+                                                   int32_t* general_list, int32_t* general_count,
+                                                   int32_t* guard) {
   __shared__ Lds<G> lds;
-  if ((int)blockIdx.x >= nitems) return;
-  const WorkItem wi = items[blockIdx.x];
-  if ((wi.n >> 16) == 0) {
-    if (threadIdx.x == 0) queue[atomicAdd(qcnt + par, 1)] = (int32_t)blockIdx.x;
-    return;
+  if ((int)blockIdx.x < nitems) {
+    const WorkItem wi = items[blockIdx.x];
+    if ((wi.n >> 16) == 0) {
+      if (threadIdx.x == 0) {
+        const int q = atomicAdd(qcnt + par, 1);
+        if (q < nitems) queue[q] = (int32_t)blockIdx.x;
+        if (guard) __hip_atomic_store(guard, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    } else {
+      group_segment<G, R, kDenseOnly>(p, wi, items + blockIdx.x, threadIdx.x, lds, general_list, general_count,
+                                      queue, qcnt + par, (int32_t)blockIdx.x, guard, nitems);
+    }
   }
-  group_segment<G, R, kDenseOnly>(p, wi, items + blockIdx.x, threadIdx.x, lds, general_list, general_count, queue,
-                                  qcnt + par, (int32_t)blockIdx.x);
+}
+
+__global__ __launch_bounds__(64) void k_tick_done(TickDone td) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(td.word, td.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 template <int G, int R>
@@ -329,16 +370,26 @@ __global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restr
     group_segment<G, R, kRest>(p, items[idx], items + idx, threadIdx.x, lds, general_list, general_count);
     __syncthreads();  // the next item reuses the single-use LDS slots
   }
-  if (td.word) {  // the tick is done once every workgroup of this, its last kernel, is
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this workgroup's stores, seen from every XCD
-      const uint32_t old = __hip_atomic_fetch_add(td.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == gridDim.x - 1) {
-        __hip_atomic_store(td.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(td.word, td.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
+  if (td.word) tick_done_signal(td);  // the tick is done once every workgroup of this, its last kernel, is
+}
+
+// One workgroup: how many items of a workgroup bin are not dense after a writeback
+// tick, published to host-mapped memory as {count, epoch} (count first, the epoch
+// with release order) -- the host's once-per-epoch check before it skips the bin's
+// k_block_rest (dm_runtime.cpp).
+__global__ __launch_bounds__(1024) void k_count_undense(const WorkItem* __restrict__ items, int n,
+                                                        unsigned long long* rec, unsigned long long epoch) {
+  __shared__ int part[16];
+  int c = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) c += (items[i].n >> 16) == 0 ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += part[w];
+    __hip_atomic_store(rec, (unsigned long long)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(rec + 1, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -2478,16 +2529,29 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
 // kernel over every item, then the rest kernel over what it queued (two launches,
 // timed separately).
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                            int32_t* glist, int32_t* gcount, hipStream_t st) {
+                            int32_t* glist, int32_t* gcount, int32_t* guard, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   switch (bin) {
-    case 3: k_block_dense<128, 4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
-    case 4: k_block_dense<128, 8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
-    case 5: k_block_dense<256, 8><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
-    case 6: k_block_dense<256, 16><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
-    case kBin6Wide: k_block_dense<512, 8><<<n, 512, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount); break;
+    case 3: k_block_dense<128, 4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
+    case 4: k_block_dense<128, 8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
+    case 5: k_block_dense<256, 8><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
+    case 6: k_block_dense<256, 16><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
+    case kBin6Wide:
+      k_block_dense<512, 8><<<n, 512, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard);
+      break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_tick_done(const TickDone& td, hipStream_t st) {
+  k_tick_done<<<1, 64, 0, st>>>(td);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_undense(const WorkItem* items, int n, unsigned long long* rec, unsigned long long epoch,
+                                hipStream_t st) {
+  k_count_undense<<<1, 1024, 0, st>>>(items, n, rec, epoch);
   return hipGetLastError();
 }
 

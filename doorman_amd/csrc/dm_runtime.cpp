@@ -25,7 +25,10 @@ hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_
                       hipStream_t st);
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                            int32_t* glist, int32_t* gcount, hipStream_t st);
+                            int32_t* glist, int32_t* gcount, int32_t* guard, hipStream_t st);
+hipError_t launch_tick_done(const TickDone& td, hipStream_t st);
+hipError_t launch_count_undense(const WorkItem* items, int n, unsigned long long* rec, unsigned long long epoch,
+                                hipStream_t st);
 hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
                            int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, const TickDone& td,
                            hipStream_t st);
@@ -246,6 +249,16 @@ struct dm_ctx {
   // (Partials::s_live): cleared at the start of every tick and by every call that
   // writes a subclients word or releases a row
   bool chain_live_ok = false;
+  // Row epoch: bumped by every call that writes rows (loads, plans, upserts, releases,
+  // wants refreshes, decide, the root's tick) -- never by a tick.  Within one epoch a
+  // writeback tick leaves every dense workgroup-bin resource dense (dm_kernels.hip),
+  // so a bin verified all-dense once in the epoch (k_count_undense) can skip its
+  // k_block_rest: nothing can be queued.
+  uint64_t row_epoch = 1;
+  void rows_changed() {
+    chain_live_ok = false;
+    row_epoch += 1;
+  }
   std::vector<int64_t> h_seg_off;
   std::vector<int64_t> h_refresh_s;
 
@@ -314,6 +327,15 @@ struct dm_ctx {
   bool bin6_wide = false;  // bin 6 on 512 x 8 workgroups (kBin6Wide): it holds most of the rows
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
+  // host-mapped, per split bin: {undense count, epoch} of the epoch's check
+  // (k_count_undense), and the guard a dense kernel sets should it queue an item on a
+  // tick whose rest kernel was skipped
+  uint64_t* h_rec = nullptr;
+  uint64_t* d_rec = nullptr;
+  int32_t* h_guard = nullptr;
+  int32_t* d_guard = nullptr;
+  uint64_t dq_ver_epoch[kSplitBins] = {};  // the epoch each bin's check was enqueued in
+  bool skip_rest = true;  // DM_SKIP_REST=0: always launch k_block_rest
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
@@ -476,6 +498,10 @@ struct dm_ctx {
     if (h_dq) (void)hipHostFree(h_dq);
     h_dq = nullptr;
     d_dq = nullptr;
+    if (h_rec) (void)hipHostFree(h_rec);
+    h_rec = d_rec = nullptr;
+    if (h_guard) (void)hipHostFree(h_guard);
+    h_guard = d_guard = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
     pa_nan.release(); pa_live.release(); p_tot.release(); p_uni.release();
@@ -595,6 +621,16 @@ static void build_plan(dm_ctx* c) {
   close();
 }
 
+// Once per row epoch, after a writeback tick of workgroup bin b (split bin i): count
+// its items left without a dense hint (k_count_undense -> h_rec).  A count of 0 lets
+// the following ticks of the epoch skip the bin's k_block_rest.
+static hipError_t check_dense(dm_ctx* c, int i, int b, hipStream_t s) {
+  if (!c->skip_rest || c->dq_ver_epoch[i] == c->row_epoch || c->h_bins[b].empty()) return hipSuccess;
+  c->dq_ver_epoch[i] = c->row_epoch;
+  return launch_count_undense(c->bins[b].p, (int)c->h_bins[b].size(), (unsigned long long*)(c->d_rec + 2 * i),
+                              (unsigned long long)c->row_epoch, s);
+}
+
 static int upload_plan(dm_ctx* c) {
   hipStream_t st = c->stream;
   DM_HIP(c, upload(c->packs, c->h_packs.data(), c->h_packs.size(), st), "plan packs");
@@ -604,6 +640,18 @@ static int upload_plan(dm_ctx* c) {
   if (!c->h_dq) {
     DM_HIP(c, hipHostMalloc((void**)&c->h_dq, dm_ctx::kSplitBins * sizeof(int32_t), hipHostMallocMapped), "dense split word");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_dq, c->h_dq, 0), "dense split word");
+    DM_HIP(c, hipHostMalloc((void**)&c->h_rec, dm_ctx::kSplitBins * 2 * sizeof(uint64_t), hipHostMallocMapped),
+           "dense split check");
+    DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0), "dense split check");
+    DM_HIP(c, hipHostMalloc((void**)&c->h_guard, dm_ctx::kSplitBins * sizeof(int32_t), hipHostMallocMapped),
+           "dense split guard");
+    DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_guard, c->h_guard, 0), "dense split guard");
+  }
+  c->rows_changed();  // new work items: no hints
+  for (int i = 0; i < dm_ctx::kSplitBins; ++i) {
+    __atomic_store_n(c->h_rec + 2 * i + 1, (uint64_t)0, __ATOMIC_RELAXED);
+    __atomic_store_n(c->h_guard + i, 0, __ATOMIC_RELAXED);
+    c->dq_ver_epoch[i] = 0;
   }
   {
     int64_t rows6 = 0;
@@ -751,6 +799,7 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
   if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
   if (const char* hw = getenv("DM_TPL_HOSTWAIT")) c->tpl_hostwait = atoi(hw) != 0;
+  if (const char* sr = getenv("DM_SKIP_REST")) c->skip_rest = atoi(sr) != 0;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1009,7 +1058,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
   c->expl_rows = true;
-  c->chain_live_ok = false;
+  c->rows_changed();
   c->have_result = false;
   if (c->cfg_loaded && (int64_t)c->h_refresh_s.size() != R) c->cfg_loaded = false;
   return DM_OK;
@@ -1017,7 +1066,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
 
 int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   DM_ENTER(c);
-  c->chain_live_ok = false;
+  c->rows_changed();
   if (!cfg || R < 0 || !cfg->kind || !cfg->capacity || !cfg->lease_length_s || !cfg->refresh_interval_s ||
       !cfg->learning_end_ns || !cfg->parent_expiry_ns || !cfg->safe_capacity)
     return c->fail(DM_E_INVAL, "bad config");
@@ -1098,6 +1147,9 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   int rc = ready(c);
   if (rc) return rc;
   if (c->tpl_pipe && (rc = commit_templates(c))) return rc;
+  for (int i = 0; c->h_guard && i < dm_ctx::kSplitBins; ++i)
+    if (__atomic_load_n(c->h_guard + i, __ATOMIC_RELAXED))
+      return c->fail(DM_E_INTERNAL, "a dense kernel queued an item on a tick that skipped its rest kernel");
   c->ticks_issued += 1;
   c->tick_seq += 1;
   c->tick_flagged = false;
@@ -1278,30 +1330,41 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
       if (good || ++c->dq_skip[i] >= c->dq_wait[i]) {
         if (!good) c->dq_wait[i] = std::min(2 * c->dq_wait[i], 4096);
         c->dq_skip[i] = 0;
-        // the rest kernel strides over whatever the dense kernel queues; its grid is
-        // only sized from the last split tick's queue (a hint: correctness never
-        // depends on it): an empty queue costs 16 workgroups that read one count
-        const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
-        DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
-                 return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc, s);
-               }),
-               "group kernel (dense split)");
+        // Every item verified dense in this row epoch: nothing can be queued, so the
+        // dense kernel is the bin's only launch (the guard catches the impossible).
+        const uint64_t* rec = c->h_rec + 2 * i;
+        const bool skip = c->skip_rest && __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
+                          __atomic_load_n(rec, __ATOMIC_RELAXED) == 0;
         TickDone td{nullptr, nullptr, 0};
         if (one_class && c->tick_word) {
           td = TickDone{c->tick_word, c->tick_ctr, c->tick_seq};
           c->tick_flagged = true;
         }
-        DM_HIP(c, timed(KC_REST3 + i, s, [&] {
-                 return launch_bin_rest(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
-                                        rest_grid, gl, gc, td, s);
+        DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
+                 return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc,
+                                         skip ? c->d_guard + i : nullptr, s);
                }),
                "group kernel (dense split)");
-        c->dq_par[i] ^= 1;
+        if (skip && td.word) DM_HIP(c, launch_tick_done(td, s), "tick-done word");
+        if (!skip) {
+          // the rest kernel strides over whatever the dense kernel queues; its grid is
+          // only sized from the last split tick's queue (a hint: correctness never
+          // depends on it): an empty queue costs 16 workgroups that read one count
+          const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
+          DM_HIP(c, timed(KC_REST3 + i, s, [&] {
+                   return launch_bin_rest(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
+                                          rest_grid, gl, gc, td, s);
+                 }),
+                 "group kernel (dense split)");
+          c->dq_par[i] ^= 1;
+        }
+        if (wb) DM_HIP(c, check_dense(c, i, b, s), "dense split check");
         continue;
       }
     }
     DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(lb, p, c->bins[b].p, n, gl, gc, s); }),
            "group kernel");
+    if (b >= 3 && b < 3 + dm_ctx::kSplitBins && wb) DM_HIP(c, check_dense(c, b - 3, b, s), "dense split check");
   }
   if (!c->h_packs.empty())
     DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), s_small); }),
@@ -1343,7 +1406,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
     return c->fail(DM_E_INVAL, "bad requests");
   if (n == 0) return DM_OK;
   c->expl_rows = true;  // decided rows take explicit expiries
-  c->chain_live_ok = false;
+  c->rows_changed();
   std::vector<int64_t> seg_of((size_t)n);
   for (int64_t k = 0; k < n; ++k) {
     const int64_t r = rows[k];
@@ -1744,7 +1807,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
   c->expl_rows = true;
-  c->chain_live_ok = false;
+  c->rows_changed();
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   DM_HIP(c, c->st_has.ensure((size_t)n), "stage has");
   DM_HIP(c, c->st_wants.ensure((size_t)n), "stage wants");
@@ -1773,6 +1836,7 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
+  c->rows_changed();  // a NaN wants ends a resource's dense state
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   DM_HIP(c, c->st_wants.ensure((size_t)n), "stage wants");
   const StageCol cols[] = {{c->st_rows.p, rows, 8}, {c->st_wants.p, wants, 8}};
@@ -1800,6 +1864,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
     return c->fail(DM_E_INVAL, "bad masked update (first_row must be a multiple of 64)");
   if (nwords == 0) return n == 0 ? DM_OK : c->fail(DM_E_INVAL, "packed values without a mask");
   if (first_row + 64 * (nwords - 1) >= c->N) return c->fail(DM_E_RANGE, "mask words past the store's end");
+  c->rows_changed();  // a NaN wants ends a resource's dense state
   const int64_t nb = (nwords + 255) / 256;
   DM_HIP(c, c->st_mask.ensure((size_t)nwords), "stage mask");
   DM_HIP(c, c->st_wants.ensure((size_t)std::max<int64_t>(n, 1)), "stage wants");
@@ -1835,7 +1900,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
-  c->chain_live_ok = false;
+  c->rows_changed();
   DM_HIP(c, c->st_rows.ensure((size_t)n), "stage rows");
   const StageCol cols[] = {{c->st_rows.p, rows, 8}};
   int rc = staged_check(c, n, cols, 1, false, false);
@@ -1880,6 +1945,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
   if (nu > 0) c->expl_rows = true;  // arrivals take explicit expiries
   if (nu > 0 || nr > 0) c->chain_live_ok = false;  // subclients words written, rows released
+  c->rows_changed();  // (wants refreshes too: a NaN wants ends a resource's dense state)
   hipStream_t st = c->stream, cp = c->cpy;
   if (!c->bat_flags.p) {
     DM_HIP(c, c->bat_flags.ensure(3), "batch flags");
@@ -2105,7 +2171,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   const bool sharded = root->hier_G != 0 && root->hier_sharded;
   const int K = sharded ? 1 : n_servers;
   root->expl_rows = true;  // the root's rows take the exchange's explicit expiries
-  root->chain_live_ok = false;
+  root->rows_changed();
   // checked at load (seg_uniform), not per round
   if (root->R <= 0 || root->N != root->R * (int64_t)K || root->seg_uniform != K)
     return root->fail(DM_E_STATE, sharded ? "sharded root store must hold one row per resource"

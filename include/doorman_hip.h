@@ -48,6 +48,7 @@ extern "C" {
 #define DM_E_KIND (-4)    /* unknown algorithm kind (the reference panics: algorithm.go:312) */
 #define DM_E_RANGE (-5)   /* row / resource index out of range */
 #define DM_E_ARGUMENT (-6) /* codes.InvalidArgument, e.g. num_clients < 1 (server.go:863-866) */
+#define DM_E_INTERNAL (-7) /* an internal invariant failed (a bug in this library) */
 
 /* pb.Algorithm_Kind (proto/doorman/doorman.proto:139-144) */
 #define DM_NO_ALGORITHM 0

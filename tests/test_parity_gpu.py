@@ -862,14 +862,77 @@ def test_dense_subclients_state(monkeypatch, cols, split, expired):
         np.testing.assert_array_equal(st["subclients"], host["subclients"], err_msg=f"tick {rnd}")
         np.testing.assert_array_equal(st["expiry_ns"], host["expiry_ns"], err_msg=f"tick {rnd}")
         # expected dense resources: 257-4096 rows, every live row with one subclient
-        # count in 1..254 (released rows beside them), at least one live row
+        # count in 1..254 (released rows beside them), or no live row at all
         want = 0
         for r in np.flatnonzero(group):
             lv = host["expiry_ns"][off[r]:off[r + 1]] != W.RELEASED
             s = host["subclients"][off[r]:off[r + 1]][lv]
-            want += int(lv.any() and s.min() == s.max() and 1 <= s[0] <= 254)
+            want += int(not lv.any() or (s.min() == s.max() and 1 <= s[0] <= 254))
         assert eng.store_stats()["dense_resources"] == want, f"tick {rnd}"
-    assert eng.store_stats()["dense_resources"] == 0  # every follower lapsed at the last tick
+    # every follower lapsed at the last tick: all released, the workgroup-bin resources stay dense
+    assert eng.store_stats()["dense_resources"] == int(group.sum())
+    eng.close()
+
+
+def _writeback_and_check(eng, host, now, label):
+    """One writeback tick against the oracle on the host copy, which then takes the tick's state."""
+    eng.apportion(now, writeback=True)
+    gets, exp = eng.leases()
+    ref = O.apportion(host, now)
+    assert_leases_match(host, gets, exp, ref, label)
+    live = ref["expiry_ns"] != W.RELEASED
+    host["has"] = np.where(live, ref["gets"], 0.0)
+    host["wants"] = np.where(live, host["wants"], 0.0)
+    host["subclients"] = np.where(live, host["subclients"], 0)
+    host["expiry_ns"] = ref["expiry_ns"].copy()
+    W.add_store_sums(host)
+
+
+def test_dense_split_skips_the_rest_kernel_once_verified():
+    """Within one row epoch (no call that writes rows since), a workgroup bin whose
+    items were all counted dense after a writeback tick (k_count_undense) runs the
+    dense kernel alone; a wants refresh (here a NaN wants, which ends a resource's
+    dense state) starts a new epoch and the rest kernel runs again until the next
+    check; followers that lapse together keep their resource dense (every row in its
+    mask).  Every tick matches the oracle on a host copy."""
+    from doorman_amd.engine import Engine
+    eng = Engine(0)
+    rng = np.random.default_rng(77)
+    sizes = np.concatenate([rng.integers(257, 4097, 24), [5, 0, 40]])
+    snap = snapshot_with_sizes(rng, sizes, kinds=(1, 2, 3), expired_frac=0.02, learning_frac=0.0,
+                               parent_expired_frac=0.0)
+    snap["lease_length_s"] = np.full(len(sizes), 20, np.int64)
+    eng.load(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    off = np.asarray(snap["seg_off"])
+    eng.set_profiling(True)
+
+    def rest_launches():
+        return sum(v[0] for k, v in eng.kernel_times().items() if k.endswith("_rest"))
+
+    for t in range(4):
+        eng.reset_kernel_times()
+        _writeback_and_check(eng, host, NOW, f"tick {t}")
+        if t == 3:  # tick 0 mixed + the check, tick 1 split with rest (record not read yet or read), then skipped
+            assert rest_launches() == 0, eng.kernel_times()
+            assert any(k.endswith("_dense") for k in eng.kernel_times())
+    fs = [r for r in range(24) if host["kind"][r] == 3]
+    assert fs, "no FairShare resource among the sampled kinds"
+    row = int(off[fs[0]] + np.flatnonzero(host["expiry_ns"][off[fs[0]]:off[fs[0] + 1]] != W.RELEASED)[0])
+    eng.update_wants(np.array([row]), np.array([np.nan]))
+    host["wants"][row] = np.nan
+    W.add_store_sums(host)
+    eng.reset_kernel_times()
+    _writeback_and_check(eng, host, NOW, "after the NaN refresh")
+    kt = eng.kernel_times()  # a new epoch: every item decided by a kernel that reads the column
+    assert rest_launches() >= 1 or any(k.startswith("block") and not k.endswith("_dense") for k in kt), kt
+    for t in range(3):  # checked again in the new epoch (the NaN resource is not dense: the rest kernel stays)
+        eng.reset_kernel_times()
+        _writeback_and_check(eng, host, NOW, f"new epoch tick {t}")
+    assert rest_launches() >= 1, eng.kernel_times()
+    for t, dt in enumerate([5, 30, 31, 32]):  # the followers lapse at +20 s: all rows released, still dense
+        _writeback_and_check(eng, host, NOW + dt * W.NS, f"lapse tick {t}")
+    assert eng.store_stats()["dense_resources"] == 24
     eng.close()
 
 
