@@ -1,6 +1,6 @@
 """Interleaved A/B timing of library builds in ONE process (cdna guide §5.4 rule 24).
 
-  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:inplace|:alternate][@VAR=value,...] ...
+  python tools/ab.py --workload c1 --rounds 8 --steps 20 LIB_A.so LIB_B.so[:inplace|:alternate][@VAR=value+...] ...
 
 Every build gets its own context with the same snapshot; rounds alternate between
 builds; per build the per-launch kernel time (HIP events) and the tick wall time
@@ -54,9 +54,10 @@ def main():
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
     engines = []
     for p in args.libs:
-        spec, _, envs = p.partition("@")  # LIB[:mode][@VAR=value,...]: environment at the engine's creation
+        spec, _, envs = p.partition("@")  # LIB[:mode][@VAR=value+...]: environment at the engine's creation
         path, _, mode = spec.partition(":")
-        e_env = dict(kv.partition("=")[::2] for kv in filter(None, envs.split(",")))
+        # VAR=value pairs split on "+" (a value may hold commas, e.g. DM_CU_PART=96,64,64,32)
+        e_env = dict(kv.partition("=")[::2] for kv in filter(None, envs.split("+")))
         with env(e_env):
             e = Engine(0, os.path.abspath(path))
         e.env = e_env  # also in force around its ticks (knobs read per launch)
