@@ -52,6 +52,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   int sr[R];  // the raw subclients words: where each row's expiry lives (dm_device.h)
   unsigned valid = 0, live = 0;
   unsigned relm = 0;  // rows a dense resource's mask says are released (bit k: row k*G + t)
+  unsigned relb = 0;  // rows whose subclients word marks them released
   // Every load is issued before any is consumed: lanes past the segment end
   // re-read row n-1 (same cache line, n >= 1 in every bin) instead of branching
   // around the load, which made the compiler wait on each row's expiry before
@@ -134,6 +135,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     valid |= vk << k;
     if (sub_released(sr[k])) e[k] = kReleased;
     live |= (vk & (p.now > e[k] ? 0u : 1u)) << k;  // store.go:174 when.After(expiry)
+    relb |= (sub_released(sr[k]) ? 1u : 0u) << k;
     s[k] = sub_value(sr[k]);
   }
   live &= ~relm;
@@ -164,7 +166,29 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   }
   {
     const AggR all_part = a.all;
-    a = group_reduce<G, AggA, OpA, false>(a, OpA(), lds.a);
+    bool fast_a = false;
+    if constexpr (G <= 64) {
+      // Sub-wave and wave groups are VALU-bound on their reductions.  In the steady
+      // state pass A's totals are known wave-wide without one: no row of the wave is
+      // released by this Clean (rows already marked released hold zeros), its live
+      // rows share one subclient count u, no wants is NaN.  Then every group's Clean
+      // sums are exact zeros and its live range is [u, u] (empty: no live row).
+      if (!p.recompute) {
+        const uint64_t lv = __ballot(live != 0);
+        const int u = __builtin_amdgcn_readlane(a.smin, lv ? (int)__builtin_ctzll(lv) : 0);
+        const bool ok = (valid & ~live & ~relb) == 0 && a.cnt == 0 && __double_as_longlong(a.h) == 0 &&
+                        __double_as_longlong(a.w) == 0 && !a.nan && (live == 0 || (a.smin == u && a.smax == u));
+        if (__all(ok)) {
+          fast_a = true;
+          const int base = (int)(threadIdx.x & 63) & ~(G - 1);
+          const uint64_t gmask = G == 64 ? ~0ull : (((1ull << G) - 1) << base);
+          const bool any_live = (lv & gmask) != 0;
+          a.smin = any_live ? u : INT32_MAX;
+          a.smax = any_live ? u : INT32_MIN;
+        }
+      }
+    }
+    if (!fast_a) a = group_reduce<G, AggA, OpA, false>(a, OpA(), lds.a);
     if (p.recompute) a.all = group_reduce<G, AggR, OpR, false>(all_part, OpR(), lds.r);
   }
   const Clean cl = clean_from(p, rs, a);

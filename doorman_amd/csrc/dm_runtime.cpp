@@ -436,6 +436,10 @@ struct dm_ctx {
   uint32_t* tick_ctr = nullptr;
   uint64_t tick_seq = 0;          // the last tick's number
   bool tick_flagged = false;      // ... and whether it stores it
+  // set by the first consumer on another stream (the exchange's order, a template
+  // slot's reuse): before it, no tick stores the word (k_tick_done costs ~5 us of the
+  // leaf's queue when nothing waits on it, e.g. the exchange on the leaf's own stream)
+  bool tick_word_wanted = false;
   uint64_t tpl_free_seq[kTplSlots] = {};  // a slot is free once the word reaches this (0: use tpl_free)
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
@@ -1336,7 +1340,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
         const bool skip = c->skip_rest && __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
                           __atomic_load_n(rec, __ATOMIC_RELAXED) == 0;
         TickDone td{nullptr, nullptr, 0};
-        if (one_class && c->tick_word) {
+        if (one_class && c->tick_word && c->tick_word_wanted) {
           td = TickDone{c->tick_word, c->tick_ctr, c->tick_seq};
           c->tick_flagged = true;
         }
@@ -2203,7 +2207,10 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     slot = leaf->tpl_free_slots.front();
     DM_HIP(root, leaf->tpl_cfg[slot].ensure((size_t)leaf->R), "template slot");
     DM_HIP(root, leaf->tpl_cold[slot].ensure((size_t)leaf->R), "template slot");
-    if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0)  // the ticks that read the slot's old
+    if (leaf->stream != root->stream) leaf->tick_word_wanted = true;
+    if (leaf->stream == root->stream) {
+      // stream order: the ticks that read the slot's old templates precede this round
+    } else if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0)  // the ticks that read the slot's old
       DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tpl_free_seq[slot],  // templates
                                         hipStreamWaitValueGte, ~0ull),                           // are done
              "template slot");
@@ -2373,7 +2380,10 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
     DM_HIP(root, leaf->join_aux(), "join leaf streams");
     // the exchange stream after the tick that wrote the block: on the tick-done word when
     // the tick stores it (no marker on the leaf's queue), else an event
-    if (leaf->tick_flagged)
+    if (leaf->stream != root->stream) leaf->tick_word_wanted = true;
+    if (leaf->stream == root->stream) {
+      // stream order
+    } else if (leaf->tick_flagged)
       DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tick_seq, hipStreamWaitValueGte, ~0ull),
              "leaf->exchange order");
     else
