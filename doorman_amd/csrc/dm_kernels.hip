@@ -543,7 +543,10 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
     sh = rs.agg_has;
     sw = rs.agg_wants;
   }
-  if (__any(valid && !lv)) {  // some row of the pack expired
+  // some row of the pack expired since its last writeback tick (a row already marked
+  // released holds zeros: subtracting it changes nothing -- C2's 1 % of released rows
+  // sent about half of the packs through this loop every tick)
+  if (__any(valid && !lv && !sub_released(sr))) {
     for (int q = 0; q < maxlen; ++q) {
       const int j = lo + q;
       const double hj = shfl_d(h, j & 63), wj = shfl_d(w, j & 63);
@@ -1963,8 +1966,12 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex 
 
 // Narrow Assign for a refresh that only changes wants (store.go:157):
 // sumWants += new - old.  Rows are unique within one call.
+// A released row is a free slot, not a client: a refresh of it changes nothing (a
+// returning client is an arrival, dm_store_upsert).  Written into it, the wants would
+// be subtracted from the resource's running sum by every later tick's Clean.
 __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ wants,
-                               RowIndex ix, double* s_wants, ResAgg* agg, const uint32_t* flags) {
+                               RowIndex ix, const int32_t* __restrict__ s_sub, double* s_wants, ResAgg* agg,
+                               const uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (*flags & kUpdReject) return;  // uniform over the grid
   const bool active = i < n;
@@ -1973,8 +1980,10 @@ __global__ void k_update_wants(int64_t n, const int64_t* __restrict__ rows, cons
   if (active) {
     const int64_t r = rows[i];
     seg = seg_of_row(ix, r);
-    d = wants[i] - s_wants[r];
-    s_wants[r] = wants[i];
+    if (!sub_released(s_sub[r])) {
+      d = wants[i] - s_wants[r];
+      s_wants[r] = wants[i];
+    }
   }
   wave_seg_add(agg, active, seg, 0.0, d, 0, false, false);
 }
@@ -2055,8 +2064,9 @@ constexpr int kMaskWords = 16;
 __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64_t* __restrict__ mask,
                                                     int64_t first_row, const int64_t* __restrict__ block_offs,
                                                     const int32_t* __restrict__ word_pre,
-                                                    const double* __restrict__ wants, RowIndex ix, double* s_wants,
-                                                    ResAgg* agg, uint32_t* flags) {
+                                                    const double* __restrict__ wants, RowIndex ix,
+                                                    const int32_t* __restrict__ s_sub, double* s_wants, ResAgg* agg,
+                                                    uint32_t* flags) {
   if (*flags & kUpdReject) return;  // uniform over the grid
   const int lane = threadIdx.x & 63;
   const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kMaskWords;
@@ -2074,6 +2084,7 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
   }
   const uint64_t below = (1ull << lane) - 1ull;
   double v[kMaskWords], old[kMaskWords];
+  uint32_t freed = 0;  // bit q: this lane's row of word q is released (k_update_wants: left alone)
 #pragma unroll
   for (int q = 0; q < kMaskWords; ++q) {  // every load in flight before the first use
     v[q] = 0.0;
@@ -2083,6 +2094,7 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
       if ((m >> lane) & 1ull) {
         v[q] = wants[readlane_any(my_off, q) + __popcll(m & below)];
         old[q] = s_wants[first_row + 64 * (w0 + q) + lane];
+        freed |= (sub_released(s_sub[first_row + 64 * (w0 + q) + lane]) ? 1u : 0u) << q;
       }
     }
   }
@@ -2094,7 +2106,7 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
     const uint64_t m = q < nw ? readlane_any(my_m, q) : 0ull;
     if (m != 0ull) {  // uniform
       const int64_t row0 = first_row + 64 * (w0 + q);
-      const bool act = (m >> lane) & 1ull;
+      const bool act = ((m >> lane) & 1ull) && !(freed >> q & 1u);
       const int s0 = __builtin_amdgcn_readlane(my_seg, q);
       const bool single = readlane_any(my_end, q) > row0 + 63 - __builtin_clzll(m);
       double d = 0.0;
@@ -2641,9 +2653,10 @@ hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, do
 }
 
 hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wants, const RowIndex& ix,
-                               double* s_wants, ResAgg* agg, const uint32_t* flags, hipStream_t st) {
+                               const int32_t* s_sub, double* s_wants, ResAgg* agg, const uint32_t* flags,
+                               hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, ix, s_wants, agg, flags);
+  k_update_wants<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, wants, ix, s_sub, s_wants, agg, flags);
   return hipGetLastError();
 }
 
@@ -2683,15 +2696,15 @@ hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, uint32_t* syn
 
 hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
                                     int64_t n_values, const double* wants, int64_t* block_sums, int32_t* word_pre,
-                                    const RowIndex& ix, double* s_wants, ResAgg* agg, uint32_t* flags,
-                                    hipStream_t st) {
+                                    const RowIndex& ix, const int32_t* s_sub, double* s_wants, ResAgg* agg,
+                                    uint32_t* flags, hipStream_t st) {
   if (nwords <= 0) return hipSuccess;
   const int64_t nb = (nwords + 255) / 256;
   k_mask_count<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, N, block_sums, word_pre, flags);
   k_mask_scan<<<1, 1024, 0, st>>>(nb, block_sums, n_values, flags);
   const int64_t waves = (nwords + kMaskWords - 1) / kMaskWords;
   k_mask_apply<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(nwords, mask, first_row, block_sums, word_pre, wants, ix,
-                                                            s_wants, agg, flags);
+                                                            s_sub, s_wants, agg, flags);
   return hipGetLastError();
 }
 

@@ -168,7 +168,9 @@ int dm_config_load(dm_ctx* ctx, int64_t n_resources, const dm_resource_cfg* cfg)
 int dm_store_upsert(dm_ctx* ctx, int64_t n, const int64_t* rows, const double* has, const double* wants,
                     const int64_t* subclients, const int64_t* expiry_ns);
 /* Assign of a refresh that only changes wants (store.go:153-167 with has, subclients and
- * expiry unchanged): sumWants += new - old.  12 bytes per update over PCIe. */
+ * expiry unchanged): sumWants += new - old.  12 bytes per update over PCIe.  A released
+ * row is a free slot, not a client: a refresh naming it changes nothing (a returning
+ * client is an arrival: dm_store_upsert).  The same holds for the mask form below. */
 int dm_store_update_wants(dm_ctx* ctx, int64_t n, const int64_t* rows, const double* wants);
 /* The same narrow Assign with the rows given as a bit mask: bit j of mask[w] is row
    first_row + 64*w + j (first_row a multiple of 64); the n set rows take wants[0..n)

@@ -625,6 +625,59 @@ def test_update_wants_mask_matches_row_form(eng):
         other.close()
 
 
+@pytest.mark.parametrize("form", ["rows", "mask"])
+def test_wants_refresh_leaves_released_rows_alone(eng, form):
+    """A released row is a free slot, not a client: a wants refresh naming it changes
+    neither the row nor its resource's running sums (a returning client is an arrival,
+    dm_store_upsert).  Written into the row, the wants would be subtracted from the
+    running sum again by every later tick's Clean.  After refreshes that mix live and
+    released rows, over several writeback ticks, every resource's sumWants equals the
+    sum of its live rows' wants and its Count their subclients; each tick matches the
+    oracle on the store as it stood."""
+    rng = np.random.default_rng(4711)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=True), expired_frac=0.1, kinds=(2, 3),
+                               learning_frac=0.0, parent_expired_frac=0.0)
+    so = np.asarray(snap["seg_off"])
+    N, R = len(snap["wants"]), len(so) - 1
+    seg_of = np.repeat(np.arange(R), np.diff(so))
+    cap = np.maximum(snap["capacity"], 1.0)
+    eng.load(snap)
+    now = NOW
+    eng.apportion(now, writeback=True)  # the expired rows are released
+    for t in range(4):
+        st = eng.read_store()
+        released = st["expiry_ns"] == W.RELEASED
+        assert released.any()
+        rows = np.sort(rng.choice(N, N // 6, replace=False))
+        w = rng.uniform(0.0, 40.0, len(rows))
+        if form == "rows":
+            eng.update_wants(rows, w)
+        else:
+            eng.update_wants_mask(W.rows_to_mask(rows, N), w)
+        st2 = eng.read_store()
+        want_w = st["wants"].copy()
+        live_rows = ~released[rows]
+        want_w[rows[live_rows]] = w[live_rows]
+        assert st2["wants"].tobytes() == want_w.tobytes(), f"round {t}: store wants"
+        res = eng.resources(safe=False)
+        live_w = np.where(released, 0.0, st2["wants"])
+        assert float_close(res["sum_wants"], np.bincount(seg_of, live_w, R), cap, 1e-12).all(), f"round {t}"
+        cur = dict(snap)
+        cur.update(has=st2["has"], wants=st2["wants"], subclients=st2["subclients"], expiry_ns=st2["expiry_ns"],
+                   agg_count=res["count"], agg_sum_has=res["sum_has"], agg_sum_wants=res["sum_wants"])
+        now += 5 * W.NS
+        ref = O.apportion(cur, now)
+        eng.apportion(now, writeback=True)
+        st3 = eng.read_store()
+        live = ref["expiry_ns"] != W.RELEASED
+        assert float_close(np.where(live, st3["has"], 0.0), np.where(live, ref["gets"], 0.0), row_capacity(cur)).all()
+        res = eng.resources(safe=False)
+        rel3 = st3["expiry_ns"] == W.RELEASED
+        np.testing.assert_array_equal(res["count"], np.bincount(seg_of, np.where(rel3, 0, st3["subclients"]), R))
+        assert float_close(res["sum_wants"], np.bincount(seg_of, np.where(rel3, 0.0, st3["wants"]), R), cap,
+                           1e-12).all(), f"round {t}: after the tick"
+
+
 def test_update_wants_mask_rejects_bad_input(eng):
     """Count mismatch (DM_E_INVAL), a bit past the store's end (DM_E_RANGE), a window
     not on a 64-row boundary (DM_E_INVAL): the store is left untouched."""
