@@ -25,3 +25,4 @@ if [ -x tools/ubench ]; then
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/cal_write -o run -- ./tools/ubench 10000000 1000 > $OUT/cal_write.log 2>&1 || exit $?
 fi
 python3 tools/pmc_summary.py $OUT $W
+cp profiles/pmc_$W.json profiles/rocprof_$W.md $OUT/ && echo "summaries in $OUT"
