@@ -135,6 +135,39 @@ struct Partials {
   int32_t* uni;
 };
 constexpr int kSegTotBytes = 128;
+
+// The speculative chain (k_large_spec / k_large_redo, dm_kernels.hip): per large
+// resource, the round-1 / round-2 totals and the live rows' count its last tick
+// verified (or redid), used as this tick's speculation; the redo's inputs and meeting
+// points.  Reductions over a resource's chunk partials here all take one fixed tree
+// (wave 0, 64 lanes striding the chunks in order), so a total recomputed from the
+// same partials is bit-identical to the stored one.
+struct SpecTot {
+  double bx, by;        // AggB of the last verified tick (FairShare E / W, ProportionalShare x / y)
+  long long bi;
+  double cee;           // AggC
+  long long csgt;
+  int32_t s0;           // the live rows' one subclient count
+  int32_t valid;        // bx .. s0 hold a tick's totals
+  uint32_t redo;        // this tick's speculation failed (set by k_large_spec, cleared by the redo)
+  uint32_t arrive[3];   // arrival counters (reset by their last arriver)
+  uint64_t ready[2];    // the redo's ready flags: its launch number + 1 once a total is stored
+  // k_large_spec's verifier leaves the resource's actual pass-A totals and round 1
+  // (equalShare from the running Count) for the redo
+  long long a_cnt;
+  double a_h, a_w;
+  int32_t a_smin, a_smax, a_nan, pad;
+  double abx, aby;
+  long long abi;
+};
+struct SpecArgs {
+  SpecTot* tot;     // [large resources]
+  uint64_t seq;     // the redo's launch number
+  int32_t* err;     // host-mapped: a redo chunk gave up waiting for its resource's others
+  uint32_t* ring;   // [4]: per tick parity, "some resource marked" and the redo's chunk tickets
+  int par;          // this tick's parity (the redo clears the other slots for the next tick)
+  int nchunks;
+};
 constexpr int kHetMaxS = 256;                    // distinct subclient counts per resource on the chain
 constexpr int kHetBuckets = 2 * kHetMaxS + 1;    // strictly between / equal to the sorted thresholds
 struct HetRes {

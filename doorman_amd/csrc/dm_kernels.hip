@@ -181,7 +181,8 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
         if (__all(ok)) {
           fast_a = true;
           const int base = (int)(threadIdx.x & 63) & ~(G - 1);
-          const uint64_t gmask = G == 64 ? ~0ull : (((1ull << G) - 1) << base);
+          uint64_t gmask = ~0ull;
+          if constexpr (G < 64) gmask = ((1ull << G) - 1) << base;
           const bool any_live = (lv & gmask) != 0;
           a.smin = any_live ? u : INT32_MAX;
           a.smax = any_live ? u : INT32_MIN;
@@ -736,6 +737,7 @@ struct ChunkRows {
 // uni >= 0: the subclients words are not read -- a row whose bit in prev_live (the
 // last writeback tick's live bits, Partials::s_live) is set holds uni, any other row is
 // marked released
+template <bool ALLH = false>  // ALLH: has of every row, loaded beside wants (the speculative chain)
 __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, ChunkRows& r, const Res& rs,
                                            int uni = -1, uint32_t prev_live = 0) {
   const double* __restrict__ wb = p.wants + ch.row0;
@@ -751,7 +753,7 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
   for (int k = 0; k < kLR; ++k) {
     const int i = k * 256 + threadIdx.x;
     r.w[k] = wb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)];
-    r.h[k] = 0.0;
+    r.h[k] = ALLH ? hb[(unsigned)(i < ch.nrows ? i : ch.nrows - 1)] : 0.0;
   }
   if (uni >= 0) {
 #pragma unroll
@@ -785,7 +787,7 @@ __device__ __forceinline__ void load_chunk(const DevParams& p, const Chunk& ch, 
     r.s[k] = sub_value(sr[k]);
   }
   // a row already marked released holds has 0 (every path that marks one zeroes it)
-  const unsigned need_h = p.recompute ? r.valid : (r.valid & ~r.live & ~r.rel);
+  const unsigned need_h = ALLH ? 0u : p.recompute ? r.valid : (r.valid & ~r.live & ~r.rel);
   if (__any(need_h != 0)) {
 #pragma unroll
     for (int k = 0; k < kLR; ++k)
@@ -1103,6 +1105,44 @@ __global__ __launch_bounds__(256) void k_large_c(DevParams p, const Chunk* __res
   }
 }
 
+// The map of one chunk (store.go:153-167 Assign): decide and write every lease of its
+// rows under the resource's totals; returns the chunk's sum of gets - has.  (k_large_map
+// keeps its own copy of the loop: called, that kernel spilled 68 B per lane.)
+__device__ __forceinline__ double map_chunk(const DevParams& p, const Chunk& ch, const ChunkRows& rw, const Res rs,
+                                            const Clean cl, const AggB b, const FsU fu) {
+  const double C = rs.C;
+  const double eq = C / (double)cl.count;
+  double delta = 0.0;
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.valid >> k & 1)) continue;
+    const unsigned u = (unsigned)(k * 256 + threadIdx.x);
+    const double w = rw.w[k], h = rw.h[k];
+    if (!(rw.live >> k & 1)) {  // released by Clean (the raw word for put_released: marked or not)
+      put_released(p, ch.row0, u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
+      continue;
+    }
+    double g;
+    if (rs.learning) {
+      g = h;
+    } else if (rs.kind == 0) {
+      g = w;
+    } else if (rs.kind == 1) {
+      g = minF(C, w);
+    } else if (rs.kind == 2) {
+      const double epc = eq * (double)rw.s[k];
+      const double unused = C - cl.sum_has + h;
+      g = (cl.sum_wants <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (b.x / b.y), unused);
+    } else {
+      g = fs_uniform_row(w, h, C, cl.sum_has, fu);
+    }
+    // an explicit row becomes a follower (its subclients word without the flag)
+    put_live(p, ch.row0, u, g, rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
+    delta += g - h;
+  }
+  return delta;
+}
+
 __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __restrict__ chunks,
                                                    const LargeSeg* __restrict__ ls, Partials P, int32_t* glist,
                                                    int32_t* gcount) {
@@ -1189,6 +1229,383 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
   if (threadIdx.x == 0) {
     tt->rel = 0;  // pass A of the next tick sets it again (every chunk has read it)
     write_resource(p, L.seg, rs, st.cl, d.v);
+  }
+}
+
+// --------------------------------------------------------------------------
+// The speculative chain (the steady state of P.b_first ticks, DM_SPEC_CHAIN).
+// k_large_spec: one launch over every chunk.  Each chunk computes its exact pass-A
+// partials and its round-1 partials (equalShare from the running Count, as pass A's
+// speculative round 1), its round-2 partials at the threshold the resource's stored
+// totals give (SpecTot: its last tick's), and writes its leases under those stored
+// totals -- unless its own rows show a lapse, a NaN wants or another count, when it
+// writes nothing.  The resource's last-arriving chunk (no waiting) reduces the
+// partials with one fixed tree and compares them bit for bit with the stored totals:
+// equal, the leases written are exactly the chain's (the same totals, the same rows)
+// and it writes the resource's record; else it marks the resource for
+// k_large_redo.  Per lease: wants and has read, gets written -- one pass instead of
+// the chain's four launches and second read.
+// k_large_redo: one launch, every chunk of an unmarked resource leaves at once.  A
+// marked resource's chunks hold their rows in registers and meet twice at most
+// (round 1 again when Clean released rows, round 2), through write-through partials,
+// the last arriver's write-through total and a ready flag (the launch number); they
+// then rewrite their leases and the last arriver stores the totals as the next
+// tick's speculation.  Waiting chunks hold wave slots (why the chain is not built
+// this way), but only a marked resource's; a wait is bounded (kSpecSpin polls: the
+// host then reports DM_E_INTERNAL).  Forward progress as for any in-order dispatched
+// grid whose chunks wait only for their own resource's (at most 489 chunks, C2).
+// --------------------------------------------------------------------------
+constexpr uint32_t kSpecSpin = 1u << 22;  // polls of ~0.1 us
+
+__device__ __forceinline__ bool dbl_pos0(double x) { return __double_as_longlong(x) == 0; }
+
+// wave 0's fixed reduction over a resource's chunk partials (lane l: chunks begin + l,
+// begin + l + 64, ... in order, then the wave's DPP tree); every lane gets the total
+template <typename T, typename Op, typename Ld>
+__device__ __forceinline__ T canon_reduce(int begin, int end, T v, Op op, Ld ld) {
+  for (int q = begin + (int)(threadIdx.x & 63); q < end; q += 64) v = op(v, ld(q));
+  return wave_reduce(v, op);
+}
+__device__ __forceinline__ AggA canon_a(const Partials& P, const LargeSeg& L) {
+  return canon_reduce(L.chunk_begin, L.chunk_end, zeroA(), OpA(), [&](int q) {
+    AggA x = zeroA();
+    x.cnt = ld_wt(P.a_cnt + q);
+    x.h = ld_wt(P.a_has + q);
+    x.w = ld_wt(P.a_wants + q);
+    x.smin = (int)ld_wt(P.a_smin + q);
+    x.smax = (int)ld_wt(P.a_smax + q);
+    x.nan = ld_wt(P.a_nan + q);
+    return x;
+  });
+}
+__device__ __forceinline__ AggB canon_b(const Partials& P, const LargeSeg& L) {
+  return canon_reduce(L.chunk_begin, L.chunk_end, AggB{0.0, 0.0, 0}, OpB(),
+                      [&](int q) { return AggB{ld_wt(P.b_x + q), ld_wt(P.b_y + q), ld_wt(P.b_w + q)}; });
+}
+__device__ __forceinline__ AggC canon_c(const Partials& P, const LargeSeg& L) {
+  return canon_reduce(L.chunk_begin, L.chunk_end, AggC{0.0, 0}, OpC(),
+                      [&](int q) { return AggC{ld_wt(P.c_ee + q), ld_wt(P.c_sgt + q)}; });
+}
+__device__ __forceinline__ double canon_d(const Partials& P, const LargeSeg& L) {
+  return canon_reduce(L.chunk_begin, L.chunk_end, SumD{0.0}, OpSumD(),
+                      [&](int q) { return SumD{ld_wt(P.d_delta + q)}; }).v;
+}
+
+// pass A (Clean sums of the rows it releases, the live rows' count range, NaN wants)
+// and round 1 with equalShare eq over the chunk's rows in registers (as k_large_a)
+__device__ __forceinline__ AggA chunk_a(const ChunkRows& rw) {
+  AggA a = zeroA();
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.valid >> k & 1)) continue;
+    if (!(rw.live >> k & 1)) {
+      a.cnt += rw.s[k];
+      a.h += rw.h[k];
+      a.w += rw.w[k];
+    } else {
+      a.smin = rw.s[k] < a.smin ? rw.s[k] : a.smin;
+      a.smax = rw.s[k] > a.smax ? rw.s[k] : a.smax;
+      a.nan |= __builtin_isnan(rw.w[k]) ? 1 : 0;
+    }
+  }
+  return a;
+}
+__device__ __forceinline__ AggB chunk_b(const ChunkRows& rw, int kind, double eq) {
+  AggB b{0.0, 0.0, 0};
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.live >> k & 1)) continue;
+    const double w = rw.w[k];
+    const int sk = rw.s[k];
+    if (kind == 2) {
+      const double e = eq * (double)sk;  // algorithm.go:273
+      if (w < e)
+        b.x += e - w;
+      else
+        b.y += w - e;
+    } else {
+      const double d = (double)sk * eq;  // algorithm.go:160
+      if (w < d)
+        b.x += d - w;
+      else if (w > d)
+        b.i += sk;
+    }
+  }
+  return b;
+}
+// round 2 at threshold Tu over the live rows, every one holding s0 (k_large_c)
+__device__ __forceinline__ AggC chunk_c(const ChunkRows& rw, int s0, double eq, double Tu) {
+  AggC x{0.0, 0};
+#pragma unroll
+  for (int k = 0; k < kLR; ++k) {
+    if (!(rw.live >> k & 1)) continue;
+    const double w = rw.w[k];
+    if (!(w > (double)s0 * eq)) continue;
+    if (w < Tu)
+      x.ee += Tu - w;
+    else if (w > Tu)
+      x.sgt += s0;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(256) void k_large_spec(DevParams p, const Chunk* __restrict__ chunks,
+                                                    const LargeSeg* __restrict__ ls, Partials P, SpecArgs S) {
+  __shared__ Lds<256> lds;
+  __shared__ int s_ok;
+  const int c = blockIdx.x;
+  const int t = threadIdx.x;
+  const Chunk ch = chunks[c];
+  const Res rs = load_res(p, ch.seg);
+  SpecTot* sp = S.tot + ch.lseg;
+  ChunkRows rw;
+  {
+    const int uni = P.s_live ? __builtin_amdgcn_readfirstlane(P.uni[c]) : -1;
+    const uint32_t prev_live = P.s_live ? P.live[(size_t)c * 256 + t] : 0u;
+    load_chunk<true>(p, ch, rw, rs, uni, prev_live);
+  }
+  const int valid = sp->valid, s0 = sp->s0;  // the stored totals (written by earlier launches)
+  const AggB bs{sp->bx, sp->by, sp->bi};
+  const AggC cs{sp->cee, sp->csgt};
+  AggA a = chunk_a(rw);
+  P.live[(size_t)c * 256 + t] = rw.live | rw.expl << 8 | rw.rel << 16;
+  const bool r1 = !rs.learning && rs.kind >= 2;
+  const bool fs = !rs.learning && rs.kind == 3;
+  const double eq = rs.C / (double)rs.agg_count;  // the running Count: exact when Clean releases nothing
+  AggB b = r1 ? chunk_b(rw, rs.kind, eq) : AggB{0.0, 0.0, 0};
+  a = group_reduce_t0<256>(a, OpA(), lds.a);
+  if (r1) b = group_reduce_t0<256>(b, OpB(), lds.b);
+  if (t == 0)  // this chunk's rows agree with the speculation: nothing released, one count s0, no NaN
+    s_ok = (valid && a.cnt == 0 && dbl_pos0(a.h) && dbl_pos0(a.w) && !a.nan &&
+            (a.smin > a.smax || (a.smin == s0 && a.smax == s0)))
+               ? 1
+               : 0;
+  __syncthreads();
+  const bool ok = s_ok != 0;
+  AggC x{0.0, 0};
+  SumD delta{0.0};
+  if (ok) {
+    AggA z = zeroA();
+    z.smin = z.smax = s0;
+    const Clean cl = clean_from(p, rs, z);  // the running sums: the Clean of a tick that releases nothing
+    const FsU fu = uniform(make_fsu(eq, s0, bs.x, bs.i, cs));
+    if (fs) x = group_reduce_t0<256>(chunk_c(rw, s0, eq, fu.T), OpC(), lds.c);
+    delta.v = map_chunk(p, ch, rw, rs, cl, uniform(bs), fu);
+    delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
+  }
+  if (t == 0) {
+    st_wt(P.a_cnt + c, (int64_t)a.cnt);
+    st_wt(P.a_has + c, a.h);
+    st_wt(P.a_wants + c, a.w);
+    st_wt(P.a_smin + c, (int64_t)a.smin);
+    st_wt(P.a_smax + c, (int64_t)a.smax);
+    st_wt(P.a_nan + c, a.nan);
+    st_wt(P.b_x + c, b.x);
+    st_wt(P.b_y + c, b.y);
+    st_wt(P.b_w + c, (int64_t)b.i);
+    st_wt(P.c_ee + c, x.ee);
+    st_wt(P.c_sgt + c, (int64_t)x.sgt);
+    st_wt(P.d_delta + c, delta.v);
+    P.uni[c] = ok ? s0 : -1;  // the redo rewrites a marked resource's
+    if (!ok) __hip_atomic_store((gu32*)&sp->redo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (t >= 64) return;  // wave 0 verifies (dm_kernel_util.h arrive_last)
+  const LargeSeg L = ls[ch.lseg];
+  if (!arrive_last(&sp->arrive[0], L.chunk_end - L.chunk_begin)) return;
+  const AggA at = canon_a(P, L);
+  const AggB bt = canon_b(P, L);
+  const AggC ct = canon_c(P, L);
+  const bool marked = __hip_atomic_load((gu32*)&sp->redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  bool same = valid && !marked && at.cnt == 0 && dbl_pos0(at.h) && dbl_pos0(at.w) && !at.nan &&
+              (at.smin > at.smax || (at.smin == s0 && at.smax == s0));
+  if (rs.kind == 2 && !rs.learning)
+    same = same && __double_as_longlong(bt.x) == __double_as_longlong(bs.x) &&
+           __double_as_longlong(bt.y) == __double_as_longlong(bs.y);
+  if (fs)
+    same = same && __double_as_longlong(bt.x) == __double_as_longlong(bs.x) && bt.i == bs.i &&
+           __double_as_longlong(ct.ee) == __double_as_longlong(cs.ee) && ct.sgt == cs.sgt;
+  if (same) {
+    const double d = canon_d(P, L);
+    if (t == 0) {
+      AggA z = zeroA();
+      z.smin = z.smax = s0;
+      write_resource(p, L.seg, rs, clean_from(p, rs, z), d);
+    }
+    return;
+  }
+  if (t == 0) {  // the redo's inputs: the actual pass-A totals and round 1 at the running Count
+    sp->redo = 1;
+    S.ring[S.par] = 1;  // (read by the next launch)
+    sp->a_cnt = at.cnt;
+    sp->a_h = at.h;
+    sp->a_w = at.w;
+    sp->a_smin = at.smin;
+    sp->a_smax = at.smax;
+    sp->a_nan = at.nan;
+    sp->abx = bt.x;
+    sp->aby = bt.y;
+    sp->abi = bt.i;
+  }
+}
+
+// every thread's write-through stores have landed, then one arrival; true (uniform)
+// for the last arriver, which resets the counter
+__device__ __forceinline__ bool spec_arrive(uint32_t* ctr, int nch, int* s_last) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)nch - 1 ? 1 : 0;
+    if (last) __hip_atomic_store((gu32*)ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_last = last;
+  }
+  __syncthreads();
+  return *s_last != 0;
+}
+__device__ __forceinline__ void spec_ready(const SpecArgs& S, uint64_t* flag) {  // the last arriver's stores landed
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_wt(flag, S.seq + 1);
+  }
+}
+__device__ __forceinline__ void spec_wait(const SpecArgs& S, const uint64_t* flag) {
+  if (threadIdx.x == 0) {
+    for (uint32_t it = 0; ld_wt(flag) < S.seq + 1; ++it) {
+      if (it >= kSpecSpin) {
+        __hip_atomic_store(S.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+  __syncthreads();
+}
+
+// one chunk of a marked resource (k_large_redo's loop)
+__device__ __forceinline__ void redo_chunk(const DevParams& p, const Chunk* __restrict__ chunks,
+                                           const LargeSeg* __restrict__ ls, const Partials& P, const SpecArgs& S,
+                                           int32_t* glist, int32_t* gcount, int c, Lds<256>& lds, int* s_last_p) {
+  int& s_last = *s_last_p;
+  const int t = threadIdx.x;
+  const Chunk ch = chunks[c];
+  SpecTot* sp = S.tot + ch.lseg;
+  const Res rs = load_res(p, ch.seg);
+  const LargeSeg L = ls[ch.lseg];
+  const int nch = L.chunk_end - L.chunk_begin;
+  ChunkRows rw;
+  load_chunk<true>(p, ch, rw, rs);  // no speculation on the rows: the subclients column
+  AggA at = zeroA();
+  at.cnt = sp->a_cnt;
+  at.h = sp->a_h;
+  at.w = sp->a_w;
+  at.smin = sp->a_smin;
+  at.smax = sp->a_smax;
+  at.nan = sp->a_nan;
+  const SegState st = uniform(seg_state_of(p, ch.seg, at));
+  if (st.general) {  // k_general decides it (its first chunk lists it)
+    if (t == 0) {
+      P.uni[c] = -1;
+      if (c == L.chunk_begin) {
+        glist[atomicAdd(gcount, 1)] = L.seg;
+        sp->redo = 0;
+        sp->valid = 0;
+      }
+    }
+    return;
+  }
+  const bool r1 = !rs.learning && rs.kind >= 2;
+  const bool fs = !rs.learning && rs.kind == 3;
+  const double eq = rs.C / (double)st.cl.count;
+  AggB bt{sp->abx, sp->aby, sp->abi};  // round 1 at the running Count: exact when Clean released nothing
+  if (r1 && at.cnt != 0) {  // round 1 again at the Count after Clean
+    const AggB x = group_reduce_t0<256>(chunk_b(rw, rs.kind, eq), OpB(), lds.b);
+    if (t == 0) {
+      st_wt(P.b_x + c, x.x);
+      st_wt(P.b_y + c, x.y);
+      st_wt(P.b_w + c, (int64_t)x.i);
+    }
+    if (spec_arrive(&sp->arrive[1], nch, &s_last)) {
+      if (t < 64) {
+        const AggB r = canon_b(P, L);
+        if (t == 0) {
+          st_wt(&sp->abx, r.x);
+          st_wt(&sp->aby, r.y);
+          st_wt(reinterpret_cast<int64_t*>(&sp->abi), (int64_t)r.i);
+        }
+      }
+      spec_ready(S, &sp->ready[0]);
+    }
+    spec_wait(S, &sp->ready[0]);
+    bt = AggB{ld_wt(&sp->abx), ld_wt(&sp->aby), ld_wt(reinterpret_cast<const int64_t*>(&sp->abi))};
+  }
+  const int s0 = st.a.smin;
+  AggC ct{0.0, 0};
+  FsU fu = make_fsu(eq, s0, bt.x, bt.i, ct);
+  if (fs) {  // round 2 at the resource's threshold
+    const AggC x = group_reduce_t0<256>(chunk_c(rw, s0, eq, fu.T), OpC(), lds.c);
+    if (t == 0) {
+      st_wt(P.c_ee + c, x.ee);
+      st_wt(P.c_sgt + c, (int64_t)x.sgt);
+    }
+    if (spec_arrive(&sp->arrive[2], nch, &s_last)) {
+      if (t < 64) {
+        const AggC r = canon_c(P, L);
+        if (t == 0) {
+          st_wt(&sp->cee, r.ee);
+          st_wt(reinterpret_cast<int64_t*>(&sp->csgt), (int64_t)r.sgt);
+        }
+      }
+      spec_ready(S, &sp->ready[1]);
+    }
+    spec_wait(S, &sp->ready[1]);
+    ct = AggC{ld_wt(&sp->cee), ld_wt(reinterpret_cast<const int64_t*>(&sp->csgt))};
+    fu = make_fsu(eq, s0, bt.x, bt.i, ct);
+  }
+  SumD delta{map_chunk(p, ch, rw, rs, st.cl, uniform(bt), uniform(fu))};
+  delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
+  if (t == 0) P.uni[c] = st.a.smin == st.a.smax ? st.a.smin : -1;
+  if (t >= 64) return;  // (the loop's barrier waits for wave 0)
+  if (t == 0) st_wt(P.d_delta + c, delta.v);
+  if (!arrive_last(&sp->arrive[0], nch)) return;
+  const double d = canon_d(P, L);
+  if (t == 0) {
+    write_resource(p, L.seg, rs, st.cl, d);
+    // the next tick's speculation: this tick's totals (round 1 and 2 as the chunks used
+    // them; a resource whose live rows hold mixed counts is not speculated on)
+    sp->bx = bt.x;
+    sp->by = bt.y;
+    sp->bi = bt.i;
+    sp->cee = ct.ee;
+    sp->csgt = ct.sgt;
+    sp->s0 = s0;
+    sp->valid = (st.a.smin >= st.a.smax) ? 1 : 0;  // one count, or no live row
+    sp->redo = 0;
+  }
+}
+
+// A grid of at least as many workgroups as the largest resource has chunks (the waits
+// of a resource's chunks are then always met: tickets go out in chunk order, so only
+// the resource at the ticket front can have chunks not yet taken).  With no resource
+// marked it leaves after one load; else its workgroups take chunk tickets in order and
+// do the marked resources' chunks.
+__global__ __launch_bounds__(256) void k_large_redo(DevParams p, const Chunk* __restrict__ chunks,
+                                                    const LargeSeg* __restrict__ ls, Partials P, SpecArgs S,
+                                                    int32_t* glist, int32_t* gcount) {
+  __shared__ Lds<256> lds;
+  __shared__ int s_last, s_c;
+  const int q = S.par ^ 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next tick's slots (its k_large_spec runs after this)
+    S.ring[q] = 0;
+    S.ring[2 + q] = 0;
+  }
+  if (!S.ring[S.par]) return;  // nothing marked (k_large_spec: the previous launch)
+  for (;;) {
+    if (threadIdx.x == 0) s_c = (int)atomicAdd(S.ring + 2 + S.par, 1u);
+    __syncthreads();
+    const int c = s_c;
+    if (c >= S.nchunks) return;
+    if (S.tot[chunks[c].lseg].redo) redo_chunk(p, chunks, ls, P, S, glist, gcount, c, lds, &s_last);
+    __syncthreads();  // every wave back (redo_chunk's waves 1-3 leave before its finish) before the next ticket
   }
 }
 
@@ -2624,6 +3041,17 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
     case 4: k_large_fin<<<nls, 256, 0, st>>>(p, ls, P, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
+                             const Partials& P, const SpecArgs& S, int redo_grid, int32_t* glist, int32_t* gcount,
+                             hipStream_t st) {
+  if (nchunks <= 0) return hipSuccess;
+  if (phase == 0)
+    k_large_spec<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, S);
+  else
+    k_large_redo<<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
   return hipGetLastError();
 }
 

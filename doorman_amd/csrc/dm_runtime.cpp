@@ -27,6 +27,9 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
                             int32_t* glist, int32_t* gcount, int32_t* guard, hipStream_t st);
 hipError_t launch_tick_done(const TickDone& td, hipStream_t st);
+hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
+                             const Partials& P, const SpecArgs& S, int redo_grid, int32_t* glist, int32_t* gcount,
+                             hipStream_t st);
 hipError_t launch_count_undense(const WorkItem* items, int n, unsigned long long* rec, unsigned long long epoch,
                                 hipStream_t st);
 hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
@@ -108,6 +111,8 @@ enum KClass {
   KC_LARGE_E,   // bucket totals,
   KC_LARGE_MH,  // the map
   KC_DECIDE,    // dm_decide: the round's device work (fast path + k_decide)
+  KC_LARGE_SPEC, // the speculative chain: k_large_spec,
+  KC_LARGE_REDO, // k_large_redo
   KC_COUNT
 };
 // bin 6 (2049-4096 rows) runs on 256 x 16 or 512 x 8 workgroups (kBin6Wide):
@@ -120,7 +125,8 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "block128x8_dense", "block256x8_dense", "block2k4k_dense",
                                      "block128x4_rest", "block128x8_rest", "block256x8_rest", "block2k4k_rest",
                                      "hier_publish",
-                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het", "decide"};
+                                     "hier_root", "large_t", "large_c_het", "large_e", "large_map_het", "decide",
+                                     "large_spec", "large_redo"};
 
 template <typename T>
 struct DBuf {
@@ -343,6 +349,15 @@ struct dm_ctx {
   DBuf<int32_t> pa_nan;
   DBuf<uint32_t> pa_live;
   DBuf<uint8_t> p_tot;
+  // the speculative chain (k_large_spec + k_large_redo; DM_SPEC_CHAIN=0: the chain):
+  // per large resource its SpecTot, the redo's launch count, the host-mapped give-up flag
+  bool spec_chain = true;
+  DBuf<SpecTot> p_spec;
+  DBuf<uint32_t> p_spec_ring;  // SpecArgs::ring
+  int redo_grid = 64;          // k_large_redo's workgroups: at least the largest resource's chunks
+  uint64_t spec_seq = 0;
+  int32_t* h_serr = nullptr;
+  int32_t* d_serr = nullptr;
   DBuf<int32_t> p_uni;
   // heterogeneous FairShare on the chain (allocated on the first tick that may need it)
   DBuf<uint32_t> ph_set;  // per large resource: distinct subclient counts (all ones between ticks)
@@ -509,7 +524,9 @@ struct dm_ctx {
     h_guard = d_guard = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pa_live.release(); p_tot.release(); p_uni.release();
+    pa_nan.release(); pa_live.release(); p_tot.release(); p_uni.release(); p_spec.release(); p_spec_ring.release();
+    if (h_serr) (void)hipHostFree(h_serr);
+    h_serr = d_serr = nullptr;
     ph_set.release(); ph_n.release(); ph_bkc.release(); ph_het.release(); ph_bkw.release(); ph_bks.release();
     ph_set_ready = 0;
     glist.release(); gcount.release();
@@ -697,6 +714,23 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, c->pa_live.ensure(nc * 256), "partials");
   DM_HIP(c, c->p_uni.ensure(nc), "partials");
   DM_HIP(c, c->p_tot.ensure(std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes), "partials");
+  {  // no resource has totals to speculate on yet (valid 0)
+    const size_t nl = std::max<size_t>(c->h_large.size(), 1);
+    DM_HIP(c, c->p_spec.ensure(nl), "speculative chain");
+    DM_HIP(c, hipMemsetAsync(c->p_spec.p, 0, nl * sizeof(SpecTot), st), "speculative chain");
+    DM_HIP(c, c->p_spec_ring.ensure(4), "speculative chain");
+    DM_HIP(c, hipMemsetAsync(c->p_spec_ring.p, 0, 4 * sizeof(uint32_t), st), "speculative chain");
+    int most = 1;
+    for (const LargeSeg& L : c->h_large) most = std::max(most, L.chunk_end - L.chunk_begin);
+    c->redo_grid = std::min<int>(std::max<int>((int)c->h_chunks.size(), 1), std::max(most, 64));
+    c->spec_seq = 0;
+    if (!c->h_serr) {
+      DM_HIP(c, hipHostMalloc((void**)&c->h_serr, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
+             "speculative chain");
+      DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_serr, c->h_serr, 0), "speculative chain");
+    }
+    __atomic_store_n(c->h_serr, 0, __ATOMIC_RELAXED);
+  }
   DM_HIP(c, hipMemsetAsync(c->p_tot.p, 0, std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes, st),
          "partials");  // SegTot::rel starts clear
   c->n_nonsmall = 0;
@@ -810,6 +844,7 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
   if (const char* hw = getenv("DM_TPL_HOSTWAIT")) c->tpl_hostwait = atoi(hw) != 0;
   if (const char* sr = getenv("DM_SKIP_REST")) c->skip_rest = atoi(sr) != 0;
+  if (const char* sc = getenv("DM_SPEC_CHAIN")) c->spec_chain = atoi(sc) != 0;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1160,6 +1195,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   for (int i = 0; c->h_guard && i < dm_ctx::kSplitBins; ++i)
     if (__atomic_load_n(c->h_guard + i, __ATOMIC_RELAXED))
       return c->fail(DM_E_INTERNAL, "a dense kernel queued an item on a tick that skipped its rest kernel");
+  if (c->h_serr && __atomic_load_n(c->h_serr, __ATOMIC_RELAXED))
+    return c->fail(DM_E_INTERNAL, "a redo workgroup of the speculative chain gave up waiting for its resource");
   c->ticks_issued += 1;
   c->tick_seq += 1;
   c->tick_flagged = false;
@@ -1183,8 +1220,12 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // serves better (72 vs 76 us).
   if ((flags & DM_WB_INPLACE) && (flags & DM_WB_ALTERNATE))
     return c->fail(DM_E_INVAL, "DM_WB_INPLACE and DM_WB_ALTERNATE are exclusive");
-  const bool pingpong =
-      wb && !(flags & DM_WB_INPLACE) && ((flags & DM_WB_ALTERNATE) || c->N * 48 > kStreamBytes);
+  // The speculative large chain (below) writes its gets before they are verified, so a
+  // tick that may take it writes the alternate column whatever the store's size.
+  const bool spec_eligible = c->spec_chain && wb && !(flags & DM_AGG_RECOMPUTE) && !c->expl_rows &&
+                             !(c->maybe_general && c->n_nonsmall > 0) && !c->h_chunks.empty();
+  const bool pingpong = wb && !(flags & DM_WB_INPLACE) &&
+                        ((flags & DM_WB_ALTERNATE) || c->N * 48 > kStreamBytes || spec_eligible);
   // A writeback tick writes no per-lease expiry: the leases it grants follow their
   // resource's expiry (dm_device.h), so only gets (and rare subclients words) move.
   if (!wb) {
@@ -1294,7 +1335,22 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     static constexpr int kSeq[9] = {0, 1, 5, 2, 6, 7, 3, 8, 4};
     static constexpr int kCls[9] = {KC_LARGE_A, KC_LARGE_B,   KC_LARGE_T,  KC_LARGE_C,  KC_LARGE_CH,
                                     KC_LARGE_E, KC_LARGE_MAP, KC_LARGE_MH, KC_LARGE_FIN};
-    for (int i = 0; i < 9 && nch > 0; ++i) {
+    // the steady state: one speculative launch, verified per resource, and a redo launch
+    // that only the resources whose totals moved use (the store's rows must not be
+    // overwritten by the speculative gets: alternate output columns)
+    const bool spec = c->spec_chain && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
+    if (spec) {
+      const SpecArgs S{c->p_spec.p, c->spec_seq, c->d_serr, c->p_spec_ring.p, (int)(c->spec_seq & 1), nch};
+      c->spec_seq += 1;
+      for (int ph = 0; ph < 2; ++ph)
+        DM_HIP(c, timed(ph == 0 ? KC_LARGE_SPEC : KC_LARGE_REDO, s_large,
+                        [&] {
+                          return launch_large_spec(ph, p, c->chunks.p, nch, c->large.p, P, S, c->redo_grid, gl, gc,
+                                                   s_large);
+                        }),
+               "large-resource kernels");
+    }
+    for (int i = 0; i < 9 && nch > 0 && !spec; ++i) {
       const int ph = kSeq[i];
       if (ph >= 5 && !het) continue;
       if (ph == 4 && !het) continue;  // the map's last-arriving chunks did fin's work

@@ -135,7 +135,8 @@ def _store_as_snapshot(snap, eng):
     return s
 
 
-def test_large_writeback_ticks_against_oracle():
+@pytest.mark.parametrize("cols", ["auto", "alternate"])  # alternate: the speculative chain
+def test_large_writeback_ticks_against_oracle(cols):
     """Writeback ticks on large FairShare / ProportionalShare resources (the chain's
     speculative round 1 and the per-resource totals it leaves in SegTot reused tick
     after tick), each checked against the oracle on the device store as it stood
@@ -183,7 +184,7 @@ def test_large_writeback_ticks_against_oracle():
                 eng.release(rng.choice(N, 500, replace=False).astype(np.int64))
             cur = pre if step == "peek" else _store_as_snapshot(snap, eng)
             ref = O.apportion(cur, now)
-            eng.apportion(now, writeback=True)
+            eng.apportion(now, writeback=True, wb_columns=cols)
             st = eng.read_store()
             live = ref["expiry_ns"] != W.RELEASED
             gets = np.where(live, st["has"], 0.0)
@@ -195,7 +196,8 @@ def test_large_writeback_ticks_against_oracle():
         eng.close()
 
 
-def test_large_writeback_ticks_with_uniform_counts_other_than_one():
+@pytest.mark.parametrize("cols", ["auto", "alternate"])  # alternate: the speculative chain
+def test_large_writeback_ticks_with_uniform_counts_other_than_one(cols):
     """the steady-state pass A takes each row's count from the last
     writeback tick's live bits and the per-chunk count the map left (Partials::uni),
     not from the subclients column.  Here every large resource holds ONE count other
@@ -239,7 +241,7 @@ def test_large_writeback_ticks_with_uniform_counts_other_than_one():
                 gets, exp = eng.leases()
                 assert_leases_match(cur, gets, exp, ref, f"tick {i} (peek)")
                 continue
-            eng.apportion(now, writeback=True)
+            eng.apportion(now, writeback=True, wb_columns=cols)
             st = eng.read_store()
             live = ref["expiry_ns"] != W.RELEASED
             gets = np.where(live, st["has"], 0.0)
@@ -253,3 +255,91 @@ def test_large_writeback_ticks_with_uniform_counts_other_than_one():
         assert worst <= 1e-9
     finally:
         eng.close()
+
+
+def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch):
+    """The speculative chain (k_large_spec: one pass under the totals the resource's
+    last tick verified, checked bit for bit per resource; k_large_redo for the
+    resources whose totals moved) against the four-launch chain (DM_SPEC_CHAIN=0) and
+    the oracle, tick after tick, on large resources of every kind (learning ones
+    included) with changes between ticks that move some resources' totals and not
+    others': releases, a wants refresh of part of two resources, a capacity change,
+    followers lapsing, a non-writeback tick.  Leases match the oracle (SURVEY.md §8c);
+    the two engines' stores hold the same released rows and subclients and running
+    sums within the oracle tolerance (their reductions run in different orders); in
+    the steady ticks the speculative engine launches no pass of the chain."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(8080)
+    sizes = np.asarray([4097, 5000, 6000, 8192, 9000, 20000, 65537, 150000, 300, 17, 5], dtype=np.int64)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(0, 1, 2, 3), expired_frac=0.01, learning_frac=0.0,
+                               parent_expired_frac=0.0)
+    snap["kind"][:8] = [3, 3, 2, 3, 2, 3, 1, 3]
+    snap["learning_end_ns"][:8] = W.INT64_MIN
+    snap["learning_end_ns"][2] = NOW + 3600 * W.NS  # one large resource in learning mode
+    snap["lease_length_s"][:8] = [40, 600, 600, 600, 35, 600, 600, 600]  # two lapse at the "lapse" tick
+    so = np.asarray(snap["seg_off"])
+    N = len(snap["wants"])
+    cap = np.maximum(snap["capacity"], 1.0)
+    monkeypatch.setenv("DM_SPEC_CHAIN", "0")
+    chain = Engine(0)
+    monkeypatch.delenv("DM_SPEC_CHAIN")
+    spec = Engine(0)
+    try:
+        chain.load(snap)
+        spec.load(snap)
+        spec.set_profiling(True)
+        plan = ["same", "same", "same", "same", "release", "same", "same", "wants", "same", "same", "capacity",
+                "same", "same", "lapse", "same", "same", "peek", "same", "same"]
+        now = NOW
+        steady = []
+        capacity = snap["capacity"].copy()
+        for i, step in enumerate(plan):
+            now += (50 if step == "lapse" else 1) * W.NS
+            if step == "release":
+                rows = rng.choice(N, 300, replace=False).astype(np.int64)
+                for e in (chain, spec):
+                    e.release(rows)
+            elif step == "wants":  # part of resources 1 and 4 (FairShare, ProportionalShare)
+                rows = np.concatenate([np.arange(so[1], so[1] + 700), np.arange(so[4], so[4] + 2000)]).astype(np.int64)
+                w = rng.uniform(0.0, 3.0, len(rows)) * np.repeat(snap["capacity"], np.diff(so))[rows] / 1000.0
+                for e in (chain, spec):
+                    e.update_wants(rows, w)
+            elif step == "capacity":  # resource 5's capacity halves
+                capacity[5] *= 0.5
+                c2 = dict(snap)
+                c2["capacity"] = capacity
+                for e in (chain, spec):
+                    e.load_config(c2)
+            cur = _store_as_snapshot(snap, spec)
+            cur["capacity"] = capacity
+            ref = O.apportion(cur, now)
+            spec.reset_kernel_times()
+            wb = step != "peek"
+            # alternate output columns (as on a store beyond the Infinity Cache, C2): the
+            # speculative gets must not overwrite has before they are verified
+            chain.apportion(now, writeback=wb, wb_columns="alternate")
+            spec.apportion(now, writeback=wb, wb_columns="alternate")
+            kt = spec.kernel_times()
+            steady.append((kt.get("large_spec", (0, 0))[0], kt.get("large_a", (0, 0))[0]))
+            if wb:
+                st = spec.read_store()
+                live = ref["expiry_ns"] != W.RELEASED
+                gets = np.where(live, st["has"], 0.0)
+                assert float_close(gets, np.where(live, ref["gets"], 0.0), row_capacity(cur)).all(), f"tick {i} ({step})"
+                a = chain.read_store()
+                np.testing.assert_array_equal(a["expiry_ns"], st["expiry_ns"], err_msg=f"tick {i} ({step})")
+                np.testing.assert_array_equal(a["subclients"], st["subclients"], err_msg=f"tick {i} ({step})")
+                ra, rb = chain.resources(safe=False), spec.resources(safe=False)
+                np.testing.assert_array_equal(ra["count"], rb["count"], err_msg=f"tick {i} ({step})")
+                for k in ("sum_has", "sum_wants"):
+                    assert float_close(ra[k], rb[k], cap, 1e-12).all(), f"tick {i} ({step}): {k}"
+            else:
+                gets, exp = spec.leases()
+                assert_leases_match(cur, gets, exp, ref, f"tick {i} (peek)")
+        # the first tick runs the chain (loaded rows carry explicit expiries); every later
+        # writeback tick the speculative launch, never pass A
+        assert steady[0] == (0, 1), steady
+        assert all(s == (1, 0) for j, s in enumerate(steady[1:], 1) if plan[j] != "peek"), steady
+    finally:
+        chain.close()
+        spec.close()
