@@ -898,7 +898,15 @@ int dm_create(int device, dm_ctx** out) {
       }
     }
   }
+  // DM_CHAIN_PRIO=1: the large chain's stream at the highest priority (a queue of its own)
+  const int prio_aux = (getenv("DM_CHAIN_PRIO") && atoi(getenv("DM_CHAIN_PRIO")) != 0) ? c->class_stream[kNumBins + 1] : -1;
   for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
+    if (i == prio_aux) {
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, hi);
+      continue;
+    }
     e = cumask && ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, masks[i].data())
                           : hipErrorNotSupported;
     if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
