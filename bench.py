@@ -746,7 +746,18 @@ def main():
             return None, None
         if world > 1:  # one RCCL communicator of the library's own, its id from rank 0
             from doorman_amd.hierarchy import rccl_unique_id
-            obj = [rccl_unique_id() if rank == 0 else None]
+            # every rank first checks that the library can load RCCL (dlopen, an id), and the
+            # ranks agree before any of them enters the collective communicator set-up: a
+            # rank that failed inside it would leave the others waiting there
+            try:
+                uid, ok = rccl_unique_id(), 1
+            except Exception as e:  # noqa: BLE001 (reported, then the agreed fallback)
+                print(f"[bench] rank {rank}: the library's RCCL is unavailable ({e})", file=sys.stderr, flush=True)
+                uid, ok = None, 0
+            if -sync_ranks("max_int", -ok) == 0:
+                exchange_used["mode"] = "python (torch.distributed all-gather: the library's RCCL is unavailable)"
+                return None, None
+            obj = [uid if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             exchange_used["mode"] = "native (dm_hier_step, library RCCL all-gather over xGMI)"
             return "rccl", obj[0]
