@@ -167,6 +167,7 @@ struct SpecArgs {
   uint32_t* ring;   // [4]: per tick parity, "some resource marked" and the redo's chunk tickets
   int par;          // this tick's parity (the redo clears the other slots for the next tick)
   int nchunks;
+  uint32_t* seen;   // host-mapped: whether the last redo launch found a resource marked
 };
 constexpr int kHetMaxS = 256;                    // distinct subclient counts per resource on the chain
 constexpr int kHetBuckets = 2 * kHetMaxS + 1;    // strictly between / equal to the sorted thresholds

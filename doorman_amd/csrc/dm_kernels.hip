@@ -1588,15 +1588,25 @@ __device__ __forceinline__ void redo_chunk(const DevParams& p, const Chunk* __re
 // the resource at the ticket front can have chunks not yet taken).  With no resource
 // marked it leaves after one load; else its workgroups take chunk tickets in order and
 // do the marked resources' chunks.
-__global__ __launch_bounds__(256) void k_large_redo(DevParams p, const Chunk* __restrict__ chunks,
-                                                    const LargeSeg* __restrict__ ls, Partials P, SpecArgs S,
-                                                    int32_t* glist, int32_t* gcount) {
+// Two builds of the same code: the full one (160 VGPRs, 3 waves per SIMD) and a light
+// one held to 64 VGPRs (8 waves; the chunk's rows spill to scratch).  A steady tick
+// marks nothing, and there the launch is all the redo costs: the light build's
+// workgroups find a free slot beside the other classes' waves much sooner (C2: 20 ->
+// 10 us of event time, the tick -3.6 us), while a redo of every large resource takes
+// it 2x as long (C2's large class: 90 -> 180 us).  The host launches the light build
+// while the last redo it saw found nothing marked and no row changed since
+// (dm_runtime.cpp); both leave the same bits.
+template <bool kLight>
+__global__ __launch_bounds__(256, kLight ? 8 : 1) void k_large_redo(DevParams p, const Chunk* __restrict__ chunks,
+                                                                     const LargeSeg* __restrict__ ls, Partials P,
+                                                                     SpecArgs S, int32_t* glist, int32_t* gcount) {
   __shared__ Lds<256> lds;
   __shared__ int s_last, s_c;
   const int q = S.par ^ 1;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next tick's slots (its k_large_spec runs after this)
     S.ring[q] = 0;
     S.ring[2 + q] = 0;
+    __hip_atomic_store(S.seen, S.ring[S.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!S.ring[S.par]) return;  // nothing marked (k_large_spec: the previous launch)
   for (;;) {
@@ -3050,8 +3060,10 @@ hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks,
   if (nchunks <= 0) return hipSuccess;
   if (phase == 0)
     k_large_spec<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, S);
+  else if (phase == 1)
+    k_large_redo<false><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
   else
-    k_large_redo<<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
+    k_large_redo<true><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
   return hipGetLastError();
 }
 

@@ -356,8 +356,12 @@ struct dm_ctx {
   DBuf<uint32_t> p_spec_ring;  // SpecArgs::ring
   int redo_grid = 64;          // k_large_redo's workgroups: at least the largest resource's chunks
   uint64_t spec_seq = 0;
-  int32_t* h_serr = nullptr;
+  int32_t* h_serr = nullptr;  // [0] the give-up flag, [1] SpecArgs::seen
   int32_t* d_serr = nullptr;
+  // k_large_redo's light build (dm_kernels.hip) while the last redo the host saw found
+  // nothing marked and no row changed since (DM_REDO_LIGHT: 0 never, 1 so, 2 always)
+  int redo_light = 1;
+  uint64_t redo_epoch = 0;  // row_epoch at the last speculative tick
   DBuf<int32_t> p_uni;
   // heterogeneous FairShare on the chain (allocated on the first tick that may need it)
   DBuf<uint32_t> ph_set;  // per large resource: distinct subclient counts (all ones between ticks)
@@ -725,11 +729,12 @@ static int upload_plan(dm_ctx* c) {
     c->redo_grid = std::min<int>(std::max<int>((int)c->h_chunks.size(), 1), std::max(most, 64));
     c->spec_seq = 0;
     if (!c->h_serr) {
-      DM_HIP(c, hipHostMalloc((void**)&c->h_serr, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
+      DM_HIP(c, hipHostMalloc((void**)&c->h_serr, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
              "speculative chain");
       DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_serr, c->h_serr, 0), "speculative chain");
     }
     __atomic_store_n(c->h_serr, 0, __ATOMIC_RELAXED);
+    __atomic_store_n(c->h_serr + 1, 1, __ATOMIC_RELAXED);  // no redo seen yet: the full build first
   }
   DM_HIP(c, hipMemsetAsync(c->p_tot.p, 0, std::max<size_t>(c->h_large.size(), 1) * kSegTotBytes, st),
          "partials");  // SegTot::rel starts clear
@@ -845,6 +850,7 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* hw = getenv("DM_TPL_HOSTWAIT")) c->tpl_hostwait = atoi(hw) != 0;
   if (const char* sr = getenv("DM_SKIP_REST")) c->skip_rest = atoi(sr) != 0;
   if (const char* sc = getenv("DM_SPEC_CHAIN")) c->spec_chain = atoi(sc) != 0;
+  if (const char* rl = getenv("DM_REDO_LIGHT")) c->redo_light = atoi(rl);
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1348,13 +1354,17 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     // overwritten by the speculative gets: alternate output columns)
     const bool spec = c->spec_chain && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
     if (spec) {
-      const SpecArgs S{c->p_spec.p, c->spec_seq, c->d_serr, c->p_spec_ring.p, (int)(c->spec_seq & 1), nch};
+      const SpecArgs S{c->p_spec.p, c->spec_seq, c->d_serr, c->p_spec_ring.p, (int)(c->spec_seq & 1), nch,
+                       reinterpret_cast<uint32_t*>(c->d_serr + 1)};
       c->spec_seq += 1;
+      const bool light = c->redo_light == 2 || (c->redo_light == 1 && c->redo_epoch == c->row_epoch &&
+                                                __atomic_load_n(c->h_serr + 1, __ATOMIC_RELAXED) == 0);
+      c->redo_epoch = c->row_epoch;
       for (int ph = 0; ph < 2; ++ph)
         DM_HIP(c, timed(ph == 0 ? KC_LARGE_SPEC : KC_LARGE_REDO, s_large,
                         [&] {
-                          return launch_large_spec(ph, p, c->chunks.p, nch, c->large.p, P, S, c->redo_grid, gl, gc,
-                                                   s_large);
+                          return launch_large_spec(ph == 0 ? 0 : light ? 2 : 1, p, c->chunks.p, nch, c->large.p, P, S,
+                                                   c->redo_grid, gl, gc, s_large);
                         }),
                "large-resource kernels");
     }

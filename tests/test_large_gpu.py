@@ -257,7 +257,8 @@ def test_large_writeback_ticks_with_uniform_counts_other_than_one(cols):
         eng.close()
 
 
-def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch):
+@pytest.mark.parametrize("redo", ["1", "2"])
+def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     """The speculative chain (k_large_spec: one pass under the totals the resource's
     last tick verified, checked bit for bit per resource; k_large_redo for the
     resources whose totals moved) against the four-launch chain (DM_SPEC_CHAIN=0) and
@@ -267,7 +268,9 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch):
     followers lapsing, a non-writeback tick.  Leases match the oracle (SURVEY.md §8c);
     the two engines' stores hold the same released rows and subclients and running
     sums within the oracle tolerance (their reductions run in different orders); in
-    the steady ticks the speculative engine launches no pass of the chain."""
+    the steady ticks the speculative engine launches no pass of the chain.  redo:
+    DM_REDO_LIGHT (1: k_large_redo's light build after a redo-free tick, so the lapse
+    tick's redo runs on it; 2: the light build on every tick)."""
     from doorman_amd.engine import Engine
     rng = np.random.default_rng(8080)
     sizes = np.asarray([4097, 5000, 6000, 8192, 9000, 20000, 65537, 150000, 300, 17, 5], dtype=np.int64)
@@ -283,6 +286,7 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch):
     monkeypatch.setenv("DM_SPEC_CHAIN", "0")
     chain = Engine(0)
     monkeypatch.delenv("DM_SPEC_CHAIN")
+    monkeypatch.setenv("DM_REDO_LIGHT", redo)
     spec = Engine(0)
     try:
         chain.load(snap)

@@ -1,7 +1,10 @@
 """Large-resource class alone: per-kernel times of C2's resources > 4096 rows
 (or the whole C2 tick with --all) for library builds and large-path modes.
 
-  python tools/large_probe.py [--all] LIB.so[:chain] ...
+  python tools/large_probe.py [--all] [--redo] LIB.so[:chain] ...
+
+--redo: before every tick a wants refresh of each resource's first row (values
+alternate), so every speculated resource fails its check and takes the redo.
 """
 import argparse
 import os
@@ -23,6 +26,7 @@ def main():
     ap.add_argument("--small", action="store_true", help="only the resources of <= 4096 rows")
     ap.add_argument("--sizes", default=None, help="LO-HI: only resources with LO <= rows <= HI")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--redo", action="store_true", help="every tick redoes every large resource")
     args = ap.parse_args()
     snap = W.c2()
     if not args.all:
@@ -35,6 +39,17 @@ def main():
             keep = (sizes <= 4096) if args.small else (sizes > 4096)
         snap = W.subset(snap, np.flatnonzero(keep))
     n = len(snap["wants"])
+    import numpy as np
+    first = np.asarray(snap["seg_off"])[:-1][np.diff(np.asarray(snap["seg_off"])) > 0]
+    w_alt = [snap["wants"][first].copy(), snap["wants"][first] * 1.01 + 0.5]
+    it = [0]
+
+    def tick(e):
+        if args.redo:
+            it[0] += 1
+            e.update_wants(first, w_alt[it[0] & 1])
+        e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+
     for p in args.libs:
         p, _, envs = p.partition("@")  # LIB[:mode][@VAR=value,...]: environment for that engine
         for kv in filter(None, envs.split(",")):
@@ -51,7 +66,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+            tick(e)
         e.sync()
         dt = (time.perf_counter() - t0) / args.steps * 1e6
         kt = e.kernel_times()
@@ -59,7 +74,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            e.apportion(W.NOW_NS, writeback=True, asynchronous=True, defer_join=True)
+            tick(e)
         e.sync()
         dp = (time.perf_counter() - t0) / args.steps * 1e6
         e.close()
