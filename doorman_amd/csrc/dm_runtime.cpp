@@ -175,7 +175,7 @@ struct dm_ctx {
   // (hipStreamWaitValue64, >=).  An event wait idles the consuming queue ~12-20 us on
   // the box (tools/xs_probe.py); this ROCm runs the stream memory operations as blit
   // kernels (__amd_rocclr_streamOps*, 3-5 us each plus a dispatch gap,
-  // tools/gpu_c3trace.sh) and measured no cheaper per step.  Events by default;
+  // a rocprofv3 kernel trace of the C3 step) and measured no cheaper per step.  Events by default;
   // DM_XS_VALUES=1 every hop as values, DM_XS_READY_VALUE=1 only the staged templates'
   // hop.  A wait on a token signalled on the waiting stream itself is skipped (stream
   // order).
