@@ -78,8 +78,12 @@ def main(d, w):
             for row in csv.DictReader(fh):
                 rows.append(row)
                 c = cls(row["Name"])
-                if c:
-                    stats[c] = {"calls": int(row["Calls"]), "avg_us": float(row["AverageNs"]) / 1e3}
+                if c:  # several kernels of one class (e.g. k_large_redo's two builds): call-weighted
+                    n, tot = int(row["Calls"]), float(row["TotalDurationNs"]) / 1e3
+                    st = stats.setdefault(c, {"calls": 0, "total_us": 0.0})
+                    st["calls"] += n
+                    st["total_us"] += tot
+                    st["avg_us"] = st["total_us"] / st["calls"]
     if not rows:
         sys.exit(f"no kernel stats under {d}/trace: not overwriting profiles/")
     fetch = counters(os.path.join(d, "fetch"))
