@@ -26,8 +26,9 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 //   n <= 16 / 32              : 8- / 16-lane groups, 2 rows per lane, 8 / 4 resources per wave (bins 7, 8)
 //   n <= 64 / 128             : 16- / 32-lane groups, 4 rows per lane, 4 / 2 resources per wave (bins 0, 1)
 //   n <= 256                  : one wave per resource, 4 rows per lane (4 resources per workgroup)
-//   n <= 512 / 1024           : one 256-thread workgroup, R = 2, 4 rows per thread in VGPRs
-//   n <= 2048 / 4096          : one 512- / 1024-thread workgroup, 4 rows per thread
+//   n <= 512 / 1024           : one 128-thread workgroup, 4 / 8 rows per thread in VGPRs (bins 3, 4)
+//   n <= 2048                 : one 256-thread workgroup, 8 rows per thread (bin 5)
+//   n <= 4096                 : one 256 x 16 or 512 x 8 workgroup (bin 6, kBin6Wide below)
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
 constexpr int kSmallMax = 8;
 constexpr int kLargeMin = 4096;
