@@ -3067,6 +3067,16 @@ hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks,
   return hipGetLastError();
 }
 
+// Workgroups of k_large_redo's full build that one CU holds at once (its forward-progress
+// bound: a marked resource's chunks wait for one another, so a resource with more chunks
+// than the whole GPU holds redo workgroups would wait forever; dm_runtime.cpp keeps such
+// a store off the speculative chain).
+int redo_blocks_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_large_redo<false>, 256, 0) != hipSuccess) return 1;
+  return n > 0 ? n : 1;
+}
+
 hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_t* gcount, int blocks,
                           hipStream_t st) {
   if (blocks <= 0) return hipSuccess;

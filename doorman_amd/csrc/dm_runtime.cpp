@@ -27,6 +27,7 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
                             int32_t* glist, int32_t* gcount, int32_t* guard, hipStream_t st);
 hipError_t launch_tick_done(const TickDone& td, hipStream_t st);
+int redo_blocks_per_cu();
 hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
                              const Partials& P, const SpecArgs& S, int redo_grid, int32_t* glist, int32_t* gcount,
                              hipStream_t st);
@@ -355,6 +356,10 @@ struct dm_ctx {
   DBuf<SpecTot> p_spec;
   DBuf<uint32_t> p_spec_ring;  // SpecArgs::ring
   int redo_grid = 64;          // k_large_redo's workgroups: at least the largest resource's chunks
+  // k_large_redo's full build: workgroups the GPU holds at once (its forward-progress
+  // bound), and whether the loaded store's largest resource fits it (else no speculation)
+  int64_t redo_cap = 0;
+  bool spec_fits = true;
   uint64_t spec_seq = 0;
   int32_t* h_serr = nullptr;  // [0] the give-up flag, [1] SpecArgs::seen
   int32_t* d_serr = nullptr;
@@ -727,6 +732,7 @@ static int upload_plan(dm_ctx* c) {
     int most = 1;
     for (const LargeSeg& L : c->h_large) most = std::max(most, L.chunk_end - L.chunk_begin);
     c->redo_grid = std::min<int>(std::max<int>((int)c->h_chunks.size(), 1), std::max(most, 64));
+    c->spec_fits = most <= c->redo_cap;
     c->spec_seq = 0;
     if (!c->h_serr) {
       DM_HIP(c, hipHostMalloc((void**)&c->h_serr, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
@@ -877,6 +883,7 @@ int dm_create(int device, dm_ctx** out) {
   const bool cumask = !getenv("DM_CUMASK") || atoi(getenv("DM_CUMASK")) != 0;
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  c->redo_cap = (int64_t)std::max(ncu, 1) * redo_blocks_per_cu();
   const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
   std::vector<std::vector<uint32_t>> masks(dm_ctx::kAux, std::vector<uint32_t>(mwords, 0u));
   for (int i = 0; i < dm_ctx::kAux; ++i)
@@ -1237,7 +1244,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // The speculative large chain (below) writes its gets before they are verified, so a
   // tick that may take it writes the alternate column whatever the store's size.
   const bool spec_eligible = c->spec_chain && wb && !(flags & DM_AGG_RECOMPUTE) && !c->expl_rows &&
-                             !(c->maybe_general && c->n_nonsmall > 0) && !c->h_chunks.empty();
+                             !(c->maybe_general && c->n_nonsmall > 0) && !c->h_chunks.empty() && c->spec_fits;
   const bool pingpong = wb && !(flags & DM_WB_INPLACE) &&
                         ((flags & DM_WB_ALTERNATE) || c->N * 48 > kStreamBytes || spec_eligible);
   // A writeback tick writes no per-lease expiry: the leases it grants follow their
@@ -1352,7 +1359,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     // the steady state: one speculative launch, verified per resource, and a redo launch
     // that only the resources whose totals moved use (the store's rows must not be
     // overwritten by the speculative gets: alternate output columns)
-    const bool spec = c->spec_chain && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
+    const bool spec = c->spec_chain && c->spec_fits && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
     if (spec) {
       const SpecArgs S{c->p_spec.p, c->spec_seq, c->d_serr, c->p_spec_ring.p, (int)(c->spec_seq & 1), nch,
                        reinterpret_cast<uint32_t*>(c->d_serr + 1)};
@@ -2531,14 +2538,16 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[5 + kNumBins];
+  int64_t v[7 + kNumBins];
   v[0] = (int64_t)c->h_packs.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
   v[2 + kNumBins] = (int64_t)c->h_chunks.size();
   v[3 + kNumBins] = c->N;
   v[4 + kNumBins] = c->bin6_wide ? 1 : 0;  // bin 6 on 512 x 8 workgroups (else 256 x 16)
-  const int n = 5 + kNumBins;
+  v[5 + kNumBins] = c->redo_cap;          // chunks of one resource the speculative chain takes at most
+  v[6 + kNumBins] = c->spec_fits ? 1 : 0;  // the store's largest resource within it
+  const int n = 7 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }

@@ -347,3 +347,49 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     finally:
         chain.close()
         spec.close()
+
+
+def test_resource_beyond_the_redo_bound_takes_the_chain():
+    """The speculative chain's redo makes a marked resource's chunks wait for one
+    another, so it holds at most as many chunks as the GPU holds redo workgroups at
+    once (plan_info spec_max_chunks: CUs x workgroups per CU of k_large_redo's full
+    build).  A store whose largest resource has more chunks never speculates: its
+    writeback ticks (alternate columns, where the speculative chain would otherwise run)
+    take the four-launch chain and match the oracle; a store within the bound does
+    speculate."""
+    rng = np.random.default_rng(909)
+    probe = _engine()
+    try:
+        small = snapshot_with_sizes(rng, np.asarray([5000, 20], dtype=np.int64), kinds=(3,), expired_frac=0.0,
+                                    learning_frac=0.0, parent_expired_frac=0.0)
+        probe.load(small)
+        info = probe.plan_info()
+        assert info["spec_fits"] == 1
+        cap = info["spec_max_chunks"]
+    finally:
+        probe.close()
+    assert 64 <= cap <= 4096, cap
+    sizes = np.asarray([cap * 2048 + 1, 6000, 300, 17], dtype=np.int64)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(3, 2), expired_frac=0.0, learning_frac=0.0, parent_expired_frac=0.0)
+    snap["kind"][:2] = [W.FAIR_SHARE, W.PROPORTIONAL_SHARE]
+    snap["expiry_ns"] = np.full(len(snap["wants"]), NOW + 3600 * W.NS, np.int64)
+    eng = _engine()
+    try:
+        eng.load(snap)
+        assert eng.plan_info()["spec_fits"] == 0
+        eng.set_profiling(True)
+        now = NOW
+        for i in range(4):
+            now += 5 * W.NS
+            cur = _store_as_snapshot(snap, eng)
+            ref = O.apportion(cur, now)
+            eng.reset_kernel_times()
+            eng.apportion(now, writeback=True, wb_columns="alternate")
+            kt = eng.kernel_times()
+            assert "large_spec" not in kt and kt.get("large_a", (0, 0))[0] == 1, kt
+            st = eng.read_store()
+            live = ref["expiry_ns"] != W.RELEASED
+            gets = np.where(live, st["has"], 0.0)
+            assert float_close(gets, np.where(live, ref["gets"], 0.0), row_capacity(cur)).all(), f"tick {i}"
+    finally:
+        eng.close()
