@@ -356,8 +356,9 @@ struct dm_ctx {
   DBuf<SpecTot> p_spec;
   DBuf<uint32_t> p_spec_ring;  // SpecArgs::ring
   int redo_grid = 64;          // k_large_redo's workgroups: at least the largest resource's chunks
-  // k_large_redo's full build: workgroups the GPU holds at once (its forward-progress
-  // bound), and whether the loaded store's largest resource fits it (else no speculation)
+  // k_large_redo's full build: 3/4 of the workgroups the GPU holds at once (its
+  // forward-progress bound), and whether the loaded store's largest resource fits it
+  // (else no speculation)
   int64_t redo_cap = 0;
   bool spec_fits = true;
   uint64_t spec_seq = 0;
@@ -883,7 +884,10 @@ int dm_create(int device, dm_ctx** out) {
   const bool cumask = !getenv("DM_CUMASK") || atoi(getenv("DM_CUMASK")) != 0;
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-  c->redo_cap = (int64_t)std::max(ncu, 1) * redo_blocks_per_cu();
+  // a quarter of headroom: the other classes' streams hold slots too, and run ahead
+  // (DM_DEFER_JOIN).  C2's 489 chunks of 768 redo well; 978 of 1024 (1024-row chunks)
+  // waited out the spin bound
+  c->redo_cap = (int64_t)std::max(ncu, 1) * redo_blocks_per_cu() * 3 / 4;
   const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
   std::vector<std::vector<uint32_t>> masks(dm_ctx::kAux, std::vector<uint32_t>(mwords, 0u));
   for (int i = 0; i < dm_ctx::kAux; ++i)

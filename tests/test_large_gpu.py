@@ -352,8 +352,8 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
 def test_resource_beyond_the_redo_bound_takes_the_chain():
     """The speculative chain's redo makes a marked resource's chunks wait for one
     another, so it holds at most as many chunks as the GPU holds redo workgroups at
-    once (plan_info spec_max_chunks: CUs x workgroups per CU of k_large_redo's full
-    build).  A store whose largest resource has more chunks never speculates: its
+    once (plan_info spec_max_chunks: 3/4 of CUs x workgroups per CU of k_large_redo's
+    full build, the other classes' streams holding slots too).  A store whose largest resource has more chunks never speculates: its
     writeback ticks (alternate columns, where the speculative chain would otherwise run)
     take the four-launch chain and match the oracle; a store within the bound does
     speculate."""
