@@ -17,4 +17,4 @@ import json
 for n in ('c2', 'default'):
     d = json.loads(open('$OUT/bench_%s.json' % n).read().strip().splitlines()[-1])
     print(n, d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'])"
-[ "${PROFILE:-1}" = 1 ] && WORKLOAD=c2 bash tools/gpu_profile.sh
+if [ "${PROFILE:-1}" = 1 ]; then WORKLOAD=c2 bash tools/gpu_profile.sh; fi
