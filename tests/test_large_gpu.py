@@ -393,3 +393,61 @@ def test_resource_beyond_the_redo_bound_takes_the_chain():
             assert float_close(gets, np.where(live, ref["gets"], 0.0), row_capacity(cur)).all(), f"tick {i}"
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("redo", ["1", "2"])
+def test_back_to_back_async_ticks_against_the_oracle(monkeypatch, redo):
+    """What bench.py runs: writeback ticks issued back to back with DM_ASYNC |
+    DM_DEFER_JOIN (the class streams join lazily; k_large_redo's build is chosen from a
+    host-mapped word the GPU writes ticks behind the host), nothing read in between.
+    Segments of such ticks include one where followers lapse (the speculation fails
+    without any host call, so the redo runs on the build the heuristic picked), and a
+    wants refresh between segments.  After each segment the store equals the oracle's
+    ticks applied in order on a host copy."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(6060)
+    sizes = np.asarray([4097, 6000, 8192, 20000, 65537, 9000, 300, 17, 5], dtype=np.int64)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(2, 3), expired_frac=0.0, learning_frac=0.0,
+                               parent_expired_frac=0.0)
+    snap["kind"][:6] = [3, 2, 3, 3, 2, 3]
+    snap["lease_length_s"][:6] = [600, 30, 600, 25, 600, 600]  # resources 1 and 3 lapse in the long gap
+    snap["expiry_ns"] = np.full(len(snap["wants"]), NOW + 3600 * W.NS, np.int64)
+    W.add_store_sums(snap)
+    so = np.asarray(snap["seg_off"])
+    monkeypatch.setenv("DM_REDO_LIGHT", redo)
+    eng = Engine(0)
+    try:
+        eng.load(snap)
+        eng.set_profiling(True)
+        host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+        now = NOW
+        segments = [[1, 1, 1], [1, 1, 1, 1], [40, 1, 1], [1, 1]]
+        for si, seg in enumerate(segments):
+            if si == 3:  # a wants refresh of part of resources 0 and 4 (a synchronous call between segments)
+                rows = np.concatenate([np.arange(so[0], so[0] + 900), np.arange(so[4], so[4] + 3000)]).astype(np.int64)
+                w = rng.uniform(0.0, 3.0, len(rows)) * np.repeat(snap["capacity"], np.diff(so))[rows] / 1000.0
+                eng.update_wants(rows, w)
+                live = host["expiry_ns"][rows] != W.RELEASED
+                host["wants"][rows] = np.where(live, w, host["wants"][rows])
+                W.add_store_sums(host)
+            for dt in seg:
+                now += dt * W.NS
+                eng.apportion(now, writeback=True, asynchronous=True, defer_join=True, wb_columns="alternate")
+                ref = O.apportion(host, now)
+                live = ref["expiry_ns"] != W.RELEASED
+                host["has"] = np.where(live, ref["gets"], 0.0)
+                host["wants"] = np.where(live, host["wants"], 0.0)
+                host["subclients"] = np.where(live, host["subclients"], 0)
+                host["expiry_ns"] = ref["expiry_ns"].copy()
+                W.add_store_sums(host)
+            eng.sync()
+            st = eng.read_store()
+            np.testing.assert_array_equal(st["expiry_ns"], host["expiry_ns"], err_msg=f"segment {si}")
+            np.testing.assert_array_equal(st["subclients"], host["subclients"], err_msg=f"segment {si}")
+            assert float_close(st["has"], host["has"], row_capacity(host)).all(), f"segment {si}"
+            res = eng.resources(safe=False)
+            np.testing.assert_array_equal(res["count"], host["agg_count"], err_msg=f"segment {si}")
+        kt = eng.kernel_times()
+        assert kt.get("large_spec", (0, 0))[0] >= 8 and kt.get("large_redo", (0, 0))[0] >= 8, kt
+    finally:
+        eng.close()
