@@ -169,7 +169,10 @@ struct SpecArgs {
   int par;          // this tick's parity (the redo clears the other slots for the next tick)
   int nchunks;
   uint32_t* seen;   // host-mapped: whether the last redo launch found a resource marked
+  const int32_t* team;  // k_large_redo_team: per team slot, (large resource) << 8 | member
+  int nslots;           // team slots: min(chunks, kTeamMax) per large resource
 };
+constexpr int kTeamMax = 64;  // workgroups that redo one large resource together
 constexpr int kHetMaxS = 256;                    // distinct subclient counts per resource on the chain
 constexpr int kHetBuckets = 2 * kHetMaxS + 1;    // strictly between / equal to the sorted thresholds
 struct HetRes {

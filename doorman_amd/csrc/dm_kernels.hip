@@ -1619,6 +1619,156 @@ __global__ __launch_bounds__(256, kLight ? 8 : 1) void k_large_redo(DevParams p,
   }
 }
 
+// The redo by teams: a marked resource's chunks are shared among W = min(chunks,
+// kTeamMax) workgroups (its team slots, in ticket order), each taking every W-th chunk
+// through each phase, its rows loaded again per phase.  The chunk partials and the
+// canonical trees are the per-chunk ones of redo_chunk (the same bits); only a team
+// waits for itself, so any grid of >= kTeamMax co-resident workgroups finishes (no
+// bound on a resource's chunks), and a steady tick's empty launch is a small grid.
+__device__ __forceinline__ void redo_team(const DevParams& p, const Chunk* __restrict__ chunks,
+                                          const LargeSeg* __restrict__ ls, const Partials& P, const SpecArgs& S,
+                                          int32_t* glist, int32_t* gcount, int l, int m, Lds<256>& lds,
+                                          int* s_last_p) {
+  int& s_last = *s_last_p;
+  const int t = threadIdx.x;
+  SpecTot* sp = S.tot + l;
+  const LargeSeg L = ls[l];
+  const int nch = L.chunk_end - L.chunk_begin;
+  const int W = nch < kTeamMax ? nch : kTeamMax;
+  AggA at = zeroA();
+  at.cnt = sp->a_cnt;
+  at.h = sp->a_h;
+  at.w = sp->a_w;
+  at.smin = sp->a_smin;
+  at.smax = sp->a_smax;
+  at.nan = sp->a_nan;
+  const SegState st = uniform(seg_state_of(p, L.seg, at));
+  const Res rs = st.rs;
+  if (st.general) {  // k_general decides it (its member 0 lists it)
+    for (int c = L.chunk_begin + m; c < L.chunk_end; c += W)
+      if (t == 0) P.uni[c] = -1;
+    if (t == 0 && m == 0) {
+      glist[atomicAdd(gcount, 1)] = L.seg;
+      sp->redo = 0;
+      sp->valid = 0;
+    }
+    return;
+  }
+  const bool r1 = !rs.learning && rs.kind >= 2;
+  const bool fs = !rs.learning && rs.kind == 3;
+  const double eq = rs.C / (double)st.cl.count;
+  AggB bt{sp->abx, sp->aby, sp->abi};  // round 1 at the running Count: exact when Clean released nothing
+  if (r1 && at.cnt != 0) {  // round 1 again at the Count after Clean
+    for (int c = L.chunk_begin + m; c < L.chunk_end; c += W) {
+      ChunkRows rw;
+      load_chunk<true>(p, chunks[c], rw, rs);
+      const AggB x = group_reduce_t0<256>(chunk_b(rw, rs.kind, eq), OpB(), lds.b);
+      if (t == 0) {
+        st_wt(P.b_x + c, x.x);
+        st_wt(P.b_y + c, x.y);
+        st_wt(P.b_w + c, (int64_t)x.i);
+      }
+      __syncthreads();
+    }
+    if (spec_arrive(&sp->arrive[1], W, &s_last)) {
+      if (t < 64) {
+        const AggB r = canon_b(P, L);
+        if (t == 0) {
+          st_wt(&sp->abx, r.x);
+          st_wt(&sp->aby, r.y);
+          st_wt(reinterpret_cast<int64_t*>(&sp->abi), (int64_t)r.i);
+        }
+      }
+      spec_ready(S, &sp->ready[0]);
+    }
+    spec_wait(S, &sp->ready[0]);
+    bt = AggB{ld_wt(&sp->abx), ld_wt(&sp->aby), ld_wt(reinterpret_cast<const int64_t*>(&sp->abi))};
+  }
+  const int s0 = st.a.smin;
+  AggC ct{0.0, 0};
+  FsU fu = make_fsu(eq, s0, bt.x, bt.i, ct);
+  if (fs) {  // round 2 at the resource's threshold
+    for (int c = L.chunk_begin + m; c < L.chunk_end; c += W) {
+      ChunkRows rw;
+      load_chunk<true>(p, chunks[c], rw, rs);
+      const AggC x = group_reduce_t0<256>(chunk_c(rw, s0, eq, fu.T), OpC(), lds.c);
+      if (t == 0) {
+        st_wt(P.c_ee + c, x.ee);
+        st_wt(P.c_sgt + c, (int64_t)x.sgt);
+      }
+      __syncthreads();
+    }
+    if (spec_arrive(&sp->arrive[2], W, &s_last)) {
+      if (t < 64) {
+        const AggC r = canon_c(P, L);
+        if (t == 0) {
+          st_wt(&sp->cee, r.ee);
+          st_wt(reinterpret_cast<int64_t*>(&sp->csgt), (int64_t)r.sgt);
+        }
+      }
+      spec_ready(S, &sp->ready[1]);
+    }
+    spec_wait(S, &sp->ready[1]);
+    ct = AggC{ld_wt(&sp->cee), ld_wt(reinterpret_cast<const int64_t*>(&sp->csgt))};
+    fu = make_fsu(eq, s0, bt.x, bt.i, ct);
+  }
+  for (int c = L.chunk_begin + m; c < L.chunk_end; c += W) {
+    ChunkRows rw;
+    const Chunk ch = chunks[c];
+    load_chunk<true>(p, ch, rw, rs);
+    SumD delta{map_chunk(p, ch, rw, rs, st.cl, uniform(bt), uniform(fu))};
+    delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
+    if (t == 0) {
+      P.uni[c] = st.a.smin == st.a.smax ? st.a.smin : -1;
+      st_wt(P.d_delta + c, delta.v);
+    }
+    __syncthreads();
+  }
+  if (!spec_arrive(&sp->arrive[0], W, &s_last)) return;
+  if (t >= 64) return;
+  const double d = canon_d(P, L);
+  if (t == 0) {
+    write_resource(p, L.seg, rs, st.cl, d);
+    // the next tick's speculation: this tick's totals (round 1 and 2 as the chunks used
+    // them; a resource whose live rows hold mixed counts is not speculated on)
+    sp->bx = bt.x;
+    sp->by = bt.y;
+    sp->bi = bt.i;
+    sp->cee = ct.ee;
+    sp->csgt = ct.sgt;
+    sp->s0 = s0;
+    sp->valid = (st.a.smin >= st.a.smax) ? 1 : 0;  // one count, or no live row
+    sp->redo = 0;
+  }
+}
+
+// Team slots in ticket order (a resource's slots consecutive): with a grid of >=
+// kTeamMax workgroups only the team at the ticket front can have members not yet taken
+template <bool kLight>
+__global__ __launch_bounds__(256, kLight ? 8 : 1) void k_large_redo_team(DevParams p, const Chunk* __restrict__ chunks,
+                                                                          const LargeSeg* __restrict__ ls, Partials P,
+                                                                          SpecArgs S, int32_t* glist, int32_t* gcount) {
+  __shared__ Lds<256> lds;
+  __shared__ int s_last, s_c;
+  const int q = S.par ^ 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next tick's slots (its k_large_spec runs after this)
+    S.ring[q] = 0;
+    S.ring[2 + q] = 0;
+    __hip_atomic_store(S.seen, S.ring[S.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (!S.ring[S.par]) return;  // nothing marked (k_large_spec: the previous launch)
+  for (;;) {
+    if (threadIdx.x == 0) s_c = (int)atomicAdd(S.ring + 2 + S.par, 1u);
+    __syncthreads();
+    const int k = s_c;
+    if (k >= S.nslots) return;
+    const int32_t tm = S.team[k];
+    const int l = tm >> 8, m = tm & 0xFF;
+    if (S.tot[l].redo) redo_team(p, chunks, ls, P, S, glist, gcount, l, m, lds, &s_last);
+    __syncthreads();  // every wave back before the next ticket
+  }
+}
+
 __global__ __launch_bounds__(256) void k_large_fin(DevParams p, const LargeSeg* __restrict__ ls, Partials P,
                                                    int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<256> lds;
@@ -3062,8 +3212,12 @@ hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks,
     k_large_spec<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, S);
   else if (phase == 1)
     k_large_redo<false><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
-  else
+  else if (phase == 2)
     k_large_redo<true><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
+  else if (phase == 3)
+    k_large_redo_team<false><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
+  else
+    k_large_redo_team<true><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
   return hipGetLastError();
 }
 

@@ -361,6 +361,11 @@ struct dm_ctx {
   // (else no speculation)
   int64_t redo_cap = 0;
   bool spec_fits = true;
+  // the redo by teams (k_large_redo_team; DM_REDO_TEAM=0: k_large_redo, one workgroup
+  // per chunk, bounded by redo_cap): team slots and the two builds' grids
+  bool redo_team = true;
+  DBuf<int32_t> p_team;
+  int nslots = 0, team_grid_full = 1, team_grid_light = 1;
   uint64_t spec_seq = 0;
   int32_t* h_serr = nullptr;  // [0] the give-up flag, [1] SpecArgs::seen
   int32_t* d_serr = nullptr;
@@ -534,7 +539,7 @@ struct dm_ctx {
     h_guard = d_guard = nullptr;
     pa_cnt.release(); pa_cnt_all.release(); pa_has_all.release(); pa_wants_all.release(); pa_smin.release(); pa_smax.release(); pb_w.release(); pc_sgt.release();
     pa_has.release(); pa_wants.release(); pb_x.release(); pb_y.release(); pc_ee.release(); pd_delta.release();
-    pa_nan.release(); pa_live.release(); p_tot.release(); p_uni.release(); p_spec.release(); p_spec_ring.release();
+    pa_nan.release(); pa_live.release(); p_tot.release(); p_uni.release(); p_spec.release(); p_spec_ring.release(); p_team.release();
     if (h_serr) (void)hipHostFree(h_serr);
     h_serr = d_serr = nullptr;
     ph_set.release(); ph_n.release(); ph_bkc.release(); ph_het.release(); ph_bkw.release(); ph_bks.release();
@@ -733,7 +738,18 @@ static int upload_plan(dm_ctx* c) {
     int most = 1;
     for (const LargeSeg& L : c->h_large) most = std::max(most, L.chunk_end - L.chunk_begin);
     c->redo_grid = std::min<int>(std::max<int>((int)c->h_chunks.size(), 1), std::max(most, 64));
-    c->spec_fits = most <= c->redo_cap;
+    c->spec_fits = c->redo_team || most <= c->redo_cap;
+    std::vector<int32_t> team;
+    for (size_t l = 0; l < c->h_large.size(); ++l) {
+      const int nch_l = c->h_large[l].chunk_end - c->h_large[l].chunk_begin;
+      for (int m = 0; m < std::min(nch_l, kTeamMax); ++m) team.push_back((int32_t)(l << 8 | (size_t)m));
+    }
+    c->nslots = (int)team.size();
+    DM_HIP(c, upload(c->p_team, team.data(), team.size(), st), "redo teams");
+    // every team's members can be resident at once: >= kTeamMax workgroups (the full
+    // build: up to what the GPU holds; the light one: a steady tick's launch is all it costs)
+    c->team_grid_full = std::max(1, (int)std::min<int64_t>(c->nslots, std::max<int64_t>(kTeamMax, c->redo_cap)));
+    c->team_grid_light = std::max(1, std::min(c->nslots, kTeamMax));
     c->spec_seq = 0;
     if (!c->h_serr) {
       DM_HIP(c, hipHostMalloc((void**)&c->h_serr, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
@@ -858,6 +874,7 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* sr = getenv("DM_SKIP_REST")) c->skip_rest = atoi(sr) != 0;
   if (const char* sc = getenv("DM_SPEC_CHAIN")) c->spec_chain = atoi(sc) != 0;
   if (const char* rl = getenv("DM_REDO_LIGHT")) c->redo_light = atoi(rl);
+  if (const char* rt = getenv("DM_REDO_TEAM")) c->redo_team = atoi(rt) != 0;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1366,16 +1383,18 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     const bool spec = c->spec_chain && c->spec_fits && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
     if (spec) {
       const SpecArgs S{c->p_spec.p, c->spec_seq, c->d_serr, c->p_spec_ring.p, (int)(c->spec_seq & 1), nch,
-                       reinterpret_cast<uint32_t*>(c->d_serr + 1)};
+                       reinterpret_cast<uint32_t*>(c->d_serr + 1), c->p_team.p, c->nslots};
       c->spec_seq += 1;
       const bool light = c->redo_light == 2 || (c->redo_light == 1 && c->redo_epoch == c->row_epoch &&
                                                 __atomic_load_n(c->h_serr + 1, __ATOMIC_RELAXED) == 0);
       c->redo_epoch = c->row_epoch;
+      const int redo_phase = c->redo_team ? (light ? 4 : 3) : (light ? 2 : 1);
+      const int redo_grid = c->redo_team ? (light ? c->team_grid_light : c->team_grid_full) : c->redo_grid;
       for (int ph = 0; ph < 2; ++ph)
         DM_HIP(c, timed(ph == 0 ? KC_LARGE_SPEC : KC_LARGE_REDO, s_large,
                         [&] {
-                          return launch_large_spec(ph == 0 ? 0 : light ? 2 : 1, p, c->chunks.p, nch, c->large.p, P, S,
-                                                   c->redo_grid, gl, gc, s_large);
+                          return launch_large_spec(ph == 0 ? 0 : redo_phase, p, c->chunks.p, nch, c->large.p, P, S,
+                                                   redo_grid, gl, gc, s_large);
                         }),
                "large-resource kernels");
     }

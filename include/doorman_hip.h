@@ -369,9 +369,10 @@ int dm_reset_kernel_times(dm_ctx* ctx);
  * sub32x4, wave64x4, block128x4, block128x8, block256x8, the 2049-4096-row bin,
  * sub8x2, sub16x2), large resources, large chunks, leases, then 1 when the
  * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), the most chunks
- * (2048 rows each) one resource may have for the speculative chain (the redo
- * kernel's co-resident workgroups), and 1 when the store's largest resource is
- * within it (else every tick takes the four-launch chain); returns 16 */
+ * (2048 rows each) one resource may have for the speculative chain with
+ * DM_REDO_TEAM=0 (the per-chunk redo kernel's co-resident workgroups), and 1 when
+ * the store may speculate (always with the default redo by teams; else only with
+ * its largest resource within that bound); returns 16 */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),

@@ -257,7 +257,7 @@ def test_large_writeback_ticks_with_uniform_counts_other_than_one(cols):
         eng.close()
 
 
-@pytest.mark.parametrize("redo", ["1", "2"])
+@pytest.mark.parametrize("redo", ["1", "2", "team0"])
 def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     """The speculative chain (k_large_spec: one pass under the totals the resource's
     last tick verified, checked bit for bit per resource; k_large_redo for the
@@ -286,6 +286,9 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     monkeypatch.setenv("DM_SPEC_CHAIN", "0")
     chain = Engine(0)
     monkeypatch.delenv("DM_SPEC_CHAIN")
+    if redo == "team0":  # k_large_redo (one workgroup per chunk) instead of the teams
+        monkeypatch.setenv("DM_REDO_TEAM", "0")
+        redo = "1"
     monkeypatch.setenv("DM_REDO_LIGHT", redo)
     spec = Engine(0)
     try:
@@ -349,14 +352,19 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
         spec.close()
 
 
-def test_resource_beyond_the_redo_bound_takes_the_chain():
-    """The speculative chain's redo makes a marked resource's chunks wait for one
-    another, so it holds at most as many chunks as the GPU holds redo workgroups at
-    once (plan_info spec_max_chunks: 3/4 of CUs x workgroups per CU of k_large_redo's
-    full build, the other classes' streams holding slots too).  A store whose largest resource has more chunks never speculates: its
-    writeback ticks (alternate columns, where the speculative chain would otherwise run)
-    take the four-launch chain and match the oracle; a store within the bound does
-    speculate."""
+@pytest.mark.parametrize("team", ["0", "1"])
+def test_resource_beyond_the_redo_bound(monkeypatch, team):
+    """team = 0 (DM_REDO_TEAM=0, k_large_redo: one workgroup per chunk, all of a marked
+    resource's chunks waiting for one another): the redo holds at most as many chunks
+    as the GPU holds its workgroups at once (plan_info spec_max_chunks: 3/4 of CUs x
+    workgroups per CU of its full build, the other classes' streams holding slots too).
+    A store whose largest resource has more chunks never speculates: its writeback
+    ticks (alternate columns, where the speculative chain would otherwise run) take the
+    four-launch chain and match the oracle.  team = 1 (the default, k_large_redo_team:
+    at most kTeamMax workgroups per resource): no bound, the same store speculates, a
+    wants refresh makes the big resource's redo run, and every tick matches the
+    oracle."""
+    monkeypatch.setenv("DM_REDO_TEAM", team)
     rng = np.random.default_rng(909)
     probe = _engine()
     try:
@@ -376,17 +384,24 @@ def test_resource_beyond_the_redo_bound_takes_the_chain():
     eng = _engine()
     try:
         eng.load(snap)
-        assert eng.plan_info()["spec_fits"] == 0
+        assert eng.plan_info()["spec_fits"] == (0 if team == "0" else 1)
         eng.set_profiling(True)
         now = NOW
-        for i in range(4):
+        so = np.asarray(snap["seg_off"])
+        for i in range(6):
             now += 5 * W.NS
+            if i == 4:  # part of the big resource's wants: its speculation fails, the redo runs
+                rows = np.arange(so[0], so[0] + 5000, dtype=np.int64)
+                eng.update_wants(rows, rng.uniform(0.0, 2.0, len(rows)))
             cur = _store_as_snapshot(snap, eng)
             ref = O.apportion(cur, now)
             eng.reset_kernel_times()
             eng.apportion(now, writeback=True, wb_columns="alternate")
             kt = eng.kernel_times()
-            assert "large_spec" not in kt and kt.get("large_a", (0, 0))[0] == 1, kt
+            if team == "0":
+                assert "large_spec" not in kt and kt.get("large_a", (0, 0))[0] == 1, kt
+            elif i >= 1:
+                assert kt.get("large_spec", (0, 0))[0] == 1, kt
             st = eng.read_store()
             live = ref["expiry_ns"] != W.RELEASED
             gets = np.where(live, st["has"], 0.0)
