@@ -22,7 +22,7 @@ CLASS = [
     (r"k_block_dense<256, 16>", "block2k4k_dense"),
     (r"k_publish\b", "hier_publish"), (r"k_hier_tick\b", "hier_root"),
     (r"k_tick_done\b", "tick_done"), (r"k_count_undense\b", "count_undense"),
-    (r"k_large_spec\b", "large_spec"), (r"k_large_redo\b", "large_redo"),
+    (r"k_large_spec\b", "large_spec"), (r"k_large_redo(_team)?\b", "large_redo"),
     (r"k_block_rest<128, 4>", "block128x4_rest"), (r"k_block_rest<128, 8>", "block128x8_rest"),
     (r"k_block_rest<256, 8>", "block256x8_rest"), (r"k_block_rest<512, 8>", "block2k4k_rest"),
     (r"k_block_rest<256, 16>", "block2k4k_rest"),
