@@ -621,6 +621,7 @@ static void build_plan(dm_ctx* c) {
   const std::vector<int64_t>& off = c->h_seg_off;
   Pack cur{};
   bool open = false;
+  std::vector<int64_t> large;
   auto close = [&]() {
     if (open) c->h_packs.push_back(cur);
     open = false;
@@ -646,16 +647,25 @@ static void build_plan(dm_ctx* c) {
     if (n <= kLargeMin) {
       c->h_bins[bin_of(n)].push_back(WorkItem{(int32_t)r, (int32_t)n, off[r]});
     } else {
-      LargeSeg L{(int32_t)r, (int32_t)c->h_chunks.size(), 0, 0};
-      for (int64_t o = off[r]; o < off[r + 1]; o += kChunkRows) {
-        Chunk ch{(int32_t)r, (int32_t)c->h_large.size(), o, (int32_t)std::min<int64_t>(kChunkRows, off[r + 1] - o), 0};
-        c->h_chunks.push_back(ch);
-      }
-      L.chunk_end = (int32_t)c->h_chunks.size();
-      c->h_large.push_back(L);
+      large.push_back(r);
     }
   }
   close();
+  // Large resources largest first: a resource is verified by its last-arriving chunk,
+  // and the largest's verification (the longest canonical trees) then overlaps the
+  // other chunks instead of trailing the launch.  Each resource's chunks stay
+  // consecutive and in row order (the canonical trees' order).
+  std::stable_sort(large.begin(), large.end(),
+                   [&](int64_t a, int64_t b) { return off[a + 1] - off[a] > off[b + 1] - off[b]; });
+  for (const int64_t r : large) {
+    LargeSeg L{(int32_t)r, (int32_t)c->h_chunks.size(), 0, 0};
+    for (int64_t o = off[r]; o < off[r + 1]; o += kChunkRows) {
+      Chunk ch{(int32_t)r, (int32_t)c->h_large.size(), o, (int32_t)std::min<int64_t>(kChunkRows, off[r + 1] - o), 0};
+      c->h_chunks.push_back(ch);
+    }
+    L.chunk_end = (int32_t)c->h_chunks.size();
+    c->h_large.push_back(L);
+  }
 }
 
 // Once per row epoch, after a writeback tick of workgroup bin b (split bin i): count
