@@ -1290,6 +1290,38 @@ __device__ __forceinline__ double canon_d(const Partials& P, const LargeSeg& L) 
   return canon_reduce(L.chunk_begin, L.chunk_end, SumD{0.0}, OpSumD(),
                       [&](int q) { return SumD{ld_wt(P.d_delta + q)}; }).v;
 }
+// canon_a, canon_b, canon_c and canon_d in one pass over the chunks (k_large_spec's
+// verifier): every partial of a 64-chunk stripe loaded at once, one round trip per
+// stripe instead of four; each quantity keeps its own order and tree (the same bits)
+struct CanonAll {
+  AggA a;
+  AggB b;
+  AggC c;
+  double d;
+};
+__device__ __forceinline__ CanonAll canon_all(const Partials& P, const LargeSeg& L) {
+  AggA a = zeroA();
+  AggB b{0.0, 0.0, 0};
+  AggC c{0.0, 0};
+  SumD d{0.0};
+  for (int q = L.chunk_begin + (int)(threadIdx.x & 63); q < L.chunk_end; q += 64) {
+    AggA x = zeroA();
+    x.cnt = ld_wt(P.a_cnt + q);
+    x.h = ld_wt(P.a_has + q);
+    x.w = ld_wt(P.a_wants + q);
+    x.smin = (int)ld_wt(P.a_smin + q);
+    x.smax = (int)ld_wt(P.a_smax + q);
+    x.nan = ld_wt(P.a_nan + q);
+    const AggB y{ld_wt(P.b_x + q), ld_wt(P.b_y + q), ld_wt(P.b_w + q)};
+    const AggC z{ld_wt(P.c_ee + q), ld_wt(P.c_sgt + q)};
+    const SumD u{ld_wt(P.d_delta + q)};
+    a = OpA()(a, x);
+    b = OpB()(b, y);
+    c = OpC()(c, z);
+    d = OpSumD()(d, u);
+  }
+  return CanonAll{wave_reduce(a, OpA()), wave_reduce(b, OpB()), wave_reduce(c, OpC()), wave_reduce(d, OpSumD()).v};
+}
 
 // pass A (Clean sums of the rows it releases, the live rows' count range, NaN wants)
 // and round 1 with equalShare eq over the chunk's rows in registers (as k_large_a)
@@ -1412,9 +1444,10 @@ __global__ __launch_bounds__(256) void k_large_spec(DevParams p, const Chunk* __
   if (t >= 64) return;  // wave 0 verifies (dm_kernel_util.h arrive_last)
   const LargeSeg L = ls[ch.lseg];
   if (!arrive_last(&sp->arrive[0], L.chunk_end - L.chunk_begin)) return;
-  const AggA at = canon_a(P, L);
-  const AggB bt = canon_b(P, L);
-  const AggC ct = canon_c(P, L);
+  const CanonAll ca = canon_all(P, L);
+  const AggA at = ca.a;
+  const AggB bt = ca.b;
+  const AggC ct = ca.c;
   const bool marked = __hip_atomic_load((gu32*)&sp->redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   bool same = valid && !marked && at.cnt == 0 && dbl_pos0(at.h) && dbl_pos0(at.w) && !at.nan &&
               (at.smin > at.smax || (at.smin == s0 && at.smax == s0));
@@ -1425,7 +1458,7 @@ __global__ __launch_bounds__(256) void k_large_spec(DevParams p, const Chunk* __
     same = same && __double_as_longlong(bt.x) == __double_as_longlong(bs.x) && bt.i == bs.i &&
            __double_as_longlong(ct.ee) == __double_as_longlong(cs.ee) && ct.sgt == cs.sgt;
   if (same) {
-    const double d = canon_d(P, L);
+    const double d = ca.d;
     if (t == 0) {
       AggA z = zeroA();
       z.smin = z.smax = s0;
