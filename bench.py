@@ -113,34 +113,67 @@ def algorithmic_bytes(n_leases: int, n_resources: int, dense_leases: float = 0) 
 
 def dense_fraction(eng, snap) -> float:
     """Share of the rows of resources with 257..4096 rows (the workgroup kernels,
-    the only ones that keep the dense state) that sit in dense resources."""
+    the only ones that keep the dense state) that sit in dense resources, in the
+    store's state right now (dm_store_stats)."""
     sizes = np.diff(snap["seg_off"])
     group = int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
     return eng.store_stats()["dense_leases"] / group if group else 0.0
 
 
+_SUB_EDGES = [("sub8x2", 9, 16), ("sub16x2", 17, 32), ("sub16x4", 33, 64), ("sub32x4", 65, 128),
+              ("wave64x4", 129, 256)]
+_GROUP_EDGES = [("block128x4", 257, 512), ("block128x8", 513, 1024), ("block256x8", 1025, 2048),
+                ("block2k4k", 2049, 4096)]
+# the kernel classes that read 24 B per lease of a dense resource (no subclients column):
+# the 128-thread mixed kernels (they load by the hint) and every dense kernel of the split form
+DENSE_READERS = ("block128x4", "block128x8") + tuple(n + "_dense" for n, _, _ in _GROUP_EDGES)
+
+
 def kernel_units(snap):
-    """(leases, resources) each kernel class of the plan processes per launch."""
+    """(leases, resources) each kernel class that dm_kernel_times can report processes
+    per launch (tests/test_bench_model.py checks the names against the library's).
+    Classes that move no lease rows of their own carry (0, resources) or (0, 0)."""
     sizes = np.diff(snap["seg_off"])
+    R = len(sizes)
     units = {}
-    edges = [("sub8x2", 9, 16), ("sub16x2", 17, 32), ("sub16x4", 33, 64), ("sub32x4", 65, 128),
-             ("wave64x4", 129, 256), ("block128x4", 257, 512), ("block128x8", 513, 1024), ("block256x8", 1025, 2048),
-             ("block2k4k", 2049, 4096)]
+
+    def rng(lo, hi):
+        m = (sizes >= lo) & (sizes <= hi)
+        return int(sizes[m].sum()), int(m.sum())
     small = sizes <= 8
     units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
-    for name, lo, hi in edges:
-        m = (sizes >= lo) & (sizes <= hi)
-        units[name] = (int(sizes[m].sum()), int(m.sum()))
-    m = (sizes >= 9) & (sizes <= 256)  # the sub-wave bins in one launch (k_subs)
-    units["subs_merged"] = (int(sizes[m].sum()), int(m.sum()))
-    big = sizes > 4096
-    for name in ("large_a", "large_b", "large_c", "large_map", "large_fin", "general"):
-        units[name] = (int(sizes[big].sum()), int(big.sum()))
-    for b in ("block128x4", "block128x8", "block256x8", "block2k4k"):  # the split form's two kernels
-        units[b + "_dense"] = units[b]
-        units[b + "_rest"] = (0, 0)  # only what the dense kernel queued; counted with the dense kernel
-    units["hier_publish"] = (0, len(sizes))
+    for name, lo, hi in _SUB_EDGES + _GROUP_EDGES:
+        units[name] = rng(lo, hi)
+    units["subs_merged"] = rng(9, 256)  # the sub-wave bins in one launch (k_subs)
+    for name, _, _ in _GROUP_EDGES:  # the split form's two kernels
+        units[name + "_dense"] = units[name]
+        units[name + "_rest"] = (0, 0)  # only what the dense kernel queued; counted with the dense kernel
+    big = rng(4097, 1 << 62)
+    # the chain's launches, the speculative chain (one pass over every large lease), the
+    # heterogeneous chain's launches: each over every row of the > 4096-row class
+    for name in ("large_a", "large_b", "large_c", "large_map", "large_fin", "large_spec", "large_t",
+                 "large_c_het", "large_e", "large_map_het"):
+        units[name] = big
+    # the redo rewrites only the resources whose speculation failed (none in a steady tick:
+    # its launch then reads one word per workgroup)
+    units["large_redo"] = (0, 0)
+    units["general"] = rng(9, 1 << 62)  # heterogeneous FairShare: any resource above 8 rows may land there
+    units["hier_publish"] = (0, R)
+    units["hier_root"] = (0, R)
+    units["hier_gather"] = (0, 0)  # 16 B per resource per server: a collective, not HBM streaming
+    units["store_upsert"] = units["store_release"] = units["decide"] = (0, 0)  # not on a tick
     return units
+
+
+def kernel_lease_bytes(name, leases_k, dense_frac):
+    """Algorithmic bytes per launch of one kernel class, split as (28-B leases, 24-B leases).
+    large_spec: a steady writeback tick through the chain reads no subclients column
+    (the last tick's live bits and per-chunk counts): 24 B per lease."""
+    if name == "large_spec":
+        return leases_k
+    if name in DENSE_READERS:
+        return dense_frac * leases_k
+    return 0.0
 
 
 def streaming_step(eng, snap, rank, n_ticks):
@@ -186,11 +219,15 @@ def streaming_step(eng, snap, rank, n_ticks):
         batches.append((*pinned, now))
     it = iter(batches)
 
-    def step():
+    def apply_only():
         mask, w, gone, new, nw, ns, t = next(it)
         eng.apply(mask, w, gone, (new, None, nw, ns, None), now_ns=t)  # the round's three update kinds, one call
-        eng.apportion(t, writeback=True, asynchronous=True)
+        return t
 
+    def step():
+        eng.apportion(apply_only(), writeback=True, asynchronous=True)
+
+    step.apply_only = apply_only  # the state a tick starts from (bench's dense share at tick time)
     return step
 
 
@@ -372,17 +409,16 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
     ktimes = run["ktimes"]
     if not ktimes:
         return None
-    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
     name, (launches, total_ms) = max(ktimes.items(), key=lambda kv: kv[1][1])
     avg_s = total_ms / launches / 1e3
     single = single_kernel_tick and len(ktimes) == 1 and launches == steps
     if single:  # one kernel per tick: HIP events around the timed region itself
         avg_s = run["stream_ms"] / steps / 1e3
-    leases_k, res_k = kernel_units(snap).get(name, (N, R))
-    # kernels that skip the subclients column of dense resources: the 128-thread mixed
-    # kernels (they load by the hint) and every dense kernel of the split form
-    group_kernel = name in ("block128x4", "block128x8") or name.endswith("_dense")
-    dense_k = run.get("dense_frac", 0.0) * leases_k if group_kernel else 0.0
+    units = kernel_units(snap)
+    if name not in units:
+        raise KeyError(f"bench.kernel_units has no entry for kernel class {name!r}: its bytes per launch are unknown")
+    leases_k, res_k = units[name]
+    dense_k = kernel_lease_bytes(name, leases_k, run.get("dense_frac", 0.0))
     alg = algorithmic_bytes(leases_k, res_k, dense_k)
     achieved = alg / avg_s / 1e9
     traffic = None
@@ -397,11 +433,13 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
             "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
             "traffic_source": f"profiles/pmc_{workload}.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, calibrated)",
             "algorithmic_bytes_per_launch": alg,
+            "leases_per_launch": leases_k, "resources_per_launch": res_k,
             "bytes_model": (f"{LEASE_BYTES} B per lease (read wants, has, int32 subclients; write gets: granted "
                             f"leases follow their resource's expiry), {DENSE_LEASE_BYTES} B for the rows of dense "
                             f"resources (every row a live follower with one subclient count: no subclients read) "
-                            f"+ {RESOURCE_BYTES} B per resource; the canonical layout of SURVEY.md 8(d) moves "
-                            f"{SURVEY_LEASE_BYTES} B per lease"),
+                            f"and for large_spec's rows (a steady tick through the chain: the last tick's live "
+                            f"bits instead of the subclients column) + {RESOURCE_BYTES} B per resource; the "
+                            f"canonical layout of SURVEY.md 8(d) moves {SURVEY_LEASE_BYTES} B per lease"),
             "dense_lease_share": round(dense_k / leases_k, 4) if leases_k else 0.0,
             "survey_layout_equivalent_GBs": round((SURVEY_LEASE_BYTES * leases_k + 64 * res_k) / avg_s / 1e9, 1),
             # SURVEY.md 8(d) / BASELINE.md 3's canonical 48 B x N + 64 B x R over the same launch time:
@@ -598,6 +636,53 @@ def exchange_self_check(torch, dist, ht, leaf, root, bounds, rank, world, g, now
                    "resources and comparing the owners' templates bit for bit"}
 
 
+def tick_dense_fraction(eng, snap, step) -> float:
+    """The dense share of the workgroup bins' rows in the state a tick starts from: after
+    a writeback tick for back-to-back ticks; for configs[4] after a round's store updates
+    (step.apply_only), which leave most resources with explicit rows, not dense."""
+    if hasattr(step, "apply_only"):
+        step.apply_only()
+        eng.sync()
+    return dense_fraction(eng, snap)
+
+
+def workload_line(name, snap, run, steps, single_kernel_tick):
+    """One workload's numbers for the bench line's `extra` (or the line itself): rate,
+    step time, the tick's fraction of HBM spec over its algorithmic bytes, per-class
+    event times, the dominant kernel's roofline."""
+    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
+    sizes = np.diff(snap["seg_off"])
+    group_leases = int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
+    t_step = run["elapsed"] / steps
+    tick_bytes = algorithmic_bytes(N, R, run["dense_frac"] * group_leases)
+    return {"workload": WORKLOADS[name], "value": N / t_step, "unit": "leases/s", "steps": steps,
+            "ms_per_step": t_step * 1e3,
+            "tick_hbm_frac": round(tick_bytes / t_step / 1e9 / HBM_PEAK_GBS, 4),
+            "tick_algorithmic_bytes": tick_bytes,
+            "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
+                        for k, v in run["ktimes"].items()},
+            "roofline": roofline_of(name, snap, run, steps, single_kernel_tick)}
+
+
+def dist_fields(dist_info, run):
+    """The N > 1 line's `dist`: torch's process group, what the library's own RCCL
+    communicator reports on every rank (null in a gloo rehearsal), per-rank step times,
+    the gather's time on the exchange stream, and the exchange's self-check."""
+    ranks = run["ranks"]
+    steps = [r["step_us"] for r in ranks]
+    ex = [r["exchange_us"] for r in ranks if r["exchange_us"] is not None]
+    d = dict(dist_info or {})
+    d.update({"rccl_nranks": [r["rccl_nranks"] for r in ranks], "rccl_rank": [r["rccl_rank"] for r in ranks],
+              "step_us_min": round(min(steps), 2), "step_us_max": round(max(steps), 2),
+              "exchange_us": round(max(ex), 2) if ex else None,
+              "exchange_us_note": "HIP events around the gather of the servers' blocks (ncclAllGather) on the "
+                                  "exchange stream, profiled steps, max over ranks"})
+    if run.get("self_check"):
+        d.update({"consistent": run["self_check"]["consistent"], "check_sample": run["self_check"]["sample"],
+                  "exchange_check": run["self_check"]})
+    return d
+
+
 def spawn_ranks(args) -> int:
     """--gpus N > 1 outside torchrun: start N ranks with torch.distributed.run before
     this process touches the GPU (a child process, never exec), return their status."""
@@ -777,7 +862,7 @@ def main():
         step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
         root = ht = None
         if args.workload == "c4":
-            step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup)
+            step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup + 1)
         if hier:
             from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
             root = Engine(dev_index)
@@ -800,13 +885,27 @@ def main():
             step = lambda: ht.tick(now, asynchronous=True)  # noqa: E731
         run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4",
                           also=[root] if root is not None else [])
-        run["dense_frac"] = dense_fraction(eng, snap)
+        run["dense_frac"] = tick_dense_fraction(eng, snap, step)
         if ht is not None:
             ht.sync()
             ht.check()  # any server whose request the root rejected (server.go:863-866) fails loudly
             if layout == "sharded":
                 run["self_check"] = exchange_self_check(torch, dist, ht, eng, root, c3_bounds(s_world), rank, world,
                                                         s_rank, now, red_dev, corrupt=args.check_corrupt)
+        # what every rank saw: its step time, the ranks its RCCL communicator counts (the
+        # library's own, not torch's process group), the gather's HIP-event time on the
+        # exchange stream (profiled steps)
+        g = run["ktimes"].get("hier_gather")
+        comm = ht.comm_info() if ht is not None else None
+        mine = {"rank": rank, "step_us": run["elapsed"] / args.steps * 1e6,
+                "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None,
+                "exchange_us": g[1] / g[0] * 1e3 if g and g[0] else None}
+        if world > 1:
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+        else:
+            allr = [mine]
+        run["ranks"] = allr
         t = torch.tensor([run["elapsed"]], dtype=torch.float64, device=red_dev)
         n = torch.tensor([len(snap["wants"])], dtype=torch.float64, device=red_dev)
         if world > 1:
@@ -826,24 +925,33 @@ def main():
     if args.rehearse_shard:
         args.no_extra = True
         args.no_cpu_baseline = True
-    if rank == 0 and world == 1 and not args.no_extra and args.workload == "c3":
-        # the 10M-lease C1 tick (BASELINE configs[1]) beside the north-star line
-        eng.close()
-        snap1 = make_workload("c1", 0)
-        e1 = Engine(dev_index)
-        e1.load(snap1)
-        st1 = lambda: e1.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
-        r1 = timed_steps(torch, e1, st1, args.steps, args.warmup, sync_ranks)
-        r1["dense_frac"] = dense_fraction(e1, snap1)
-        n1 = len(snap1["wants"])
-        extra["c1"] = {"workload": WORKLOADS["c1"], "value": n1 * args.steps / r1["elapsed"], "unit": "leases/s",
-                       "ms_per_step": r1["elapsed"] / args.steps * 1e3,
-                       "roofline": roofline_of("c1", snap1, r1, args.steps, True)}
-        e1.close()
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(snap, now, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_extra and args.workload == "c3":
+        # the other single-GPU configurations beside the north-star line: configs[1] (C1),
+        # configs[2] (C2, the Zipf load-imbalance stress) and configs[4]'s per-GPU streaming
+        # store (C4: 10 rounds by default, each round's update batch held in pinned memory)
+        eng.close()
+        if root is not None:
+            root.close()
+            root = None
+        for name in ("c1", "c2", "c4"):
+            snapx = make_workload(name, 0)
+            ex = Engine(dev_index)
+            ex.load(snapx)
+            if name == "c4":
+                kx = min(args.steps, 10)
+                stx = streaming_step(ex, snapx, 0, 2 * kx + args.warmup + 1)
+            else:
+                kx = args.steps
+                stx = lambda: ex.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
+            rx = timed_steps(torch, ex, stx, kx, args.warmup, sync_ranks, extra_warm=name != "c4")
+            rx["dense_frac"] = tick_dense_fraction(ex, snapx, stx)
+            extra[name] = workload_line(name, snapx, rx, kx, single_kernel_tick=name == "c1")
+            ex.close()
+            del snapx
+
     eng.close()
     if root is not None:
         root.close()
@@ -883,7 +991,9 @@ def main():
                             "; every GPU holds a full store and is an intermediate server of the same resources")
                            + (f"; every step the exchange: publish per-resource totals, all-gather "
                               f"{'(RCCL) ' if world > 1 and not gloo else ''}of {world} block(s), the root's round "
-                              f"over every resource on each GPU, this server's grants"
+                              + ("over this GPU's own resource range (only its owner requests a resource)"
+                                 if layout == "sharded" else "over every resource on each GPU")
+                              + ", this server's grants"
                               + ("" if args.no_pipeline else ", pipelined beside the next leaf tick (one tick of "
                                                              "lag, dm_hier_pipeline)") if hier else "")),
                        "layout": layout, "resources_per_gpu": R, "leases_per_gpu": N, "leases_total": int(n_total),
@@ -891,10 +1001,7 @@ def main():
                                        else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
             "exchange": exchange_used["mode"] if hier else None,
-            "dist": (((dist_info or {}) | {"consistent": run["self_check"]["consistent"],
-                                          "check_sample": run["self_check"]["sample"],
-                                          "exchange_check": run["self_check"]})
-                     if run.get("self_check") else dist_info),
+            "dist": dist_fields(dist_info, run) if world > 1 else None,
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
             "host_enqueue_us_per_step": round(run["host_enqueue_s"] / args.steps * 1e6, 2),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}

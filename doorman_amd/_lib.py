@@ -116,6 +116,8 @@ _SIGS = {
     "dm_hier_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "dm_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_hier_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "dm_hier_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "dm_kernel_class_names": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int]),
     "dm_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dm_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KernelTime), ctypes.c_int]),
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),
@@ -175,6 +177,15 @@ def lib(path: str | None = None):
                                "(make -C doorman_amd/csrc); there is no CPU fallback")
         _lib = _bind(LIB_PATH)
     return _lib
+
+
+def kernel_class_names() -> list[str]:
+    """The kernel classes dm_kernel_times reports (no context or GPU needed)."""
+    L = lib()
+    n = L.dm_kernel_class_names(None, 0)
+    arr = (ctypes.c_char_p * n)()
+    check(L.dm_kernel_class_names(arr, n), None, L)
+    return [x.decode() for x in arr]
 
 
 def check(rc: int, ctx=None, L=None) -> int:

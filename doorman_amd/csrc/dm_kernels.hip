@@ -418,35 +418,16 @@ __global__ __launch_bounds__(1024) void k_count_undense(const WorkItem* __restri
   }
 }
 
-// One wave per resource (n <= 64 R), four independent waves per workgroup: wave
-// reductions only (DPP, no barriers), four resources in flight per workgroup.
-template <int R>
-__global__ __launch_bounds__(256) void k_wave(DevParams p, WorkItem* __restrict__ items, int nitems,
-                                              int32_t* general_list, int32_t* general_count) {
-  Lds<64> lds;  // unused by wave reductions
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= nitems) return;
-  group_segment<64, R>(p, items[i], items + i, threadIdx.x & 63, lds, general_list, general_count);
-}
-
-// Sub-wave groups: G = 16 or 32 lanes own one resource of up to G*R rows (R rows
+// Sub-wave groups: G = 8, 16 or 32 lanes own one resource of up to G*R rows (R rows
 // per lane), so a wave decides 64 / G resources with one set of reduction chains
-// (DPP inside each 16-lane row, plus one readlane combine for G = 32).  Small
-// resources are VALU-bound on their per-resource reductions (~28 reduced dwords
-// per pass set, 4 DPP steps each): narrow groups with several rows per lane share
-// every DPP step among 64 / G resources.
-template <int G, int R = 1>
-__global__ __launch_bounds__(256) void k_sub(DevParams p, WorkItem* __restrict__ items, int nitems,
-                                             int32_t* general_list, int32_t* general_count) {
-  Lds<G> lds;  // unused by sub-wave reductions
-  const int i = blockIdx.x * (256 / G) + (int)(threadIdx.x / G);
-  if (i >= nitems) return;  // whole groups only: reductions never cross a group
-  group_segment<G, R>(p, items[i], items + i, threadIdx.x & (G - 1), lds, general_list, general_count);
-}
-
-// The sub-wave bins in one launch (DM_MERGE_SUBS): the workgroups of each bin
-// follow one another in blockIdx order, so the class stream runs them without a
-// kernel boundary (drain + ramp) between bins.  Register use is the largest bin's.
+// (DPP inside each 16-lane row, plus one readlane combine for G = 32); G = 64 is one
+// wave per resource (wave reductions only, no barriers).  Small resources are
+// VALU-bound on their per-resource reductions (~28 reduced dwords per pass set, 4 DPP
+// steps each): narrow groups with several rows per lane share every DPP step among
+// 64 / G resources.
+// The sub-wave bins in one launch (k_subs): the workgroups of each bin follow one
+// another in blockIdx order, so the class stream runs them without a kernel boundary
+// (drain + ramp) between bins.  Register use is the largest bin's.
 template <int G, int R>
 __device__ __forceinline__ void sub_part(const DevParams& p, WorkItem* __restrict__ items, int nitems, int blk,
                                          int32_t* general_list, int32_t* general_count) {
@@ -1245,15 +1226,15 @@ __global__ __launch_bounds__(256) void k_large_map(DevParams p, const Chunk* __r
 // and it writes the resource's record; else it marks the resource for
 // k_large_redo.  Per lease: wants and has read, gets written -- one pass instead of
 // the chain's four launches and second read.
-// k_large_redo: one launch, every chunk of an unmarked resource leaves at once.  A
-// marked resource's chunks hold their rows in registers and meet twice at most
-// (round 1 again when Clean released rows, round 2), through write-through partials,
-// the last arriver's write-through total and a ready flag (the launch number); they
-// then rewrite their leases and the last arriver stores the totals as the next
-// tick's speculation.  Waiting chunks hold wave slots (why the chain is not built
-// this way), but only a marked resource's; a wait is bounded (kSpecSpin polls: the
-// host then reports DM_E_INTERNAL).  Forward progress as for any in-order dispatched
-// grid whose chunks wait only for their own resource's (at most 489 chunks, C2).
+// k_large_redo_team: one launch, every workgroup leaves at once when nothing is
+// marked.  A marked resource's chunks are shared by a team of at most kTeamMax
+// workgroups that meet twice at most (round 1 again when Clean released rows, round
+// 2), through write-through partials, the last arriver's write-through total and a
+// ready flag (the launch number); they then rewrite their leases and the last arriver
+// stores the totals as the next tick's speculation.  Only a team waits for itself, so
+// any grid of >= kTeamMax co-resident workgroups finishes; a wait is still bounded
+// (kSpecSpin polls: the host then reports DM_E_INTERNAL and refuses the store until it
+// is reloaded).
 // --------------------------------------------------------------------------
 constexpr uint32_t kSpecSpin = 1u << 22;  // polls of ~0.1 us
 
@@ -1514,150 +1495,21 @@ __device__ __forceinline__ void spec_wait(const SpecArgs& S, const uint64_t* fla
   __syncthreads();
 }
 
-// one chunk of a marked resource (k_large_redo's loop)
-__device__ __forceinline__ void redo_chunk(const DevParams& p, const Chunk* __restrict__ chunks,
-                                           const LargeSeg* __restrict__ ls, const Partials& P, const SpecArgs& S,
-                                           int32_t* glist, int32_t* gcount, int c, Lds<256>& lds, int* s_last_p) {
-  int& s_last = *s_last_p;
-  const int t = threadIdx.x;
-  const Chunk ch = chunks[c];
-  SpecTot* sp = S.tot + ch.lseg;
-  const Res rs = load_res(p, ch.seg);
-  const LargeSeg L = ls[ch.lseg];
-  const int nch = L.chunk_end - L.chunk_begin;
-  ChunkRows rw;
-  load_chunk<true>(p, ch, rw, rs);  // no speculation on the rows: the subclients column
-  AggA at = zeroA();
-  at.cnt = sp->a_cnt;
-  at.h = sp->a_h;
-  at.w = sp->a_w;
-  at.smin = sp->a_smin;
-  at.smax = sp->a_smax;
-  at.nan = sp->a_nan;
-  const SegState st = uniform(seg_state_of(p, ch.seg, at));
-  if (st.general) {  // k_general decides it (its first chunk lists it)
-    if (t == 0) {
-      P.uni[c] = -1;
-      if (c == L.chunk_begin) {
-        glist[atomicAdd(gcount, 1)] = L.seg;
-        sp->redo = 0;
-        sp->valid = 0;
-      }
-    }
-    return;
-  }
-  const bool r1 = !rs.learning && rs.kind >= 2;
-  const bool fs = !rs.learning && rs.kind == 3;
-  const double eq = rs.C / (double)st.cl.count;
-  AggB bt{sp->abx, sp->aby, sp->abi};  // round 1 at the running Count: exact when Clean released nothing
-  if (r1 && at.cnt != 0) {  // round 1 again at the Count after Clean
-    const AggB x = group_reduce_t0<256>(chunk_b(rw, rs.kind, eq), OpB(), lds.b);
-    if (t == 0) {
-      st_wt(P.b_x + c, x.x);
-      st_wt(P.b_y + c, x.y);
-      st_wt(P.b_w + c, (int64_t)x.i);
-    }
-    if (spec_arrive(&sp->arrive[1], nch, &s_last)) {
-      if (t < 64) {
-        const AggB r = canon_b(P, L);
-        if (t == 0) {
-          st_wt(&sp->abx, r.x);
-          st_wt(&sp->aby, r.y);
-          st_wt(reinterpret_cast<int64_t*>(&sp->abi), (int64_t)r.i);
-        }
-      }
-      spec_ready(S, &sp->ready[0]);
-    }
-    spec_wait(S, &sp->ready[0]);
-    bt = AggB{ld_wt(&sp->abx), ld_wt(&sp->aby), ld_wt(reinterpret_cast<const int64_t*>(&sp->abi))};
-  }
-  const int s0 = st.a.smin;
-  AggC ct{0.0, 0};
-  FsU fu = make_fsu(eq, s0, bt.x, bt.i, ct);
-  if (fs) {  // round 2 at the resource's threshold
-    const AggC x = group_reduce_t0<256>(chunk_c(rw, s0, eq, fu.T), OpC(), lds.c);
-    if (t == 0) {
-      st_wt(P.c_ee + c, x.ee);
-      st_wt(P.c_sgt + c, (int64_t)x.sgt);
-    }
-    if (spec_arrive(&sp->arrive[2], nch, &s_last)) {
-      if (t < 64) {
-        const AggC r = canon_c(P, L);
-        if (t == 0) {
-          st_wt(&sp->cee, r.ee);
-          st_wt(reinterpret_cast<int64_t*>(&sp->csgt), (int64_t)r.sgt);
-        }
-      }
-      spec_ready(S, &sp->ready[1]);
-    }
-    spec_wait(S, &sp->ready[1]);
-    ct = AggC{ld_wt(&sp->cee), ld_wt(reinterpret_cast<const int64_t*>(&sp->csgt))};
-    fu = make_fsu(eq, s0, bt.x, bt.i, ct);
-  }
-  SumD delta{map_chunk(p, ch, rw, rs, st.cl, uniform(bt), uniform(fu))};
-  delta = group_reduce_t0<256>(delta, OpSumD(), lds.d);
-  if (t == 0) P.uni[c] = st.a.smin == st.a.smax ? st.a.smin : -1;
-  if (t >= 64) return;  // (the loop's barrier waits for wave 0)
-  if (t == 0) st_wt(P.d_delta + c, delta.v);
-  if (!arrive_last(&sp->arrive[0], nch)) return;
-  const double d = canon_d(P, L);
-  if (t == 0) {
-    write_resource(p, L.seg, rs, st.cl, d);
-    // the next tick's speculation: this tick's totals (round 1 and 2 as the chunks used
-    // them; a resource whose live rows hold mixed counts is not speculated on)
-    sp->bx = bt.x;
-    sp->by = bt.y;
-    sp->bi = bt.i;
-    sp->cee = ct.ee;
-    sp->csgt = ct.sgt;
-    sp->s0 = s0;
-    sp->valid = (st.a.smin >= st.a.smax) ? 1 : 0;  // one count, or no live row
-    sp->redo = 0;
-  }
-}
-
-// A grid of at least as many workgroups as the largest resource has chunks (the waits
-// of a resource's chunks are then always met: tickets go out in chunk order, so only
-// the resource at the ticket front can have chunks not yet taken).  With no resource
-// marked it leaves after one load; else its workgroups take chunk tickets in order and
-// do the marked resources' chunks.
-// Two builds of the same code: the full one (160 VGPRs, 3 waves per SIMD) and a light
-// one held to 64 VGPRs (8 waves; the chunk's rows spill to scratch).  A steady tick
-// marks nothing, and there the launch is all the redo costs: the light build's
-// workgroups find a free slot beside the other classes' waves much sooner (C2: 20 ->
-// 10 us of event time, the tick -3.6 us), while a redo of every large resource takes
-// it 2x as long (C2's large class: 90 -> 180 us).  The host launches the light build
-// while the last redo it saw found nothing marked and no row changed since
-// (dm_runtime.cpp); both leave the same bits.
-template <bool kLight>
-__global__ __launch_bounds__(256, kLight ? 8 : 1) void k_large_redo(DevParams p, const Chunk* __restrict__ chunks,
-                                                                     const LargeSeg* __restrict__ ls, Partials P,
-                                                                     SpecArgs S, int32_t* glist, int32_t* gcount) {
-  __shared__ Lds<256> lds;
-  __shared__ int s_last, s_c;
-  const int q = S.par ^ 1;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next tick's slots (its k_large_spec runs after this)
-    S.ring[q] = 0;
-    S.ring[2 + q] = 0;
-    __hip_atomic_store(S.seen, S.ring[S.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (!S.ring[S.par]) return;  // nothing marked (k_large_spec: the previous launch)
-  for (;;) {
-    if (threadIdx.x == 0) s_c = (int)atomicAdd(S.ring + 2 + S.par, 1u);
-    __syncthreads();
-    const int c = s_c;
-    if (c >= S.nchunks) return;
-    if (S.tot[chunks[c].lseg].redo) redo_chunk(p, chunks, ls, P, S, glist, gcount, c, lds, &s_last);
-    __syncthreads();  // every wave back (redo_chunk's waves 1-3 leave before its finish) before the next ticket
-  }
-}
-
 // The redo by teams: a marked resource's chunks are shared among W = min(chunks,
 // kTeamMax) workgroups (its team slots, in ticket order), each taking every W-th chunk
-// through each phase, its rows loaded again per phase.  The chunk partials and the
-// canonical trees are the per-chunk ones of redo_chunk (the same bits); only a team
-// waits for itself, so any grid of >= kTeamMax co-resident workgroups finishes (no
-// bound on a resource's chunks), and a steady tick's empty launch is a small grid.
+// through each phase, its rows loaded again per phase.  Every chunk partial is one
+// 256-thread reduction and every total one canonical tree (canon_*), so the bits are
+// those the chain would write; only a team waits for itself, so any grid of >= kTeamMax
+// co-resident workgroups finishes (no bound on a resource's chunks).  (Round 4's
+// per-chunk redo, one workgroup per chunk with every chunk of a resource co-resident,
+// was retired in round 5.)
+// Two builds of the same code: the full one and a light one held to 64 VGPRs (8 waves;
+// a chunk's rows spill to scratch).  A steady tick marks nothing, and there the launch
+// is all the redo costs: the light build's workgroups find a free slot beside the
+// other classes' waves much sooner (C2: 20 -> 10 us of event time, the tick -3.6 us),
+// while a redo of every large resource takes it about 2x as long.  The host launches
+// the light build while the last redo it saw found nothing marked and no row changed
+// since (dm_runtime.cpp); both leave the same bits.
 __device__ __forceinline__ void redo_team(const DevParams& p, const Chunk* __restrict__ chunks,
                                           const LargeSeg* __restrict__ ls, const Partials& P, const SpecArgs& S,
                                           int32_t* glist, int32_t* gcount, int l, int m, Lds<256>& lds,
@@ -3143,21 +2995,16 @@ hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_
   return hipGetLastError();
 }
 
+// the workgroup bins (3-6) in their one-kernel form; the sub-wave bins run in k_subs
 hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const unsigned wg4 = (unsigned)((n + 3) / 4);
   switch (bin) {
-    case 0: k_sub<16, 4><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 1: k_sub<32, 4><<<(unsigned)((n + 7) / 8), 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 2: k_wave<4><<<wg4, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 3: k_block<128, 4><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
     case 4: k_block<128, 8><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
     case 5: k_block<256, 8><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 6: k_block<256, 16><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case kBin6Wide: k_block<512, 8><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 7: k_sub<8, 2><<<(unsigned)((n + 31) / 32), 256, 0, st>>>(p, segs, n, glist, gcount); break;
-    case 8: k_sub<16, 2><<<(unsigned)((n + 15) / 16), 256, 0, st>>>(p, segs, n, glist, gcount); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -3244,23 +3091,17 @@ hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks,
   if (phase == 0)
     k_large_spec<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, S);
   else if (phase == 1)
-    k_large_redo<false><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
-  else if (phase == 2)
-    k_large_redo<true><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
-  else if (phase == 3)
     k_large_redo_team<false><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
   else
     k_large_redo_team<true><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
   return hipGetLastError();
 }
 
-// Workgroups of k_large_redo's full build that one CU holds at once (its forward-progress
-// bound: a marked resource's chunks wait for one another, so a resource with more chunks
-// than the whole GPU holds redo workgroups would wait forever; dm_runtime.cpp keeps such
-// a store off the speculative chain).
+// Workgroups of the redo's full build that one CU holds at once (the full build's grid:
+// up to 3/4 of what the GPU holds, dm_runtime.cpp).
 int redo_blocks_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_large_redo<false>, 256, 0) != hipSuccess) return 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_large_redo_team<false>, 256, 0) != hipSuccess) return 1;
   return n > 0 ? n : 1;
 }
 

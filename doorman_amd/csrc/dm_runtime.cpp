@@ -114,6 +114,7 @@ enum KClass {
   KC_DECIDE,    // dm_decide: the round's device work (fast path + k_decide)
   KC_LARGE_SPEC, // the speculative chain: k_large_spec,
   KC_LARGE_REDO, // k_large_redo
+  KC_HIER_GATHER, // dm_hier_step's gather of the servers' blocks (ncclAllGather, or a rehearsal's copy)
   KC_COUNT
 };
 // bin 6 (2049-4096 rows) runs on 256 x 16 or 512 x 8 workgroups (kBin6Wide):
@@ -127,7 +128,7 @@ const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",   
                                      "block128x4_rest", "block128x8_rest", "block256x8_rest", "block2k4k_rest",
                                      "hier_publish",
                                      "hier_root", "large_t", "large_c_het", "large_e", "large_map_het", "decide",
-                                     "large_spec", "large_redo"};
+                                     "large_spec", "large_redo", "hier_gather"};
 
 template <typename T>
 struct DBuf {
@@ -164,22 +165,20 @@ struct dm_ctx {
   // auxiliary streams: independent size bins of one tick run concurrently
   static constexpr int kAux = 4;
   // auxiliary stream of each work class: bins 0..kNumBins-1, small packs, large chain
-  // (DM_SPLIT="ddddddddddd" overrides, one digit per class, for A/B runs)
-  int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (packs alone)
+  // (round 4 moved every bin to each other stream in A/Bs: this split won every one)
+  static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (packs alone)
   hipStream_t aux[kAux] = {};
   hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
   // Cross-stream order between the context's streams (fork / join of a tick's work
   // classes, the pipelined hierarchy's template slots, dm_stream_wait): an event
-  // recorded on the producing stream and waited on by the consuming one, or a rising
-  // sequence number written into a signal word (hipStreamWriteValue64) and waited for
-  // (hipStreamWaitValue64, >=).  An event wait idles the consuming queue ~12-20 us on
-  // the box (tools/xs_probe.py); this ROCm runs the stream memory operations as blit
-  // kernels (__amd_rocclr_streamOps*, 3-5 us each plus a dispatch gap,
-  // a rocprofv3 kernel trace of the C3 step) and measured no cheaper per step.  Events by default;
-  // DM_XS_VALUES=1 every hop as values, DM_XS_READY_VALUE=1 only the staged templates'
-  // hop.  A wait on a token signalled on the waiting stream itself is skipped (stream
-  // order).
+  // recorded on the producing stream and waited on by the consuming one.  An event wait
+  // idles the consuming queue ~12-20 us on the box (tools/xs_probe.py); stream-memory
+  // tokens (hipStreamWriteValue64 / WaitValue64, which this ROCm runs as blit kernels
+  // of 3-5 us each plus a dispatch gap) measured no cheaper per step (round 4: 75.0 vs
+  // 72.2 us per N = 8 shard step) and were retired in round 5.  The one stream-memory
+  // signal kept is the tick-done word (below).  A wait on a token signalled on the
+  // waiting stream itself is skipped (stream order).
   static constexpr int kTplSlots = 4;  // staged templates: in use + pending (lag 2) + the one being written
   enum : int {
     XS_FORK = 0,
@@ -193,35 +192,20 @@ struct dm_ctx {
   };
   struct XsTok {
     int w = 0;
-    uint64_t v = 0;
     hipStream_t s = nullptr;  // the stream it was signalled on
     bool rec = false;         // recorded (else the wait records on s first: lazy signal)
-    bool val = false;         // a stream-memory signal (else an event)
   };
-  bool xs_values = false;      // every token as stream memory (DM_XS_VALUES=1)
   // A pipelined leaf's staged templates from another stream: the host waits for the
   // exchange that made them and the leaf's stream gets no barrier (a queue waiting on
   // another queue here costs ~12-16 us even when the signal is long set -- the step of
   // an N = 8 shard idled that long every tick, tools/step_trace.py); the host stays at
-  // most ~one step ahead, the device never waits.  DM_TPL_HOSTWAIT=0: the barrier.
-  bool tpl_hostwait = true;
-  bool xs_can_value = false;   // signal words allocated
-  // the staged templates' hop -- the only one a pipelined leaf tick waits on -- as
-  // stream memory (DM_XS_READY_VALUE=1).  Off: with the exchange on a second stream the
-  // C3 step took 455.5 us with it against 451.6 us with an event (one stream: 446 us;
-  // tools/gpu_xs2.sh), the wait kernel's dispatch costing what the barrier did
-  bool xs_ready_value = false;
-  uint64_t* xs_word[XS_N] = {};  // signal memory, one word per allocation
-  uint64_t xs_seq[XS_N] = {};
+  // most ~one step ahead, the device never waits.
   hipEvent_t xs_ev[XS_N] = {};
-  hipError_t xs_signal(int w, hipStream_t s, XsTok* tok, bool value = false) {
+  hipError_t xs_signal(int w, hipStream_t s, XsTok* tok) {
     tok->w = w;
     tok->s = s;
     tok->rec = true;
-    tok->val = xs_can_value && (value || xs_values);
-    if (!tok->val) return hipEventRecord(xs_ev[w], s);
-    tok->v = ++xs_seq[w];
-    return hipStreamWriteValue64(s, xs_word[w], tok->v, 0);
+    return hipEventRecord(xs_ev[w], s);
   }
   // A signal recorded only if a wait on another stream needs it, then at that wait:
   // it orders after everything the signalling stream holds by then (never less than
@@ -230,13 +214,11 @@ struct dm_ctx {
     tok->w = w;
     tok->s = s;
     tok->rec = false;
-    tok->val = false;
   }
   hipError_t xs_wait(const XsTok& tok, hipStream_t s) {
     if (tok.s == s || tok.s == nullptr) return hipSuccess;  // same stream, or known complete
     if (!tok.rec) return xs_order(tok.w, tok.s, s);
-    if (!tok.val) return hipStreamWaitEvent(s, xs_ev[tok.w], 0);
-    return hipStreamWaitValue64(s, xs_word[tok.w], tok.v, hipStreamWaitValueGte, ~0ull);
+    return hipStreamWaitEvent(s, xs_ev[tok.w], 0);
   }
   hipError_t xs_order(int w, hipStream_t from, hipStream_t to) {
     if (from == to) return hipSuccess;
@@ -248,6 +230,13 @@ struct dm_ctx {
 
   int64_t R = 0, N = 0;
   bool store_loaded = false, cfg_loaded = false;
+  // A device-side invariant failed (a redo workgroup gave up waiting, a dense kernel
+  // queued an item on a tick that skipped its rest kernel: the host-mapped words
+  // below).  The tick that tripped it may have written wrong leases and sums into the
+  // store, so every call that reads, updates or ticks the store refuses it from then
+  // on (DM_E_INTERNAL) until dm_store_load replaces it.
+  bool store_lost = false;
+  std::string lost_msg;
   // the store may hold explicit-expiry rows: set by every call that can write one
   // (load, upserts, decide, the root's tick), cleared by a writeback tick (which
   // turns every live explicit row into a follower).  Without them pass A's
@@ -316,9 +305,9 @@ struct dm_ctx {
   DBuf<WorkItem> bins[kNumBins];
   DBuf<Chunk> chunks;
   DBuf<LargeSeg> large;
-  // the sub-wave bins in one launch (k_subs; DM_MERGE_SUBS=0: one launch per bin):
-  // C2 tick 144-145 -> 138 us (tools/ab.py, both orders, one box)
-  bool merge_subs = true;
+  // the sub-wave bins run in one launch (k_subs): C2 tick 144-145 -> 138 us against
+  // one launch per bin (tools/ab.py, both orders, one box; the per-bin form was
+  // retired in round 5)
   // The 128-thread bins (3, 4) split by the dense hint (k_block_dense + k_block_rest)
   // on a tick that follows a writeback tick (only those set hints), unless the last
   // split tick the host has heard of queued more than a quarter of the bin's items
@@ -343,7 +332,6 @@ struct dm_ctx {
   int32_t* h_guard = nullptr;
   int32_t* d_guard = nullptr;
   uint64_t dq_ver_epoch[kSplitBins] = {};  // the epoch each bin's check was enqueued in
-  bool skip_rest = true;  // DM_SKIP_REST=0: always launch k_block_rest
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
@@ -355,15 +343,12 @@ struct dm_ctx {
   bool spec_chain = true;
   DBuf<SpecTot> p_spec;
   DBuf<uint32_t> p_spec_ring;  // SpecArgs::ring
-  int redo_grid = 64;          // k_large_redo's workgroups: at least the largest resource's chunks
-  // k_large_redo's full build: 3/4 of the workgroups the GPU holds at once (its
-  // forward-progress bound), and whether the loaded store's largest resource fits it
-  // (else no speculation)
+  // 3/4 of the redo workgroups (full build) the GPU holds at once: the full build's
+  // grid when the store has that many team slots
   int64_t redo_cap = 0;
-  bool spec_fits = true;
-  // the redo by teams (k_large_redo_team; DM_REDO_TEAM=0: k_large_redo, one workgroup
-  // per chunk, bounded by redo_cap): team slots and the two builds' grids
-  bool redo_team = true;
+  // the redo by teams (k_large_redo_team): team slots and the two builds' grids.  (The
+  // per-chunk redo of round 4, bounded by redo_cap chunks per resource, was retired in
+  // round 5: the teams need only kTeamMax co-resident workgroups for any resource.)
   DBuf<int32_t> p_team;
   int nslots = 0, team_grid_full = 1, team_grid_light = 1;
   uint64_t spec_seq = 0;
@@ -462,7 +447,7 @@ struct dm_ctx {
   // split tick's rest kernel stores its number when the tick is done.  Another queue
   // waits on the word (hipStreamWaitValue64) instead of an event recorded on this queue
   // (each marker on the leaf's queue cost a ~10-us bubble per N = 8 shard step).
-  // DM_TICK_FLAG=0: events only.
+  // nullptr when the device cannot wait on stream values: events then.
   uint64_t* tick_word = nullptr;
   uint32_t* tick_ctr = nullptr;
   uint64_t tick_seq = 0;          // the last tick's number
@@ -487,6 +472,31 @@ struct dm_ctx {
   }
   int hip_fail(hipError_t e, const char* what) {
     return fail(DM_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
+  // The device's failure words (host-mapped, written by kernels of earlier ticks):
+  // once one is set the store is lost (store_lost).  Called at the entry of every call
+  // that touches the store and after every host wait that may have completed a tick.
+  int check_device() {
+    if (!store_lost) {
+      for (int i = 0; h_guard && i < kSplitBins; ++i)
+        if (__atomic_load_n(h_guard + i, __ATOMIC_RELAXED)) {
+          store_lost = true;
+          lost_msg = "a dense kernel queued an item on a tick that skipped its rest kernel";
+        }
+      if (!store_lost && h_serr && __atomic_load_n(h_serr, __ATOMIC_RELAXED)) {
+        store_lost = true;
+        lost_msg = "a redo workgroup of the speculative chain gave up waiting for its resource";
+      }
+    }
+    if (!store_lost) return DM_OK;
+    return fail(DM_E_INTERNAL, "internal failure on the device: " + lost_msg +
+                                   "; the store's leases and sums may be wrong, reload it (dm_store_load)");
+  }
+  // wait for the context stream, then report a device failure the wait completed
+  int synced(const char* what) {
+    const hipError_t e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_fail(e, what);
+    return check_device();
   }
   hipEvent_t take_event() {
     if (!event_pool.empty()) {
@@ -591,6 +601,13 @@ struct dm_ctx {
     (ctx)->main_dirty = true;                                 \
   } while (0)
 
+// Entry of every call that reads or updates the store: refuse a lost store
+// (dm_ctx::store_lost) with the device's message.
+#define DM_STORE_OK(ctx)                             \
+  do {                                               \
+    if (int _rc = (ctx)->check_device()) return _rc; \
+  } while (0)
+
 template <typename T>
 static hipError_t upload(DBuf<T>& b, const T* src, size_t n, hipStream_t st) {
   hipError_t e = b.ensure(n);
@@ -672,7 +689,7 @@ static void build_plan(dm_ctx* c) {
 // its items left without a dense hint (k_count_undense -> h_rec).  A count of 0 lets
 // the following ticks of the epoch skip the bin's k_block_rest.
 static hipError_t check_dense(dm_ctx* c, int i, int b, hipStream_t s) {
-  if (!c->skip_rest || c->dq_ver_epoch[i] == c->row_epoch || c->h_bins[b].empty()) return hipSuccess;
+  if (c->dq_ver_epoch[i] == c->row_epoch || c->h_bins[b].empty()) return hipSuccess;
   c->dq_ver_epoch[i] = c->row_epoch;
   return launch_count_undense(c->bins[b].p, (int)c->h_bins[b].size(), (unsigned long long*)(c->d_rec + 2 * i),
                               (unsigned long long)c->row_epoch, s);
@@ -745,10 +762,6 @@ static int upload_plan(dm_ctx* c) {
     DM_HIP(c, hipMemsetAsync(c->p_spec.p, 0, nl * sizeof(SpecTot), st), "speculative chain");
     DM_HIP(c, c->p_spec_ring.ensure(4), "speculative chain");
     DM_HIP(c, hipMemsetAsync(c->p_spec_ring.p, 0, 4 * sizeof(uint32_t), st), "speculative chain");
-    int most = 1;
-    for (const LargeSeg& L : c->h_large) most = std::max(most, L.chunk_end - L.chunk_begin);
-    c->redo_grid = std::min<int>(std::max<int>((int)c->h_chunks.size(), 1), std::max(most, 64));
-    c->spec_fits = c->redo_team || most <= c->redo_cap;
     std::vector<int32_t> team;
     for (size_t l = 0; l < c->h_large.size(); ++l) {
       const int nch_l = c->h_large[l].chunk_end - c->h_large[l].chunk_begin;
@@ -810,7 +823,7 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
 // ---------------------------------------------------------------------------
 extern "C" {
 
-const char* dm_version(void) { return "doorman-hip 0.3 (gfx950, abi 3)"; }
+const char* dm_version(void) { return "doorman-hip 0.4 (gfx950, abi 4)"; }
 
 int dm_device_count(int* out) {
   if (!out) return DM_E_INVAL;
@@ -825,37 +838,13 @@ int dm_device_count(int* out) {
   return DM_OK;
 }
 
-// The context's cross-stream order (dm_ctx::xs_signal): events, or with DM_XS_VALUES=1
-// signal-memory words, zeroed (events when the device cannot wait on stream values).
+// The context's cross-stream order (dm_ctx::xs_signal): one event per hop kind.
 static hipError_t xs_setup(dm_ctx* c) {
-  if (const char* xv = getenv("DM_XS_VALUES")) c->xs_values = atoi(xv) != 0;
-  if (const char* xr = getenv("DM_XS_READY_VALUE")) c->xs_ready_value = atoi(xr) != 0;
   for (int i = 0; i < dm_ctx::XS_N; ++i) {
     hipError_t e = hipEventCreateWithFlags(&c->xs_ev[i], hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
-  if (!c->xs_values && !c->xs_ready_value) return hipSuccess;  // events only: no signal memory
-  int can = 0;
-  if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, c->device) != hipSuccess || !can) {
-    (void)hipGetLastError();
-    return hipSuccess;  // events only
-  }
-  for (int i = 0; i < dm_ctx::XS_N; ++i) {
-    void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess ||
-        hipStreamWriteValue64(c->stream, p, 0, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      if (p) (void)hipFree(p);
-      for (int j = 0; j < i; ++j) {
-        (void)hipFree(c->xs_word[j]);
-        c->xs_word[j] = nullptr;
-      }
-      return hipStreamSynchronize(c->stream);  // events only
-    }
-    c->xs_word[i] = (uint64_t*)p;
-  }
-  c->xs_can_value = true;
-  return hipStreamSynchronize(c->stream);
+  return hipSuccess;
 }
 
 int dm_create(int device, dm_ctx** out) {
@@ -878,23 +867,16 @@ int dm_create(int device, dm_ctx** out) {
   }
   dm_ctx* c = new dm_ctx();
   c->device = device;
-  if (const char* ms = getenv("DM_MERGE_SUBS")) c->merge_subs = atoi(ms) != 0;
+  // Test hooks: each forces one of two product paths that the
+  // library chooses between by itself, so that a test can compare the two on the same
+  // ticks.  No other environment switch exists (round 5 retired the A/B probes).
   if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
-  if (const char* hw = getenv("DM_TPL_HOSTWAIT")) c->tpl_hostwait = atoi(hw) != 0;
-  if (const char* sr = getenv("DM_SKIP_REST")) c->skip_rest = atoi(sr) != 0;
   if (const char* sc = getenv("DM_SPEC_CHAIN")) c->spec_chain = atoi(sc) != 0;
   if (const char* rl = getenv("DM_REDO_LIGHT")) c->redo_light = atoi(rl);
-  if (const char* rt = getenv("DM_REDO_TEAM")) c->redo_team = atoi(rt) != 0;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
   }
-  if (const char* sp = getenv("DM_SPLIT"))  // A/B of the work-class -> stream assignment
-    for (int i = 0; i < kNumBins + 2 && sp[i]; ++i) {  // one base-36 digit per class
-      const int d = sp[i] >= 'a' ? sp[i] - 'a' + 10 : sp[i] - '0';
-      if (d < 0 || d >= dm_ctx::kAux) break;
-      c->class_stream[i] = d;
-    }
   e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -907,52 +889,19 @@ int dm_create(int device, dm_ctx** out) {
   // round robin with every other stream of the process (torch's included), so which
   // work classes ended up serialised behind one queue depended on how many streams
   // existed before: C2 tick 147-179 us by creation order, 147-151 us with the masks
-  // (tools/host_cost.py, one process per run).  DM_CUMASK=0 restores plain streams.
-  const bool cumask = !getenv("DM_CUMASK") || atoi(getenv("DM_CUMASK")) != 0;
+  // (tools/host_cost.py, one process per run).  Static CU partitions (round 3-4 A/Bs:
+  // 139-491 us against 136-140 us) and a high-priority chain stream (a queue shared
+  // again) lost, and were retired in round 5.
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   // a quarter of headroom: the other classes' streams hold slots too, and run ahead
-  // (DM_DEFER_JOIN).  C2's 489 chunks of 768 redo well; 978 of 1024 (1024-row chunks)
-  // waited out the spin bound
+  // (DM_DEFER_JOIN)
   c->redo_cap = (int64_t)std::max(ncu, 1) * redo_blocks_per_cu() * 3 / 4;
   const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
-  std::vector<std::vector<uint32_t>> masks(dm_ctx::kAux, std::vector<uint32_t>(mwords, 0u));
-  for (int i = 0; i < dm_ctx::kAux; ++i)
-    for (int b = 0; b < ncu; ++b) masks[i][(size_t)(b / 32)] |= 1u << (b % 32);
-  // A/B probe: DM_CU_PART="n0,n1,n2,n3" gives auxiliary stream i its own n_i CUs
-  // (interleaved over the CU index, so every stream spans every XCD) instead of all
-  if (const char* part = getenv("DM_CU_PART")) {
-    int want[dm_ctx::kAux] = {0, 0, 0, 0}, got[dm_ctx::kAux] = {0, 0, 0, 0}, total = 0;
-    sscanf(part, "%d,%d,%d,%d", &want[0], &want[1], &want[2], &want[3]);
-    for (int i = 0; i < dm_ctx::kAux; ++i) total += want[i];
-    if (total > 0 && total <= ncu) {
-      for (auto& m : masks) std::fill(m.begin(), m.end(), 0u);
-      for (int b = 0; b < total; ++b) {  // the stream furthest below its share takes the next CU
-        int best = 0;
-        double gap = -1e9;
-        for (int i = 0; i < dm_ctx::kAux; ++i) {
-          const double g = (double)want[i] * (b + 1) / total - got[i];
-          if (want[i] > got[i] && g > gap) {
-            gap = g;
-            best = i;
-          }
-        }
-        masks[best][(size_t)(b / 32)] |= 1u << (b % 32);
-        ++got[best];
-      }
-    }
-  }
-  // DM_CHAIN_PRIO=1: the large chain's stream at the highest priority (a queue of its own)
-  const int prio_aux = (getenv("DM_CHAIN_PRIO") && atoi(getenv("DM_CHAIN_PRIO")) != 0) ? c->class_stream[kNumBins + 1] : -1;
+  std::vector<uint32_t> mask(mwords, 0u);
+  for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
   for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
-    if (i == prio_aux) {
-      int lo = 0, hi = 0;
-      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-      e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, hi);
-      continue;
-    }
-    e = cumask && ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, masks[i].data())
-                          : hipErrorNotSupported;
+    e = ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, mask.data()) : hipErrorNotSupported;
     if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
       (void)hipGetLastError();
       e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
@@ -961,7 +910,7 @@ int dm_create(int device, dm_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
-  if (e == hipSuccess && (!getenv("DM_TICK_FLAG") || atoi(getenv("DM_TICK_FLAG")) != 0)) {
+  if (e == hipSuccess) {
     int can = 0;
     if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && can &&
         hipExtMallocWithFlags((void**)&c->tick_word, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess &&
@@ -1017,10 +966,8 @@ void dm_destroy(dm_ctx* c) {
     (void)hipStreamSynchronize(c->cpy);
     (void)hipStreamDestroy(c->cpy);
   }
-  for (int i = 0; i < dm_ctx::XS_N; ++i) {
+  for (int i = 0; i < dm_ctx::XS_N; ++i)
     if (c->xs_ev[i]) (void)hipEventDestroy(c->xs_ev[i]);
-    if (c->xs_word[i]) (void)hipFree(c->xs_word[i]);
-  }
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_bat)
@@ -1062,9 +1009,9 @@ int dm_stream_wait(dm_ctx* c, void* s) {
 
 int dm_sync(dm_ctx* c) {
   DM_ENTER(c);
-  DM_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  const int rc = c->synced("hipStreamSynchronize");
   c->collect_profile();
-  return DM_OK;
+  return rc;
 }
 
 int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
@@ -1154,6 +1101,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
     c->all_sub_one = s->subclients[i] == 1 || s->expiry_ns[i] == DM_RELEASED;
   DM_HIP(c, hipStreamSynchronize(st), "store load");
   c->store_loaded = true;
+  c->store_lost = false;  // upload_plan cleared the device's failure words
   c->expl_rows = true;
   c->rows_changed();
   c->have_result = false;
@@ -1199,6 +1147,7 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
 
 static int ready(dm_ctx* c) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
+  if (int rc = c->check_device()) return rc;
   if (!c->cfg_loaded || (int64_t)c->h_refresh_s.size() != c->R)
     return c->fail(DM_E_STATE, "no configuration loaded for the store's resources");
   return DM_OK;
@@ -1217,10 +1166,20 @@ static int commit_templates(dm_ctx* c) {
   if (take < 0) return DM_OK;
   DM_HIP(c, c->join_aux(), "join");  // deferred class work also read the old templates
   const dm_ctx::XsTok& rt = c->tpl_ready[take];
-  if (c->tpl_hostwait && rt.rec && !rt.val && rt.s && rt.s != c->stream) {
+  if (rt.rec && rt.s && rt.s != c->stream) {
+    // poll: the wake-up of a blocking wait comes too late for the next launch to be
+    // queued in time.  Bounded by time (the exchange may wait on a slower rank's
+    // all-gather): after 50 us of polling, a blocking wait frees the core.
     hipError_t q = hipEventQuery(c->xs_ev[rt.w]);
-    for (int spin = 0; q == hipErrorNotReady && spin < (1 << 20); ++spin) q = hipEventQuery(c->xs_ev[rt.w]);  // poll:
-    // the wake-up of a blocking wait comes too late for the next launch to be queued in time
+    if (q == hipErrorNotReady) {
+      timespec t0{}, t1{};
+      clock_gettime(CLOCK_MONOTONIC, &t0);
+      do {
+        q = hipEventQuery(c->xs_ev[rt.w]);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+      } while (q == hipErrorNotReady &&
+               (t1.tv_sec - t0.tv_sec) * 1000000000LL + (t1.tv_nsec - t0.tv_nsec) < 50000);
+    }
     if (q == hipErrorNotReady) q = hipEventSynchronize(c->xs_ev[rt.w]);
     if (q != hipSuccess) return c->hip_fail(q, "staged templates");
   } else {
@@ -1244,11 +1203,6 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   int rc = ready(c);
   if (rc) return rc;
   if (c->tpl_pipe && (rc = commit_templates(c))) return rc;
-  for (int i = 0; c->h_guard && i < dm_ctx::kSplitBins; ++i)
-    if (__atomic_load_n(c->h_guard + i, __ATOMIC_RELAXED))
-      return c->fail(DM_E_INTERNAL, "a dense kernel queued an item on a tick that skipped its rest kernel");
-  if (c->h_serr && __atomic_load_n(c->h_serr, __ATOMIC_RELAXED))
-    return c->fail(DM_E_INTERNAL, "a redo workgroup of the speculative chain gave up waiting for its resource");
   c->ticks_issued += 1;
   c->tick_seq += 1;
   c->tick_flagged = false;
@@ -1275,7 +1229,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // The speculative large chain (below) writes its gets before they are verified, so a
   // tick that may take it writes the alternate column whatever the store's size.
   const bool spec_eligible = c->spec_chain && wb && !(flags & DM_AGG_RECOMPUTE) && !c->expl_rows &&
-                             !(c->maybe_general && c->n_nonsmall > 0) && !c->h_chunks.empty() && c->spec_fits;
+                             !(c->maybe_general && c->n_nonsmall > 0) && !c->h_chunks.empty();
   const bool pingpong = wb && !(flags & DM_WB_INPLACE) &&
                         ((flags & DM_WB_ALTERNATE) || c->N * 48 > kStreamBytes || spec_eligible);
   // A writeback tick writes no per-lease expiry: the leases it grants follow their
@@ -1390,7 +1344,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     // the steady state: one speculative launch, verified per resource, and a redo launch
     // that only the resources whose totals moved use (the store's rows must not be
     // overwritten by the speculative gets: alternate output columns)
-    const bool spec = c->spec_chain && c->spec_fits && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
+    const bool spec = c->spec_chain && !het && P.b_first && wb && p.out_gets != p.has && nch > 0;
     if (spec) {
       const SpecArgs S{c->p_spec.p, c->spec_seq, c->d_serr, c->p_spec_ring.p, (int)(c->spec_seq & 1), nch,
                        reinterpret_cast<uint32_t*>(c->d_serr + 1), c->p_team.p, c->nslots};
@@ -1398,8 +1352,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
       const bool light = c->redo_light == 2 || (c->redo_light == 1 && c->redo_epoch == c->row_epoch &&
                                                 __atomic_load_n(c->h_serr + 1, __ATOMIC_RELAXED) == 0);
       c->redo_epoch = c->row_epoch;
-      const int redo_phase = c->redo_team ? (light ? 4 : 3) : (light ? 2 : 1);
-      const int redo_grid = c->redo_team ? (light ? c->team_grid_light : c->team_grid_full) : c->redo_grid;
+      const int redo_phase = light ? 2 : 1;
+      const int redo_grid = light ? c->team_grid_light : c->team_grid_full;
       for (int ph = 0; ph < 2; ++ph)
         DM_HIP(c, timed(ph == 0 ? KC_LARGE_SPEC : KC_LARGE_REDO, s_large,
                         [&] {
@@ -1422,8 +1376,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   const bool split_dense = c->have_result && c->last_writeback;
   // the sub-wave bins (8x2, 16x2, 16x4, 32x4, 64x4) in one launch on bin 0's stream
   static constexpr int kSubBins[5] = {7, 8, 0, 1, 2}, kSubG[5] = {8, 16, 16, 32, 64};
-  const bool merge_subs = c->merge_subs;
-  if (merge_subs) {
+  {
     SubBins sb{};
     int nonempty = 0;
     for (int k = 0; k < 5; ++k) {
@@ -1442,7 +1395,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   for (int b = kNumBins - 1; b >= 0; --b) {
     const int n = (int)c->h_bins[b].size();
     if (n == 0) continue;
-    if (merge_subs && (b == 7 || b == 8 || b <= 2)) continue;
+    if (b == 7 || b == 8 || b <= 2) continue;  // k_subs
     hipStream_t s = cls_stream(b);
     const int lb = (b == 6 && c->bin6_wide) ? kBin6Wide : b;  // the launchers' bin (shape)
     if (b >= 3 && b < 3 + dm_ctx::kSplitBins && ((c->dense_split >> (b - 3)) & 1) && split_dense) {
@@ -1457,7 +1410,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
         // Every item verified dense in this row epoch: nothing can be queued, so the
         // dense kernel is the bin's only launch (the guard catches the impossible).
         const uint64_t* rec = c->h_rec + 2 * i;
-        const bool skip = c->skip_rest && __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
+        const bool skip = __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
                           __atomic_load_n(rec, __ATOMIC_RELAXED) == 0;
         TickDone td{nullptr, nullptr, 0};
         if (one_class && c->tick_word && c->tick_word_wanted) {
@@ -1510,8 +1463,9 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (wb) c->expl_rows = false;
   c->chain_live_ok = wb && chain_live;
   if (!(flags & DM_ASYNC)) {
-    DM_HIP(c, hipStreamSynchronize(st), "tick");
+    rc = c->synced("tick");
     c->collect_profile();
+    return rc;
   }
   return DM_OK;
 }
@@ -1703,7 +1657,7 @@ int dm_decide(dm_ctx* c, int64_t now_ns, int64_t n, const int64_t* rows, const d
   DM_HIP(c, c->timed(KC_DECIDE, st, launches), "decide requests");
   DM_HIP(c, download(shas.data(), (const double*)c->rq_gets.p, 0, n, st), "read decisions");
   DM_HIP(c, download(ssub.data(), (const int64_t*)c->rq_exp.p, 0, n, st), "read decisions");
-  DM_HIP(c, hipStreamSynchronize(st), "decide requests");
+  if (int rs = c->synced("decide requests")) return rs;
   for (int64_t i = 0; i < n; ++i) {
     gets[order[(size_t)i]] = shas[(size_t)i];
     expiry_ns[order[(size_t)i]] = ssub[(size_t)i];
@@ -1718,6 +1672,7 @@ static int check_range(dm_ctx* c, int64_t off, int64_t n, int64_t total) {
 
 int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* expiry_ns) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
@@ -1731,12 +1686,12 @@ int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* exp
   } else {
     DM_HIP(c, download(expiry_ns, (const int64_t*)c->out_expiry.p, off, n, c->stream), "read expiry");
   }
-  DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
-  return DM_OK;
+  return c->synced("read leases");
 }
 
 int dm_read_leases_rows(dm_ctx* c, int64_t n, const int64_t* rows, double* gets, int64_t* expiry_ns) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad rows");
   if (n == 0) return DM_OK;
@@ -1755,8 +1710,7 @@ int dm_read_leases_rows(dm_ctx* c, int64_t n, const int64_t* rows, double* gets,
            "resolve expiry");
   DM_HIP(c, download(gets, (const double*)c->st_has.p, 0, n, c->stream), "read gets");
   DM_HIP(c, download(expiry_ns, (const int64_t*)c->st_exp.p, 0, n, c->stream), "read expiry");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "read leases");
-  return DM_OK;
+  return c->synced("read leases");
 }
 
 int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, int64_t* expiry_time_s,
@@ -1797,6 +1751,7 @@ int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, in
 int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* sum_has, double* sum_wants,
                       double* safe) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   int rc = check_range(c, r0, n, c->R);
   if (rc) return rc;
   if (safe && !c->have_result) return c->fail(DM_E_STATE, "safe capacity needs a dm_apportion result");
@@ -1808,7 +1763,7 @@ int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* 
   // the device config: a hierarchy exchange rewrites a leaf's templates (dm_hier_root_tick)
   if (safe) DM_HIP(c, download(cf.data(), (const ResCfg*)c->cfg.p, r0, n, c->stream), "read config");
   if (safe) DM_HIP(c, download(cc.data(), (const ResCold*)c->cold.p, r0, n, c->stream), "read config");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "read resources");
+  if (int rs = c->synced("read resources")) return rs;
   for (int64_t i = 0; i < n; ++i) {
     if (count) count[i] = v[i].count;
     if (sum_has) sum_has[i] = v[i].sum_has;
@@ -1845,6 +1800,7 @@ int dm_read_config(dm_ctx* c, int64_t r0, int64_t n, int32_t* kind, double* capa
 
 int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants, int64_t* sub, int64_t* exp) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
@@ -1859,8 +1815,7 @@ int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants,
     DM_HIP(c, download(exp, (const int64_t*)c->st_exp.p, 0, n, c->stream), "read expiry");
     DM_HIP(c, download(sub, (const int64_t*)c->st_sub.p, 0, n, c->stream), "read subclients");
   }
-  DM_HIP(c, hipStreamSynchronize(c->stream), "read store");
-  return DM_OK;
+  return c->synced("read store");
 }
 
 // Rows of one upsert/release call: in range and unique (a bitmap over the table,
@@ -1915,7 +1870,7 @@ static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
   DM_HIP(c, launch_clear_rows(n, c->st_rows.p, c->N, c->row_bits.p, c->stream), "clear rows");
   DM_HIP(c, hipMemcpyAsync(c->h_flags, c->upd_flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream),
          "update flags");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "update");
+  if (int rs = c->synced("update")) return rs;
   const uint32_t f = *c->h_flags;
   *flags_out = f;
   if (f & kUpdRange) return c->fail(DM_E_RANGE, "row out of range");
@@ -1927,6 +1882,7 @@ static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
 int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has, const double* wants,
                     const int64_t* sub, const int64_t* exp) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !has || !wants || !sub || !exp))) return c->fail(DM_E_INVAL, "bad upsert");
   if (n == 0) return DM_OK;
@@ -1957,6 +1913,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
 
 int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const double* wants) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && (!rows || !wants))) return c->fail(DM_E_INVAL, "bad update");
   if (n == 0) return DM_OK;
@@ -1983,6 +1940,7 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
 int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, const uint64_t* mask, int64_t n,
                                const double* wants) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (first_row < 0 || (first_row & 63) || nwords < 0 || n < 0 || (nwords > 0 && !mask) || (n > 0 && !wants))
     return c->fail(DM_E_INVAL, "bad masked update (first_row must be a multiple of 64)");
@@ -2011,7 +1969,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
          "masked update");
   DM_HIP(c, hipMemcpyAsync(c->h_flags, c->upd_flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream),
          "update flags");
-  DM_HIP(c, hipStreamSynchronize(c->stream), "update");
+  if (int rs = c->synced("update")) return rs;
   const uint32_t f = *c->h_flags;
   if (f & kUpdRange) return c->fail(DM_E_RANGE, "mask bit past the store's end");
   if (f & kUpdCount) return c->fail(DM_E_INVAL, "packed values must match the mask's set bits");
@@ -2022,6 +1980,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
 
 int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad release");
   if (n == 0) return DM_OK;
@@ -2047,6 +2006,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
 // later part (k_carry_reject); earlier parts stay applied.
 int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (!b) return c->fail(DM_E_INVAL, "null batch");
   const int64_t nw = b->wants_nwords, nm = b->wants_n, nr = b->release_n, nu = b->upsert_n;
@@ -2149,7 +2109,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     DM_HIP(c, launch_clear_rows(nu, c->st_rows.p, c->N, c->row_bits.p, st), "clear rows");
   }
   DM_HIP(c, hipMemcpyAsync(c->h_bat_flags, F, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "batch flags");
-  DM_HIP(c, hipStreamSynchronize(st), "batch");
+  if (int rs = c->synced("batch")) return rs;
   c->have_result = false;
   const uint32_t f0 = c->h_bat_flags[0], f1 = c->h_bat_flags[1], f2 = c->h_bat_flags[2];
   auto reject = [&](uint32_t f, const char* part) -> int {
@@ -2205,6 +2165,7 @@ int dm_aggregate_bands(const double* wants, const int64_t* num_clients, int64_t 
 
 int dm_publish_totals(dm_ctx* c, void* dst) {
   DM_ENTER(c);
+  DM_STORE_OK(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (!dst) return c->fail(DM_E_INVAL, "null destination");
   if (!c->pub_sync.p) {
@@ -2287,6 +2248,7 @@ int dm_hier_pipeline(dm_ctx* leaf, int on) {
 // must precede it on the root's stream.
 int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns, dm_ctx* leaf, int server) {
   DM_ENTER(root);
+  DM_STORE_OK(root);
   if (!root->store_loaded || !root->cfg_loaded) return root->fail(DM_E_STATE, "root store / config not loaded");
   if (!gathered || !leaf) return root->fail(DM_E_INVAL, "null gathered buffer or leaf context");
   if (n_servers <= 0 || n_servers > kHierMaxServers)
@@ -2388,7 +2350,7 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
       leaf->xs_signal_lazy(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot]);
     else
       DM_HIP(root,
-             leaf->xs_signal(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot], leaf->xs_ready_value),
+             leaf->xs_signal(dm_ctx::XS_READY0 + slot, root->stream, &leaf->tpl_ready[slot]),
              "staged templates");
     leaf->tpl_pending.push_back(dm_ctx::Staged{slot, leaf->ticks_issued});
   } else if (!same) {  // the leaf's next tick after its new templates
@@ -2409,6 +2371,8 @@ struct RcclApi {
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
 };
 static const RcclApi* rccl_api() {
@@ -2426,7 +2390,10 @@ static const RcclApi* rccl_api() {
       api.all_gather = (decltype(api.all_gather))dlsym(api.h, "ncclAllGather");
       api.comm_destroy = (decltype(api.comm_destroy))dlsym(api.h, "ncclCommDestroy");
       api.error_string = (decltype(api.error_string))dlsym(api.h, "ncclGetErrorString");
-      if (!api.get_unique_id || !api.comm_init_rank || !api.all_gather || !api.comm_destroy || !api.error_string)
+      api.comm_count = (decltype(api.comm_count))dlsym(api.h, "ncclCommCount");
+      api.comm_user_rank = (decltype(api.comm_user_rank))dlsym(api.h, "ncclCommUserRank");
+      if (!api.get_unique_id || !api.comm_init_rank || !api.all_gather || !api.comm_destroy || !api.error_string ||
+          !api.comm_count || !api.comm_user_rank)
         api.h = nullptr;
     }
   }
@@ -2469,6 +2436,17 @@ int dm_hier_comm_init(dm_ctx* root, const void* id, int nranks, int rank) {
   return DM_OK;
 }
 
+int dm_hier_comm_info(dm_ctx* root, int* nranks, int* rank) {
+  DM_CHECK_CTX(root);
+  if (!nranks || !rank) return root->fail(DM_E_INVAL, "null output");
+  if (!root->nccl_comm) return root->fail(DM_E_STATE, "the exchange has no RCCL communicator");
+  const RcclApi* r = rccl_api();
+  ncclResult_t e = r->comm_count(root->nccl_comm, nranks);
+  if (e == ncclSuccess) e = r->comm_user_rank(root->nccl_comm, rank);
+  if (e != ncclSuccess) return root->fail(DM_E_HIP, std::string("ncclCommCount/UserRank: ") + r->error_string(e));
+  return DM_OK;
+}
+
 int dm_hier_attach(dm_ctx* leaf, dm_ctx* root, int server, void* const* ring, int nring, void* gathered,
                    void* exchange_stream) {
   DM_ENTER(root);
@@ -2492,7 +2470,7 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
   DM_CHECK_CTX(root);
   if (!leaf || root->hs_leaf != leaf) return root->fail(DM_E_STATE, "dm_hier_attach this leaf to the root first");
   int rc = dm_apportion(leaf, now_ns, DM_WRITEBACK | DM_ASYNC | DM_DEFER_JOIN);
-  if (rc) return rc;
+  if (rc) return root->fail(rc, "leaf tick: " + leaf->err);  // callers read the root's message
   const int64_t n = (int64_t)root->hs_ring.size();
   void* block = root->hs_ring[(size_t)((leaf->pub_k - 1) % n)];  // what this tick published
   const int G = root->hier_G;
@@ -2510,14 +2488,22 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
     else
       DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->exchange order");
     const size_t bytes = (size_t)root->hier_stride * 16;
+    // (timed as one class on the exchange stream while profiling: bench.py's exchange_us)
     if (root->nccl_comm) {  // every server's block, in server order, over xGMI
       const RcclApi* r = rccl_api();
-      const ncclResult_t e = r->all_gather(block, root->hs_gathered, (size_t)root->hier_stride * 2, ncclFloat64,
-                                           root->nccl_comm, root->stream);
+      ncclResult_t e = ncclSuccess;
+      DM_HIP(root, root->timed(KC_HIER_GATHER, root->stream, [&] {
+               e = r->all_gather(block, root->hs_gathered, (size_t)root->hier_stride * 2, ncclFloat64,
+                                 root->nccl_comm, root->stream);
+               return hipSuccess;
+             }),
+             "gather");
       if (e != ncclSuccess) return root->fail(DM_E_HIP, std::string("ncclAllGather: ") + r->error_string(e));
     } else {  // a rehearsal: this server's slot only
-      DM_HIP(root, hipMemcpyAsync((char*)root->hs_gathered + (size_t)root->hs_server * bytes, block, bytes,
-                                  hipMemcpyDeviceToDevice, root->stream),
+      DM_HIP(root, root->timed(KC_HIER_GATHER, root->stream, [&] {
+               return hipMemcpyAsync((char*)root->hs_gathered + (size_t)root->hs_server * bytes, block, bytes,
+                                     hipMemcpyDeviceToDevice, root->stream);
+             }),
              "gather (local)");
     }
     gathered = root->hs_gathered;
@@ -2544,6 +2530,12 @@ int dm_set_profiling(dm_ctx* c, int on) {
   DM_CHECK_CTX(c);
   c->profiling = on != 0;
   return DM_OK;
+}
+
+int dm_kernel_class_names(const char** names, int max) {
+  if (!names && max > 0) return DM_E_INVAL;
+  for (int i = 0; i < KC_COUNT && i < max; ++i) names[i] = kClassNames[i];
+  return KC_COUNT;
 }
 
 int dm_kernel_times(dm_ctx* c, dm_kernel_time* out, int max) {
@@ -2578,8 +2570,8 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   v[2 + kNumBins] = (int64_t)c->h_chunks.size();
   v[3 + kNumBins] = c->N;
   v[4 + kNumBins] = c->bin6_wide ? 1 : 0;  // bin 6 on 512 x 8 workgroups (else 256 x 16)
-  v[5 + kNumBins] = c->redo_cap;          // chunks of one resource the speculative chain takes at most
-  v[6 + kNumBins] = c->spec_fits ? 1 : 0;  // the store's largest resource within it
+  v[5 + kNumBins] = c->redo_cap;  // 3/4 of the redo's full-build workgroups the GPU holds at once
+  v[6 + kNumBins] = 1;            // every store may speculate (the redo by teams has no bound)
   const int n = 7 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;

@@ -22,7 +22,6 @@ doorman_amd so the HIP library binds to torch's HIP runtime.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 
@@ -149,14 +148,10 @@ class HierarchicalTick:
         # a second stream costs per step (~20 us of idle GPU each): the
         # exchange then runs on the leaf's stream, still one tick of lag (staged slots).
         self.stream = torch.cuda.Stream(device=dev)
-        # (DM_HIER_XSTREAM=1: a second stream at G = 1 too -- tests and A/B runs of the
-        # cross-stream form on one GPU)
-        own = self.G > 1 or os.environ.get("DM_HIER_XSTREAM", "0") == "1"
+        own = self.G > 1
         # the exchange's kernels (gather, root round) are few and short, but beside a leaf tick
         # that fills every CU they wait for slots: a high-priority queue lets them in first
-        # (DM_XPRIO=0: normal priority)
-        prio = -1 if os.environ.get("DM_XPRIO", "1") != "0" else 0
-        self.xstream = torch.cuda.Stream(device=dev, priority=prio) if pipelined and own else self.stream
+        self.xstream = torch.cuda.Stream(device=dev, priority=-1) if pipelined and own else self.stream
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
         # lag: ticks of lag of the pipelined templates (dm_hier_pipeline): default 1 with the
@@ -178,6 +173,17 @@ class HierarchicalTick:
         gp = self.gathered[0].data_ptr() if self.G > 1 else None
         _lib.check(L.dm_hier_attach(leaf._ctx, root._ctx, self.g, ring, nbuf, gp, self.xstream.cuda_stream),
                    root._ctx, L)
+
+    def comm_info(self):
+        """(ranks, rank) as the library's RCCL communicator itself reports them
+        (dm_hier_comm_info: ncclCommCount / ncclCommUserRank), or None without one."""
+        from . import _lib
+        if self.native != "rccl":
+            return None
+        L = self.root._L
+        n, r = ctypes.c_int(0), ctypes.c_int(-1)
+        _lib.check(L.dm_hier_comm_info(self.root._ctx, ctypes.byref(n), ctypes.byref(r)), self.root._ctx, L)
+        return n.value, r.value
 
     def exchange(self, now_ns: int):
         """publish -> all-gather -> the root's round -> this server's new templates

@@ -38,7 +38,12 @@
 extern "C" {
 #endif
 
-#define DM_ABI_VERSION 3
+/* 4 (round 5): dm_kernel_class_names, dm_hier_comm_info; dm_plan_info's slot 14 is the
+   redo's co-resident workgroup bound (was the per-chunk redo's chunk bound), slot 15
+   always 1; the DM_* environment switches other than the test hooks are gone
+   (INTEGRATION.md §5).  3 (round 4): dm_hier_attach / dm_hier_step / dm_rccl_unique_id /
+   dm_hier_comm_init and DM_E_INTERNAL added, dm_set_large_path and DM_LARGE_* removed. */
+#define DM_ABI_VERSION 4
 
 /* return codes */
 #define DM_OK 0
@@ -351,6 +356,10 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns);
 #define DM_RCCL_ID_BYTES 128
 int dm_rccl_unique_id(void* id_out);
 int dm_hier_comm_init(dm_ctx* root, const void* id, int nranks, int rank);
+/* What the exchange's communicator itself reports (ncclCommCount, ncclCommUserRank):
+ * the ranks RCCL saw and this one's rank, so a multi-GPU run can show that RCCL, not
+ * only torch.distributed, spans the node.  DM_E_STATE without a communicator. */
+int dm_hier_comm_info(dm_ctx* root, int* nranks, int* rank);
 
 /* Large resources (more than 4096 rows) run on 2048-row chunks in stream-ordered
  * launches (Clean + speculative round 1, round 1 again only where Clean released
@@ -364,15 +373,16 @@ int dm_hier_comm_init(dm_ctx* root, const void* id, int nranks, int rank);
 int dm_set_profiling(dm_ctx* ctx, int on);
 /* fills up to max entries; returns the number of kernel classes (>= 0) */
 int dm_kernel_times(dm_ctx* ctx, dm_kernel_time* out, int max);
+/* the names dm_kernel_times reports, in its order (static strings; no context or GPU
+ * needed); returns the number of classes */
+int dm_kernel_class_names(const char** names, int max);
 int dm_reset_kernel_times(dm_ctx* ctx);
 /* plan summary of the loaded store: small packs, items per dispatch bin (sub16x4,
  * sub32x4, wave64x4, block128x4, block128x8, block256x8, the 2049-4096-row bin,
  * sub8x2, sub16x2), large resources, large chunks, leases, then 1 when the
- * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), the most chunks
- * (2048 rows each) one resource may have for the speculative chain with
- * DM_REDO_TEAM=0 (the per-chunk redo kernel's co-resident workgroups), and 1 when
- * the store may speculate (always with the default redo by teams; else only with
- * its largest resource within that bound); returns 16 */
+ * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), 3/4 of the redo's
+ * full-build workgroups the GPU holds at once (its grid bound), and 1 (every store may
+ * speculate: the redo by teams needs only 64 co-resident workgroups); returns 16 */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),

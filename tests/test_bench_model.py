@@ -36,6 +36,43 @@ def test_kernel_units_cover_every_row_once():
     assert units["block128x8"] == (513 + 1024, 2)
 
 
+def test_every_kernel_class_has_units():
+    """Every class dm_kernel_times can report (the library's own list, no GPU needed) has
+    a units entry, so the roofline never falls back to whole-snapshot bytes; an unknown
+    name raises."""
+    from doorman_amd import _lib
+    sizes = np.array([1, 9, 300, 5000])
+    snap = W.make_snapshot(sizes, 1.0, 0.0, 1, W.NOW_NS + W.NS, W.FAIR_SHARE, 10.0)
+    units = bench.kernel_units(snap)
+    names = _lib.kernel_class_names()
+    assert "large_spec" in names and "large_redo" in names and "hier_gather" in names
+    missing = [n for n in names if n not in units]
+    assert not missing, missing
+    run = {"ktimes": {"no_such_kernel": (1, 1.0)}, "stream_ms": 1.0}
+    try:
+        bench.roofline_of("c2", snap, run, 1, False)
+    except KeyError:
+        pass
+    else:
+        raise AssertionError("an unknown kernel class must raise")
+
+
+def test_large_spec_roofline_counts_the_large_class_only():
+    """C2's speculative chain: the roofline divides by the > 4096-row class's bytes (24 B
+    per lease: the steady tick reads no subclients column), not the whole snapshot's
+    (round 4's line reported 3x the real fraction)."""
+    snap = bench.make_workload("c2", 0)
+    sizes = np.diff(snap["seg_off"])
+    big = sizes > 4096
+    run = {"ktimes": {"large_spec": (10, 1.0), "subs_merged": (10, 0.5)}, "stream_ms": 1.0, "dense_frac": 1.0}
+    r = bench.roofline_of("c2", snap, run, 10, False)
+    assert r["kernel"] == "large_spec"
+    assert r["leases_per_launch"] == int(sizes[big].sum()) and r["resources_per_launch"] == int(big.sum())
+    assert r["algorithmic_bytes_per_launch"] == 24 * int(sizes[big].sum()) + 97 * int(big.sum())
+    # C2's large class: 6.08M leases in 244 resources
+    assert 6.0e6 < r["leases_per_launch"] < 6.2e6 and r["resources_per_launch"] == 244
+
+
 def test_self_check_root_round_matches_the_reference_model():
     """bench.root_round_one (the N > 1 exchange self-check's restatement of the sharded
     root round, one row per resource) against the hierarchy model (tests/hier_model.py:

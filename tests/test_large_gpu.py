@@ -257,7 +257,7 @@ def test_large_writeback_ticks_with_uniform_counts_other_than_one(cols):
         eng.close()
 
 
-@pytest.mark.parametrize("redo", ["1", "2", "team0"])
+@pytest.mark.parametrize("redo", ["1", "2"])
 def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     """The speculative chain (k_large_spec: one pass under the totals the resource's
     last tick verified, checked bit for bit per resource; k_large_redo for the
@@ -269,7 +269,7 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     the two engines' stores hold the same released rows and subclients and running
     sums within the oracle tolerance (their reductions run in different orders); in
     the steady ticks the speculative engine launches no pass of the chain.  redo:
-    DM_REDO_LIGHT (1: k_large_redo's light build after a redo-free tick, so the lapse
+    DM_REDO_LIGHT (1: the redo's light build after a redo-free tick, so the lapse
     tick's redo runs on it; 2: the light build on every tick)."""
     from doorman_amd.engine import Engine
     rng = np.random.default_rng(8080)
@@ -286,9 +286,6 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
     monkeypatch.setenv("DM_SPEC_CHAIN", "0")
     chain = Engine(0)
     monkeypatch.delenv("DM_SPEC_CHAIN")
-    if redo == "team0":  # k_large_redo (one workgroup per chunk) instead of the teams
-        monkeypatch.setenv("DM_REDO_TEAM", "0")
-        redo = "1"
     monkeypatch.setenv("DM_REDO_LIGHT", redo)
     spec = Engine(0)
     try:
@@ -352,19 +349,12 @@ def test_speculative_chain_against_the_chain_and_the_oracle(monkeypatch, redo):
         spec.close()
 
 
-@pytest.mark.parametrize("team", ["0", "1"])
-def test_resource_beyond_the_redo_bound(monkeypatch, team):
-    """team = 0 (DM_REDO_TEAM=0, k_large_redo: one workgroup per chunk, all of a marked
-    resource's chunks waiting for one another): the redo holds at most as many chunks
-    as the GPU holds its workgroups at once (plan_info spec_max_chunks: 3/4 of CUs x
-    workgroups per CU of its full build, the other classes' streams holding slots too).
-    A store whose largest resource has more chunks never speculates: its writeback
-    ticks (alternate columns, where the speculative chain would otherwise run) take the
-    four-launch chain and match the oracle.  team = 1 (the default, k_large_redo_team:
-    at most kTeamMax workgroups per resource): no bound, the same store speculates, a
-    wants refresh makes the big resource's redo run, and every tick matches the
-    oracle."""
-    monkeypatch.setenv("DM_REDO_TEAM", team)
+def test_resource_beyond_the_co_resident_redo_workgroups():
+    """A resource with more chunks than 3/4 of the redo workgroups the GPU holds at once
+    (plan_info redo_resident_cap: the bound round 4's per-chunk redo had, every chunk of a
+    marked resource waiting for the others): the redo by teams (at most kTeamMax
+    workgroups per resource) has no such bound, so the store speculates, a wants refresh
+    makes the big resource's redo run, and every tick matches the oracle."""
     rng = np.random.default_rng(909)
     probe = _engine()
     try:
@@ -373,7 +363,7 @@ def test_resource_beyond_the_redo_bound(monkeypatch, team):
         probe.load(small)
         info = probe.plan_info()
         assert info["spec_fits"] == 1
-        cap = info["spec_max_chunks"]
+        cap = info["redo_resident_cap"]
     finally:
         probe.close()
     assert 64 <= cap <= 4096, cap
@@ -384,7 +374,7 @@ def test_resource_beyond_the_redo_bound(monkeypatch, team):
     eng = _engine()
     try:
         eng.load(snap)
-        assert eng.plan_info()["spec_fits"] == (0 if team == "0" else 1)
+        assert eng.plan_info()["spec_fits"] == 1
         eng.set_profiling(True)
         now = NOW
         so = np.asarray(snap["seg_off"])
@@ -398,9 +388,7 @@ def test_resource_beyond_the_redo_bound(monkeypatch, team):
             eng.reset_kernel_times()
             eng.apportion(now, writeback=True, wb_columns="alternate")
             kt = eng.kernel_times()
-            if team == "0":
-                assert "large_spec" not in kt and kt.get("large_a", (0, 0))[0] == 1, kt
-            elif i >= 1:
+            if i >= 1:
                 assert kt.get("large_spec", (0, 0))[0] == 1, kt
             st = eng.read_store()
             live = ref["expiry_ns"] != W.RELEASED

@@ -64,24 +64,20 @@ def test_doc_examples_at_every_bin(eng, size, kind):
     assert_resources_match(snap, res, ref)
 
 
-@pytest.mark.parametrize("merge", ["0", "1"])
 @pytest.mark.parametrize("variant", ["uniform", "edge"])
-def test_sub_wave_bins_merged_and_separate(monkeypatch, merge, variant):
-    """The sub-wave bins (9-256 rows) in one launch (k_subs, the default) and one
-    launch per bin (DM_MERGE_SUBS=0) both match the oracle."""
-    from doorman_amd.engine import Engine
-    monkeypatch.setenv("DM_MERGE_SUBS", merge)  # read when the context is created
+def test_sub_wave_bins(eng, variant):
+    """The sub-wave bins (9-256 rows: 8 x 2, 16 x 2, 16 x 4, 32 x 4, 64 x 4 lane groups)
+    in their one launch (k_subs) match the oracle."""
     rng = np.random.default_rng(77)
     sizes = np.concatenate([binned_sizes(rng), rng.integers(9, 257, 300)])
     snap = snapshot_with_sizes(rng, sizes, edge=variant == "edge")
-    with Engine(0) as e:
-        e.load(snap)
-        e.apportion(NOW)
-        gets, exp = e.leases()
-        res = e.resources()
+    eng.load(snap)
+    eng.apportion(NOW)
+    gets, exp = eng.leases()
+    res = eng.resources()
     ref = O.apportion(snap, NOW)
-    assert_leases_match(snap, gets, exp, ref, f"merge={merge} {variant}")
-    assert_resources_match(snap, res, ref, f"merge={merge} {variant}")
+    assert_leases_match(snap, gets, exp, ref, variant)
+    assert_resources_match(snap, res, ref, variant)
 
 
 @pytest.mark.parametrize("seed", range(6))

@@ -529,7 +529,9 @@ def test_decide_100k_requests_on_a_100k_client_resource():
     device time (dm_kernel_times "decide") is reported and must stay under 10 ms; the
     first 3000 requests are checked against the oracle's literal replay (a prefix of a
     sequential round is decided exactly as in the whole round), the whole round's
-    capacity bookkeeping by the grants' sum."""
+    capacity bookkeeping by the grants' sum (asserted <= capacity, every grant >= 0),
+    and a 9000-request round (several event blocks and scan chunks) request by request
+    against the sequential replay."""
     rng = np.random.default_rng(5)
     n = 100_000
     snap = _fast_round_snapshot(rng, np.array([n], np.int64), [W.FAIR_SHARE], [1])
@@ -552,6 +554,26 @@ def test_decide_100k_requests_on_a_100k_client_resource():
     cap = snap["capacity"][0]
     assert float_close(gets[:3000], ref_g, np.full(3000, cap)).all()
     np.testing.assert_array_equal(exp[:3000], ref_e)
+    # the whole round's capacity bookkeeping: no grant negative, and the grants (every
+    # client's lease after the round: each asked once) never exceed the capacity
+    assert (gets >= 0).all()
+    assert gets.sum() <= cap * (1 + 1e-12), (gets.sum(), cap)
     print(f"\n100k requests on a 100k-client resource: {ms:.2f} ms of device time (bar 10 ms); "
           f"sum of grants {gets.sum():.6f} of capacity {cap}")
     assert launches == 1 and ms < 10.0, ms
+    # beyond the first 3000: a round of 9000 requests on the same resource (4 Assign-event
+    # blocks of kFdBlock = 2048, 9 scan chunks of kFdChunk = 1024) decided by the fast path
+    # and by the sequential replay (DM_DECIDE_FAST=0) must agree on every request
+    k = 9000
+    out = []
+    for fast in (True, False):
+        e = _decide_engine(fast)
+        try:
+            e.load(snap)
+            out.append(e.decide(NOW, rows[:k], has[:k], wants[:k], sub[:k]))
+        finally:
+            e.close()
+    (gf, ef), (gs, es) = out
+    np.testing.assert_array_equal(ef, es)
+    ok = float_close(gf, gs, np.full(k, cap))
+    assert ok.all(), np.flatnonzero(~ok)[:10]
