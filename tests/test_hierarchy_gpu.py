@@ -660,6 +660,10 @@ def test_native_step_matches_the_python_step(G, native):
         # slot 0 through ncclAllGather): the RCCL leg's plumbing on one GPU
         kw = {"comm_id": rccl_unique_id(), "comm_ranks": 1} if mode == "rccl" else {}
         ht = HierarchicalTick(torch, leaf, root, R, G, 0, gather, shard_lo=lo, pipelined=True, native=mode, **kw)
+        if mode == "rccl":  # what RCCL itself counts (dm_hier_comm_info): one rank, this one
+            assert ht.comm_info() == (1, 0)
+        else:
+            assert ht.comm_info() is None
         if G > 1:
             ht.gathered[0].copy_(torch.from_numpy(others).to(ht.gathered[0].device))
         out = []
