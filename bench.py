@@ -141,7 +141,7 @@ def kernel_units(snap):
         m = (sizes >= lo) & (sizes <= hi)
         return int(sizes[m].sum()), int(m.sum())
     small = sizes <= 8
-    units["small_packed"] = (int(sizes[small].sum()), int(small.sum()))
+    units["small_tiles"] = (int(sizes[small].sum()), int(small.sum()))
     for name, lo, hi in _SUB_EDGES + _GROUP_EDGES:
         units[name] = rng(lo, hi)
     units["subs_merged"] = rng(9, 256)  # the sub-wave bins in one launch (k_subs)
@@ -728,6 +728,8 @@ def main():
                     help="native: each step is one library call (dm_hier_step: the leaf tick, then the block "
                          "gathered by the library's own RCCL communicator and the root round on the exchange "
                          "stream); python: the same sequence from Python (torch.distributed all-gather)")
+    ap.add_argument("--lib", default=None,
+                    help="A/B only: another build of the same ABI (tools/ab_libs/*.so) for every engine of the run")
     ap.add_argument("--check-corrupt", action="store_true",
                     help="test only: the exchange self-check's step corrupts one rank's gathered copy (expect "
                          "dist.consistent false)")
@@ -855,7 +857,7 @@ def main():
         the snapshot and the engines (closed by the caller)."""
         snap = make_workload(args.workload, s_rank, s_world, layout)
         R = len(snap["seg_off"]) - 1
-        eng = Engine(dev_index)
+        eng = Engine(dev_index, args.lib)
         eng.load(snap)
         now = W.NOW_NS
         # back-to-back ticks: a forked tick's class streams join lazily (DM_DEFER_JOIN)
@@ -865,7 +867,7 @@ def main():
             step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup + 1)
         if hier:
             from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
-            root = Engine(dev_index)
+            root = Engine(dev_index, args.lib)
             if layout == "sharded":  # the root of the whole snapshot: one row per resource (its owner's)
                 bounds = c3_bounds(s_world)
                 root.load(root_snapshot(C3_R, 1, W.FAIR_SHARE, 1000.0, lease_length_s=20))
@@ -938,7 +940,7 @@ def main():
             root = None
         for name in ("c1", "c2", "c4"):
             snapx = make_workload(name, 0)
-            ex = Engine(dev_index)
+            ex = Engine(dev_index, args.lib)
             ex.load(snapx)
             if name == "c4":
                 kx = min(args.steps, 10)

@@ -22,7 +22,7 @@ constexpr uint32_t kSubReleased = 0xFFFFFFFFu;
 constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 
 // Dispatch bins.  A segment of n rows goes to:
-//   n <= kSmallMax            : wave-packed literal path (many resources per wave)
+//   n <= kSmallMax            : tiles of consecutive resources, one resource per thread (k_tile_small)
 //   n <= 16 / 32              : 8- / 16-lane groups, 2 rows per lane, 8 / 4 resources per wave (bins 7, 8)
 //   n <= 64 / 128             : 16- / 32-lane groups, 4 rows per lane, 4 / 2 resources per wave (bins 0, 1)
 //   n <= 256                  : one wave per resource, 4 rows per lane (4 resources per workgroup)
@@ -30,7 +30,11 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 //   n <= 2048                 : one 256-thread workgroup, 8 rows per thread (bin 5)
 //   n <= 4096                 : one 256 x 16 or 512 x 8 workgroup (bin 6, kBin6Wide below)
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
-constexpr int kSmallMax = 8;
+#ifndef DM_SMALL_MAX
+#define DM_SMALL_MAX 8
+#endif
+constexpr int kSmallMax = DM_SMALL_MAX;
+static_assert(kSmallMax <= 32, "k_tile_small keeps a resource's live rows in a 32-bit mask");
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
 constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, block256x8, the 2049-4096 bin, sub8x2, sub16x2
@@ -43,13 +47,23 @@ constexpr int kBin6Wide = 9;
 // from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
 constexpr int64_t kStreamBytes = 1LL << 30;
 
-struct Pack {  // a run of consecutive small resources covering <= 64 rows
+
+// A tile of consecutive small resources (n <= kSmallMax) for k_tile_small: at most
+// kTileRes resources and kTileRows rows, one 256-thread workgroup each.  Its rows are
+// staged in LDS by the whole workgroup (coalesced), each resource's record is loaded by
+// the thread that decides it (consecutive records: coalesced too), so a tile needs one
+// memory round trip before its compute instead of the packed kernel's two.
+#ifndef DM_TILE_ROWS
+#define DM_TILE_ROWS 1024
+#endif
+constexpr int kTileRows = DM_TILE_ROWS;
+constexpr int kTileRes = 256;
+struct Tile {
   int32_t first_seg;
-  int32_t nseg;  // <= 63
+  int32_t nseg;    // <= kTileRes
   int64_t row0;
-  int32_t nrows;  // <= 64
-  int32_t maxlen;  // longest resource in the pack
-  uint8_t rel[64];  // rel[k] = seg_off[first_seg + k] - row0, k <= nseg (inline: no dependent load)
+  int32_t nrows;   // <= kTileRows
+  int32_t pad;
 };
 
 struct WorkItem {  // one resource of a size bin: no dependent load before its rows

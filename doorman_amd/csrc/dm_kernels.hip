@@ -14,6 +14,7 @@
 //
 // Float semantics follow Go on amd64: binary64, no FMA contraction (built with
 // -ffp-contract=off), minF = `l > r ? r : l`, IEEE division by zero.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "dm_kernel_util.h"
@@ -348,8 +349,12 @@ __device__ __forceinline__ void tick_done_signal(const TickDone& td) {
   }
 }
 
+#ifndef DM_DENSE8_WAVES
+#define DM_DENSE8_WAVES 1
+#endif
+constexpr int kDense8Waves = DM_DENSE8_WAVES;
 template <int G, int R>
-__global__ __launch_bounds__(G) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
+__global__ __launch_bounds__(G, (G == 128 && R == 8) ? kDense8Waves : 1) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
                                                    int32_t* queue, int32_t* qcnt, int par,
                                                    int32_t* general_list, int32_t* general_count,
                                                    int32_t* guard) {
@@ -452,117 +457,139 @@ __global__ __launch_bounds__(256, 5) void k_subs(DevParams p, SubBins sb, int32_
 }
 
 // --------------------------------------------------------------------------
-// Wave-packed small resources (n <= kSmallMax): one wave covers a run of whole
-// resources; every lane evaluates its own client literally, looping over its
-// resource's rows in row order (shuffles).  Sums are taken in the same order as
-// the oracle, so this path is bit-exact against it.
-// Shuffle budget per loop step: wants (2 dwords) + one int carrying subclients
-// and the live bit (sl = live ? s : ~s); Clean's loop runs only when a row of the
-// pack expired; the owners' sumHas loop moves gets - has as one double.
+// Tiles of small resources (n <= kSmallMax), one 256-thread workgroup per tile
+// (dm_device.h Tile): the workgroup stages the tile's rows in LDS with lane-strided
+// (coalesced) loads while thread k loads resource k's offsets and record (consecutive
+// records: coalesced as well) -- one memory round trip, where the packed kernel waits
+// for its pack, then for the records its rows' resources name.  Thread k then decides
+// resource k literally, in row order (sums in the oracle's order: bit-exact), from LDS;
+// the gets go back to global memory row-parallel (coalesced), and each resource's
+// record from its thread (coalesced).
 // --------------------------------------------------------------------------
-
-__global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restrict__ packs, int npacks) {
-  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wv >= npacks) return;
+// This wave's share of a copy of nwords 4-B words from global memory into LDS by
+// LDS-DMA (global_load_lds_dword: no VGPR destination, 256 B per wave-instruction;
+// lanes past the end re-read the last word into the slack of the last 256 B).  The
+// workgroup's next __syncthreads() waits for the copies (vmcnt(0) before the barrier).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+__device__ __forceinline__ void glds_words(const void* src, void* lds_dst, int nwords, int wave, int nwaves) {
   const int lane = threadIdx.x & 63;
-  const Pack& pkr = packs[wv];
-  const int first_seg = pkr.first_seg, nseg = pkr.nseg, nrows = pkr.nrows, maxlen = pkr.maxlen;
-  const int64_t row0 = pkr.row0;
-  const bool valid = lane < nrows;
-  // rows first (every lane loads; lanes past the pack re-read its last row), so
-  // their latency overlaps the segment search and the config gathers
-  double w = 0.0, h = 0.0;
-  int sr = 0;  // raw subclients word (expiry encoding, dm_device.h)
-  const int64_t myrow = row0 + (valid ? lane : (nrows > 0 ? nrows - 1 : 0));
-  if (nrows > 0) {
-    w = p.wants[myrow];
-    h = p.has[myrow];
-    sr = p.sub[myrow];
+  for (int c = wave; c * 64 < nwords; c += nwaves) {
+    const int i = c * 64 + lane;
+    const int ii = i < nwords ? i : nwords - 1;
+    __builtin_amdgcn_global_load_lds((glob_void_t*)((const uint32_t*)src + ii), (lds_void_t*)((uint32_t*)lds_dst + c * 64),
+                                     4, 0, 0);
   }
-  // resource of this row: last k < nseg with rel[k] <= lane (offsets relative to row0)
-  const int offk = lane <= nseg ? (int)pkr.rel[lane] : INT32_MAX;
-  int k = 0;
-#pragma unroll
-  for (int step = 32; step > 0; step >>= 1) {
-    const int c = k + step;
-    const int oc = shfl_i(offk, c < 64 ? c : 63);
-    if (c < nseg && oc <= lane) k = c;
-  }
-  // shuffles run on the full wave (a masked-off source lane would read stale LDS)
-  const int seg_lo = shfl_i(offk, k), seg_hi = shfl_i(offk, k + 1 < 64 ? k + 1 : 63);
-  const int lo = valid ? seg_lo : 0;
-  const int hi = valid ? seg_hi : 0;
-  const int seg = first_seg + k;
+}
+
+#ifndef DM_TILE_WAVES
+#define DM_TILE_WAVES 1
+#endif
+constexpr int kTileWaves = DM_TILE_WAVES;
+struct TileLds {
+  double w[kTileRows];
+  double h[kTileRows];  // a row's has, then its gets (only the row's own resource thread reads either)
+  int32_t sr[kTileRows];
+  uint8_t lv[kTileRows];
+};
+
+__global__ __launch_bounds__(256, kTileWaves) void k_tile_small(DevParams p, const Tile* __restrict__ tiles) {
+  __shared__ TileLds L;
+  const Tile tl = tiles[blockIdx.x];
+  const int t = threadIdx.x;
+  const int64_t row0 = tl.row0;
+  const int nrows = tl.nrows, nseg = tl.nseg;
+  constexpr int K = kTileRows / 256;
+  // the records first, then the rows: every load of the tile is in flight before the
+  // first is consumed (the LDS stores below)
+  const bool own = t < nseg;
+  const int seg = tl.first_seg + (own ? t : 0);
+  const int64_t lo64 = p.seg_off[seg], hi64 = p.seg_off[seg + 1];
   const Res rs = load_res(p, seg);
-  int64_t e = rs.follow_exp;  // followers expire with their resource; explicit rows read theirs
-  if (__any(nrows > 0 && any_explicit(rs)) && any_explicit(rs) && sub_explicit(sr)) e = p.expiry[myrow];
-  if (sub_released(sr)) e = kReleased;
-  const int lv = (valid && !(p.now > e)) ? 1 : 0;  // store.go:174
-  int s = sub_value(sr);
-  if (!valid) {
-    w = 0.0;
-    h = 0.0;
-    s = 0;
+#ifdef DM_TILE_GLDS
+  if (nrows > 0) {  // LDS-DMA: the rows reach LDS without VGPRs
+    const int wave = t >> 6;
+    glds_words(p.wants + row0, L.w, 2 * nrows, wave, 4);
+    glds_words(p.has + row0, L.h, 2 * nrows, wave, 4);
+    glds_words(p.sub + row0, L.sr, nrows, wave, 4);
   }
-  const int sl = lv ? s : ~s;  // subclients and the live bit in one shuffle
-
-  // Clean, in row order (store.go:169-181)
-  long long count = 0;
-  double sh = 0.0, sw = 0.0;
-  if (p.recompute) {
-    for (int q = 0; q < maxlen; ++q) {
-      const int j = lo + q;
-      const double hj = shfl_d(h, j & 63), wj = shfl_d(w, j & 63);
-      const int sj = shfl_i(sl, j & 63);
-      if (j < hi) {
-        sh += hj - 0.0;
-        sw += wj - 0.0;
-        count += sj >= 0 ? sj : ~sj;
-      }
-    }
-  } else {
-    count = rs.agg_count;
-    sh = rs.agg_has;
-    sw = rs.agg_wants;
-  }
-  // some row of the pack expired since its last writeback tick (a row already marked
-  // released holds zeros: subtracting it changes nothing -- C2's 1 % of released rows
-  // sent about half of the packs through this loop every tick)
-  if (__any(valid && !lv && !sub_released(sr))) {
-    for (int q = 0; q < maxlen; ++q) {
-      const int j = lo + q;
-      const double hj = shfl_d(h, j & 63), wj = shfl_d(w, j & 63);
-      const int sj = shfl_i(sl, j & 63);
-      if (j < hi && sj < 0) {
-        sw -= wj;
-        sh -= hj;
-        count -= ~sj;
-      }
+#else
+  double wv[K], hv[K];
+  int sv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k * 256 < nrows) {  // uniform
+      const int i = k * 256 + t;
+      const unsigned u = (unsigned)(i < nrows ? i : nrows - 1);
+      wv[k] = *col_at(p.wants + row0, u);
+      hv[k] = *col_at(p.has + row0, u);
+      sv[k] = *col_at(p.sub + row0, u);
     }
   }
-
-  const double C = rs.C;
-  const double eq = C / (double)count;
-  double g = 0.0;
-  // every lane runs every loop (shuffles need the full wave); results are
-  // selected per lane afterwards.
-  double x = 0.0, y = 0.0;
-  long long wi = 0;
-  const bool ps = !rs.learning && rs.kind == 2, fs = !rs.learning && rs.kind == 3;
-  if (__any(ps || fs)) {
-    for (int q = 0; q < maxlen; ++q) {
-      const int j = lo + q;
-      const double wj = shfl_d(w, j & 63);
-      const int sj = shfl_i(sl, j & 63);
-      if (j < hi && sj >= 0) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = k * 256 + t;
+    if (k * 256 < nrows && i < nrows) {
+      L.w[i] = wv[k];
+      L.h[i] = hv[k];
+      L.sr[i] = sv[k];
+    }
+  }
+#endif
+  __syncthreads();
+  if (own) {
+    const int lo = (int)(lo64 - row0), hi = (int)(hi64 - row0);
+    // Clean (store.go:169-181): the store's running sums (or rebuilt from every row in
+    // row order, recompute mode) less the rows that expired, in row order
+    long long count;
+    double sh, sw;
+    if (p.recompute) {
+      count = 0;
+      sh = 0.0;
+      sw = 0.0;
+      for (int q = lo; q < hi; ++q) {
+        sh += L.h[q] - 0.0;
+        sw += L.w[q] - 0.0;
+        count += sub_value(L.sr[q]);
+      }
+    } else {
+      count = rs.agg_count;
+      sh = rs.agg_has;
+      sw = rs.agg_wants;
+    }
+    const bool expl_rows = any_explicit(rs);
+    unsigned live = 0;  // bit q - lo (n <= kSmallMax)
+    for (int q = lo; q < hi; ++q) {
+      const int32_t raw = L.sr[q];
+      int64_t e = rs.follow_exp;
+      if (expl_rows && sub_explicit(raw)) e = p.expiry[row0 + q];
+      if (sub_released(raw)) e = kReleased;
+      const bool lv = !(p.now > e);  // store.go:174
+      live |= (lv ? 1u : 0u) << (q - lo);
+      if (!lv && !sub_released(raw)) {  // expired: Clean releases it (a released row holds zeros)
+        sw -= L.w[q];
+        sh -= L.h[q];
+        count -= sub_value(raw);
+      }
+    }
+    const double C = rs.C;
+    const double eq = C / (double)count;
+    const bool ps = !rs.learning && rs.kind == 2, fs = !rs.learning && rs.kind == 3;
+    double x = 0.0, y = 0.0;
+    long long wi = 0;
+    if (ps || fs) {
+      for (int q = lo; q < hi; ++q) {
+        if (!(live >> (q - lo) & 1)) continue;
+        const double wj = L.w[q];
+        const int sj = sub_value(L.sr[q]);
         if (ps) {
-          const double e2 = eq * (double)sj;
+          const double e2 = eq * (double)sj;  // algorithm.go:273
           if (wj < e2)
             x += e2 - wj;
           else
             y += wj - e2;
-        } else if (fs) {
-          const double d = (double)sj * eq;
+        } else {
+          const double d = (double)sj * eq;  // algorithm.go:160
           if (wj < d)
             x += d - wj;
           else if (wj > d)
@@ -570,74 +597,76 @@ __global__ __launch_bounds__(256) void k_small(DevParams p, const Pack* __restri
         }
       }
     }
+    double osh = sh;  // Assign: sumHas += gets - has (store.go:156), row order
+    double Tc = 0.0;  // round 2 at the last threshold asked for (uniform subclients: one per resource)
+    AggC cc{0.0, 0};
+    bool have_c = false;
+    for (int q = lo; q < hi; ++q) {
+      const bool lv = live >> (q - lo) & 1;
+      L.lv[q] = lv ? 1 : 0;
+      if (!p.writeback) __builtin_nontemporal_store(lv ? (int64_t)rs.exp_out : (int64_t)kReleased,
+                                                    col_at(p.out_expiry + row0, (uint32_t)q));
+      if (!lv) {
+        L.h[q] = 0.0;
+        continue;
+      }
+      const double w = L.w[q], h = L.h[q];
+      const int s = sub_value(L.sr[q]);
+      double g;
+      if (rs.learning) {
+        g = h;  // Learn (algorithm.go:297-302)
+      } else if (rs.kind == 0) {
+        g = w;  // NoAlgorithm
+      } else if (rs.kind == 1) {
+        g = minF(C, w);  // Static
+      } else if (ps) {
+        const double epc = eq * (double)s;  // :233
+        const double unused = C - sh + h;   // :239
+        g = (sw <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (x / y), unused);
+      } else {
+        double T = 0.0;
+        if (!fs_stage01(w, h, s, C, sh, eq, x, wi, &g, &T)) {
+          if (!have_c || __double_as_longlong(T) != __double_as_longlong(Tc)) {
+            cc = AggC{0.0, 0};
+            for (int j = lo; j < hi; ++j) {  // round 2 at this row's threshold (algorithm.go:189-204)
+              if (!(live >> (j - lo) & 1)) continue;
+              const double wj = L.w[j];
+              const int sj = sub_value(L.sr[j]);
+              if (!(wj > (double)sj * eq)) continue;
+              if (wj < T)
+                cc.ee += T - wj;
+              else if (wj > T)
+                cc.sgt += sj;
+            }
+            Tc = T;
+            have_c = true;
+          }
+          g = fs_stage2(w, h, s, C, sh, eq, x, wi, T, cc);
+        }
+      }
+      L.h[q] = g;
+      osh += g - h;
+    }
+    write_resource(p, seg, rs, Clean{count, osh, sw}, 0.0);
   }
-  double T = 0.0;
-  bool need2 = false;
-  if (rs.learning) {
-    g = h;
-  } else if (rs.kind == 0) {
-    g = w;
-  } else if (rs.kind == 1) {
-    g = minF(C, w);
-  } else if (rs.kind == 2) {
-    const double epc = eq * (double)s;
-    const double unused = C - sh + h;
-    g = (sw <= C || w <= epc) ? minF(w, unused) : minF(epc + (w - epc) * (x / y), unused);
-  } else {
-    need2 = !fs_stage01(w, h, s, C, sh, eq, x, wi, &g, &T);
-  }
-  const int any2 = __any(need2 && valid && lv);
-  if (any2) {
-    AggC c{0.0, 0};
-    for (int q = 0; q < maxlen; ++q) {
-      const int j = lo + q;
-      const double wj = shfl_d(w, j & 63);
-      const int sj = shfl_i(sl, j & 63);
-      if (j < hi && sj >= 0 && wj > (double)sj * eq) {
-        if (wj < T)
-          c.ee += T - wj;
-        else if (wj > T)
-          c.sgt += sj;
+  __syncthreads();
+  // the leases, row-parallel (put_live / put_released of the packed kernel)
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = k * 256 + t;
+    if (k * 256 < nrows && i < nrows) {
+      const int32_t raw = L.sr[i];
+      if (L.lv[i]) {
+        __builtin_nontemporal_store(L.h[i], col_at(p.out_gets + row0, (uint32_t)i));
+        if (p.writeback && raw < 0) *col_at(p.out_sub + row0, (uint32_t)i) = raw & 0x7FFFFFFF;
+      } else {
+        __builtin_nontemporal_store(0.0, col_at(p.out_gets + row0, (uint32_t)i));
+        if (p.writeback && !sub_released(raw)) {
+          *col_at(p.out_wants + row0, (uint32_t)i) = 0.0;
+          *col_at(p.out_sub + row0, (uint32_t)i) = (int32_t)kSubReleased;
+        }
       }
     }
-    if (need2) g = fs_stage2(w, h, s, C, sh, eq, x, wi, T, c);
-  }
-  if (valid) {
-    if (lv)
-      put_live(p, row0, (uint32_t)lane, g, rs, sr);
-    else
-      put_released(p, row0, (uint32_t)lane, sr);
-  }
-  // per-resource results: lane k (< nseg) owns resource first_seg + k
-  const bool owner = lane < nseg;
-  const int olo = offk;
-  const int ohi = shfl_i(offk, lane + 1 < 64 ? lane + 1 : 63);
-  long long ocount = __shfl(count, olo & 63, 64);
-  double osh = shfl_d(sh, olo & 63), osw = shfl_d(sw, olo & 63);
-  const double gh = g - h;  // Assign: sumHas += gets - has (store.go:156)
-  for (int q = 0; q < maxlen; ++q) {
-    const int j = olo + q;
-    const double dj = shfl_d(gh, j & 63);
-    const int sj = shfl_i(sl, j & 63);
-    if (owner && j < ohi && sj >= 0) osh += dj;
-  }
-  // the record's expiries from the resource's first row lane (no second config load)
-  Res ors;
-  ors.exp_out = shfl_any(rs.exp_out, olo & 63);
-  ors.follow_exp = shfl_any(rs.follow_exp, olo & 63);
-  ors.xstate = shfl_i(rs.xstate, olo & 63);
-  if (owner) {
-    const int oseg = first_seg + lane;
-    if (olo == ohi) {  // resource without rows
-      ocount = p.recompute ? 0 : p.agg[oseg].count;
-      osh = p.recompute ? 0.0 : p.agg[oseg].sum_has;
-      osw = p.recompute ? 0.0 : p.agg[oseg].sum_wants;
-      ors.exp_out = p.now + (int64_t)p.cfg[oseg].lease_len_s * kNs;
-      ors.follow_exp = p.agg[oseg].follow_exp;
-      ors.xstate = p.expl[oseg];
-    }
-    Clean oc{ocount, osh, osw};
-    write_resource(p, oseg, ors, oc, 0.0);
   }
 }
 
@@ -2989,9 +3018,9 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
 // --------------------------------------------------------------------------
 // host-side launchers (called by dm_runtime.cpp)
 // --------------------------------------------------------------------------
-hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st) {
+hipError_t launch_tile_small(const DevParams& p, const Tile* tiles, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_small<<<(n + 3) / 4, 256, 0, st>>>(p, packs, n);
+  k_tile_small<<<n, 256, 0, st>>>(p, tiles);
   return hipGetLastError();
 }
 
@@ -3021,16 +3050,32 @@ hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, in
 // The 128-thread bins (3: 128 x 4, 4: 128 x 8) split by the dense hint: the dense
 // kernel over every item, then the rest kernel over what it queued (two launches,
 // timed separately).
+// done (optional): an event the launch itself completes (hipExtLaunchKernel's stop
+// event: no marker packet of its own on the queue), for another stream to wait on
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                            int32_t* glist, int32_t* gcount, int32_t* guard, hipStream_t st) {
+                            int32_t* glist, int32_t* gcount, int32_t* guard, hipEvent_t done, hipStream_t st) {
   if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)n);
   switch (bin) {
-    case 3: k_block_dense<128, 4><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
-    case 4: k_block_dense<128, 8><<<n, 128, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
-    case 5: k_block_dense<256, 8><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
-    case 6: k_block_dense<256, 16><<<n, 256, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard); break;
+    case 3:
+      hipExtLaunchKernelGGL(k_block_dense<128, 4>, grid, dim3(128), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
+                            par, glist, gcount, guard);
+      break;
+    case 4:
+      hipExtLaunchKernelGGL(k_block_dense<128, 8>, grid, dim3(128), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
+                            par, glist, gcount, guard);
+      break;
+    case 5:
+      hipExtLaunchKernelGGL(k_block_dense<256, 8>, grid, dim3(256), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
+                            par, glist, gcount, guard);
+      break;
+    case 6:
+      hipExtLaunchKernelGGL(k_block_dense<256, 16>, grid, dim3(256), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
+                            par, glist, gcount, guard);
+      break;
     case kBin6Wide:
-      k_block_dense<512, 8><<<n, 512, 0, st>>>(p, segs, n, queue, qcnt, par, glist, gcount, guard);
+      hipExtLaunchKernelGGL(k_block_dense<512, 8>, grid, dim3(512), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
+                            par, glist, gcount, guard);
       break;
     default: return hipErrorInvalidValue;
   }
@@ -3203,3 +3248,4 @@ hipError_t launch_hier_tick(const DevParams& p, const HierArgs& ha, hipStream_t 
 }
 
 }  // namespace dm
+

@@ -20,12 +20,12 @@
 #include "dm_device.h"
 
 namespace dm {
-hipError_t launch_small(const DevParams& p, const Pack* packs, int n, hipStream_t st);
+hipError_t launch_tile_small(const DevParams& p, const Tile* tiles, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                            int32_t* glist, int32_t* gcount, int32_t* guard, hipStream_t st);
+                            int32_t* glist, int32_t* gcount, int32_t* guard, hipEvent_t done, hipStream_t st);
 hipError_t launch_tick_done(const TickDone& td, hipStream_t st);
 int redo_blocks_per_cu();
 hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
@@ -119,7 +119,7 @@ enum KClass {
 };
 // bin 6 (2049-4096 rows) runs on 256 x 16 or 512 x 8 workgroups (kBin6Wide):
 // "block2k4k" names the bin, dm_plan_info says which shape ran
-const char* kClassNames[KC_COUNT] = {"small_packed", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
+const char* kClassNames[KC_COUNT] = {"small_tiles", "sub16x4",    "sub32x4",    "wave64x4",   "block128x4",
                                      "block128x8",   "block256x8", "block2k4k",  "sub8x2",    "sub16x2",
                                      "large_a",      "large_b",
                                      "large_c",      "large_map",  "large_fin",  "general",    "store_upsert",
@@ -164,9 +164,9 @@ struct dm_ctx {
   hipStream_t stream = nullptr;
   // auxiliary streams: independent size bins of one tick run concurrently
   static constexpr int kAux = 4;
-  // auxiliary stream of each work class: bins 0..kNumBins-1, small packs, large chain
+  // auxiliary stream of each work class: bins 0..kNumBins-1, small tiles, large chain
   // (round 4 moved every bin to each other stream in A/Bs: this split won every one)
-  static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (packs alone)
+  static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (small class alone)
   hipStream_t aux[kAux] = {};
   hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
@@ -297,11 +297,11 @@ struct dm_ctx {
     return hipSuccess;
   }
   // plan
-  std::vector<Pack> h_packs;
+  std::vector<Tile> h_tiles;  // small resources (n <= kSmallMax) in tiles (k_tile_small)
   std::vector<WorkItem> h_bins[kNumBins];
   std::vector<Chunk> h_chunks;
   std::vector<LargeSeg> h_large;
-  DBuf<Pack> packs;
+  DBuf<Tile> tiles;
   DBuf<WorkItem> bins[kNumBins];
   DBuf<Chunk> chunks;
   DBuf<LargeSeg> large;
@@ -452,11 +452,15 @@ struct dm_ctx {
   uint32_t* tick_ctr = nullptr;
   uint64_t tick_seq = 0;          // the last tick's number
   bool tick_flagged = false;      // ... and whether it stores it
+  bool tick_evented = false;      // ... as the completion of its dense kernel (tick_ev, DM_TICK_EVENT)
+  static constexpr int kTickEv = 8;
+  hipEvent_t tick_ev[kTickEv] = {};
   // set by the first consumer on another stream (the exchange's order, a template
   // slot's reuse): before it, no tick stores the word (k_tick_done costs ~5 us of the
   // leaf's queue when nothing waits on it, e.g. the exchange on the leaf's own stream)
   bool tick_word_wanted = false;
   uint64_t tpl_free_seq[kTplSlots] = {};  // a slot is free once the word reaches this (0: use tpl_free)
+  bool tpl_free_ev[kTplSlots] = {};       // ... signalled by the tick's event (tick_ev) instead of the word
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
   bool profiling = false;
@@ -535,7 +539,7 @@ struct dm_ctx {
     seg_off.release(); blk_seg.release(); wants.release(); has.release(); sub.release(); expiry.release();
     agg.release(); expl.release(); cfg.release(); cold.release();
     out_gets.release(); out_expiry.release(); res.release();
-    packs.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
+    tiles.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
     for (int i = 0; i < kSplitBins; ++i) {
       dq_list[i].release();
       dq_cnt[i].release();
@@ -631,43 +635,39 @@ static int bin_of(int64_t n) {
 }
 
 static void build_plan(dm_ctx* c) {
-  c->h_packs.clear();
+  c->h_tiles.clear();
   for (auto& b : c->h_bins) b.clear();
   c->h_chunks.clear();
   c->h_large.clear();
   const std::vector<int64_t>& off = c->h_seg_off;
-  Pack cur{};
-  bool open = false;
   std::vector<int64_t> large;
-  auto close = [&]() {
-    if (open) c->h_packs.push_back(cur);
-    open = false;
+  // runs of consecutive small resources: tiles of at most kTileRes resources and kTileRows rows
+  Tile tc{};
+  bool topen = false;
+  auto tclose = [&]() {
+    if (topen) c->h_tiles.push_back(tc);
+    topen = false;
   };
   for (int64_t r = 0; r < c->R; ++r) {
     const int64_t n = off[r + 1] - off[r];
     if (n <= kSmallMax) {
-      if (open && (cur.nrows + n > 64 || cur.nseg >= 63)) close();
-      if (!open) {
-        cur = Pack{};
-        cur.first_seg = (int32_t)r;
-        cur.row0 = off[r];
-        open = true;
+      if (topen && (tc.nrows + n > kTileRows || tc.nseg >= kTileRes)) tclose();
+      if (!topen) {
+        tc = Tile{(int32_t)r, 0, off[r], 0, 0};
+        topen = true;
       }
-      cur.rel[cur.nseg] = (uint8_t)(off[r] - cur.row0);
-      cur.nseg += 1;
-      cur.rel[cur.nseg] = (uint8_t)(off[r] + n - cur.row0);
-      cur.nrows += (int32_t)n;
-      cur.maxlen = std::max<int32_t>(cur.maxlen, (int32_t)n);
+      tc.nseg += 1;
+      tc.nrows += (int32_t)n;
       continue;
     }
-    close();
+    tclose();
     if (n <= kLargeMin) {
       c->h_bins[bin_of(n)].push_back(WorkItem{(int32_t)r, (int32_t)n, off[r]});
     } else {
       large.push_back(r);
     }
   }
-  close();
+  tclose();
   // Large resources largest first: a resource is verified by its last-arriving chunk,
   // and the largest's verification (the longest canonical trees) then overlaps the
   // other chunks instead of trailing the launch.  Each resource's chunks stay
@@ -697,7 +697,7 @@ static hipError_t check_dense(dm_ctx* c, int i, int b, hipStream_t s) {
 
 static int upload_plan(dm_ctx* c) {
   hipStream_t st = c->stream;
-  DM_HIP(c, upload(c->packs, c->h_packs.data(), c->h_packs.size(), st), "plan packs");
+  DM_HIP(c, upload(c->tiles, c->h_tiles.data(), c->h_tiles.size(), st), "plan tiles");
   for (int b = 0; b < kNumBins; ++b) DM_HIP(c, upload(c->bins[b], c->h_bins[b].data(), c->h_bins[b].size(), st), "plan bins");
   DM_HIP(c, upload(c->chunks, c->h_chunks.data(), c->h_chunks.size(), st), "plan chunks");
   DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
@@ -927,6 +927,7 @@ int dm_create(int device, dm_ctx** out) {
     }
   }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
+  for (int i = 0; i < dm_ctx::kTickEv && e == hipSuccess; ++i) e = hipEventCreate(&c->tick_ev[i]);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
     dm_destroy(c);
@@ -971,6 +972,8 @@ void dm_destroy(dm_ctx* c) {
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_bat)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : c->tick_ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->tick_word) (void)hipFree(c->tick_word);
@@ -1192,6 +1195,7 @@ static int commit_templates(dm_ctx* c) {
   // the next exchange into it waits for the ticks enqueued so far: on the tick-done word
   // when the last of them stores it, else on a (lazy) event
   c->tpl_free_seq[take] = c->tick_flagged ? c->tick_seq : 0;
+  c->tpl_free_ev[take] = c->tick_flagged && c->tick_evented;
   c->xs_signal_lazy(dm_ctx::XS_FREE0 + take, c->stream, &c->tpl_free[take]);
   c->tpl_free_rec[take] = true;
   c->tpl_free_slots.push_back(take);
@@ -1206,6 +1210,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   c->ticks_issued += 1;
   c->tick_seq += 1;
   c->tick_flagged = false;
+  c->tick_evented = false;
   const bool wb = flags & DM_WRITEBACK;
   DevParams p{};
   p.seg_off = c->seg_off.p;
@@ -1290,14 +1295,14 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   unsigned used = 0;  // auxiliary streams with work this tick
   for (int b = 0; b < kNumBins; ++b)
     if (!c->h_bins[b].empty()) used |= 1u << c->class_stream[b];
-  if (!c->h_packs.empty()) used |= 1u << c->class_stream[kNumBins];
+  if (!c->h_tiles.empty()) used |= 1u << c->class_stream[kNumBins];
   if (nch > 0) used |= 1u << c->class_stream[kNumBins + 1];
   const bool fork = __builtin_popcount(used) > 1;
   int nonempty_bins = 0;
   for (int b = 0; b < kNumBins; ++b) nonempty_bins += c->h_bins[b].empty() ? 0 : 1;
   // one work class on the context stream, no kernel after its split bin's rest kernel:
   // that kernel can store the tick-done word
-  const bool one_class = !fork && nch == 0 && c->h_packs.empty() && !general && nonempty_bins == 1;
+  const bool one_class = !fork && nch == 0 && c->h_tiles.empty() && !general && nonempty_bins == 1;
   auto cls_stream = [&](int cls) { return fork ? c->aux[c->class_stream[cls]] : st; };
   hipStream_t s_large = cls_stream(kNumBins + 1), s_small = cls_stream(kNumBins);
   if (!fork) {  // everything on the context stream, after any deferred class work
@@ -1417,12 +1422,21 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
           td = TickDone{c->tick_word, c->tick_ctr, c->tick_seq};
           c->tick_flagged = true;
         }
+        // the tick's last kernel: with DM_TICK_EVENT its own completion is the tick-done
+        // signal (an event in a ring, waited on by the exchange stream), else k_tick_done
+        hipEvent_t done = nullptr;
+#ifdef DM_TICK_EVENT
+        if (skip && td.word) {
+          done = c->tick_ev[c->tick_seq % dm_ctx::kTickEv];
+          c->tick_evented = true;
+        }
+#endif
         DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
                  return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc,
-                                         skip ? c->d_guard + i : nullptr, s);
+                                         skip ? c->d_guard + i : nullptr, done, s);
                }),
                "group kernel (dense split)");
-        if (skip && td.word) DM_HIP(c, launch_tick_done(td, s), "tick-done word");
+        if (skip && td.word && !done) DM_HIP(c, launch_tick_done(td, s), "tick-done word");
         if (!skip) {
           // the rest kernel strides over whatever the dense kernel queues; its grid is
           // only sized from the last split tick's queue (a hint: correctness never
@@ -1443,8 +1457,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
            "group kernel");
     if (b >= 3 && b < 3 + dm_ctx::kSplitBins && wb) DM_HIP(c, check_dense(c, b - 3, b, s), "dense split check");
   }
-  if (!c->h_packs.empty())
-    DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_small(p, c->packs.p, (int)c->h_packs.size(), s_small); }),
+  if (!c->h_tiles.empty())
+    DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_tile_small(p, c->tiles.p, (int)c->h_tiles.size(), s_small); }),
            "small kernel");
   if (fork) {
     c->aux_pending = true;
@@ -2293,10 +2307,15 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     if (leaf->stream != root->stream) leaf->tick_word_wanted = true;
     if (leaf->stream == root->stream) {
       // stream order: the ticks that read the slot's old templates precede this round
-    } else if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0)  // the ticks that read the slot's old
-      DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tpl_free_seq[slot],  // templates
-                                        hipStreamWaitValueGte, ~0ull),                           // are done
-             "template slot");
+    } else if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0) {  // the ticks that read the slot's old
+      if (leaf->tpl_free_ev[slot])                                            // templates are done
+        DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tpl_free_seq[slot] % dm_ctx::kTickEv], 0),
+               "template slot");
+      else
+        DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tpl_free_seq[slot],
+                                          hipStreamWaitValueGte, ~0ull),
+               "template slot");
+    }
     else if (leaf->tpl_free_rec[slot])
       DM_HIP(root, leaf->xs_wait(leaf->tpl_free[slot], root->stream), "template slot");
     tcfg = leaf->tpl_cfg[slot].p;
@@ -2482,7 +2501,10 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
     if (leaf->stream != root->stream) leaf->tick_word_wanted = true;
     if (leaf->stream == root->stream) {
       // stream order
-    } else if (leaf->tick_flagged)
+    } else if (leaf->tick_flagged && leaf->tick_evented)
+      DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tick_seq % dm_ctx::kTickEv], 0),
+             "leaf->exchange order");
+    else if (leaf->tick_flagged)
       DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tick_seq, hipStreamWaitValueGte, ~0ull),
              "leaf->exchange order");
     else
@@ -2564,7 +2586,7 @@ int dm_reset_kernel_times(dm_ctx* c) {
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
   int64_t v[7 + kNumBins];
-  v[0] = (int64_t)c->h_packs.size();
+  v[0] = (int64_t)c->h_tiles.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
   v[2 + kNumBins] = (int64_t)c->h_chunks.size();

@@ -377,7 +377,7 @@ int dm_kernel_times(dm_ctx* ctx, dm_kernel_time* out, int max);
  * needed); returns the number of classes */
 int dm_kernel_class_names(const char** names, int max);
 int dm_reset_kernel_times(dm_ctx* ctx);
-/* plan summary of the loaded store: small packs, items per dispatch bin (sub16x4,
+/* plan summary of the loaded store: small-resource tiles, items per dispatch bin (sub16x4,
  * sub32x4, wave64x4, block128x4, block128x8, block256x8, the 2049-4096-row bin,
  * sub8x2, sub16x2), large resources, large chunks, leases, then 1 when the
  * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), 3/4 of the redo's

@@ -26,7 +26,7 @@ def test_kernel_units_cover_every_row_once():
                       4096, 4097, 9000])
     snap = W.make_snapshot(sizes, 1.0, 0.0, 1, W.NOW_NS + W.NS, W.FAIR_SHARE, 10.0)
     units = bench.kernel_units(snap)
-    bins = ["small_packed", "sub8x2", "sub16x2", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8",
+    bins = ["small_tiles", "sub8x2", "sub16x2", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8",
             "block256x8", "block2k4k", "large_a"]
     assert sum(units[b][0] for b in bins) == int(sizes.sum())
     assert sum(units[b][1] for b in bins) == len(sizes)

@@ -155,7 +155,7 @@ def test_benched_c2_steady_state_against_the_oracle_at_full_size():
             eng.sync()
             _check(eng, host, pick, so, f"segment {si} ({ticks} ticks)")
         kt = eng.kernel_times()
-        for k in ("large_spec", "large_redo", "subs_merged", "small_packed"):
+        for k in ("large_spec", "large_redo", "subs_merged", "small_tiles"):
             assert kt.get(k, (0, 0))[0] >= 8, (k, kt)
         dense = sum(kt.get(n + "_dense", (0, 0))[0] for n in ("block128x4", "block128x8", "block256x8", "block2k4k"))
         rest = sum(kt.get(n + "_rest", (0, 0))[0] for n in ("block128x4", "block128x8", "block256x8", "block2k4k"))

@@ -295,7 +295,7 @@ def test_c2_zipf_full_size_sampled(eng):
     snap = W.c2()
     eng.load(snap)
     info = eng.plan_info()
-    assert info["leases"] == 13_970_034 and info["large_resources"] > 0 and info["small_packs"] > 0
+    assert info["leases"] == 13_970_034 and info["large_resources"] > 0 and info["small_tiles"] > 0
     eng.apportion(NOW)
     rng = np.random.default_rng(6)
     sample = np.unique(np.concatenate([[0, 1, 2, 3, 7, 100, 121, 122, 243, 244],

@@ -32,7 +32,7 @@ CLASS = [
     (r"k_block<256, 8(, \d)?>", "block256x8"), (r"k_block<512, 8(, \d)?>", "block2k4k"), (r"k_block<256, 16(, \d)?>", "block2k4k"), (r"k_block<512, 4(, \d)?>", "block512x4"), (r"k_block<1024, 4(, \d)?>", "block1024x4"),
     (r"k_wave<4(, \d)?>", "wave64x4"), (r"k_sub<16, 4>", "sub16x4"), (r"k_sub<32, 4>", "sub32x4"),
     (r"k_sub<8, 2>", "sub8x2"), (r"k_sub<16, 2>", "sub16x2"),
-    (r"k_small\b", "small_packed"), (r"k_subs\b", "subs_merged"), (r"k_large_a\b", "large_a"), (r"k_large_b\b", "large_b"),
+    (r"k_tile_small\b", "small_tiles"), (r"k_subs\b", "subs_merged"), (r"k_large_a\b", "large_a"), (r"k_large_b\b", "large_b"),
     (r"k_large_c\b", "large_c"), (r"k_large_map\b", "large_map"), (r"k_large_fin\b", "large_fin"),
     (r"k_general\b", "general"), (r"k_flat8\(", "ubench_flat8"), (r"k_flat8nt\(", "ubench_flat8nt"),
 ]
