@@ -30,10 +30,7 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 //   n <= 2048                 : one 256-thread workgroup, 8 rows per thread (bin 5)
 //   n <= 4096                 : one 256 x 16 or 512 x 8 workgroup (bin 6, kBin6Wide below)
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
-#ifndef DM_SMALL_MAX
-#define DM_SMALL_MAX 8
-#endif
-constexpr int kSmallMax = DM_SMALL_MAX;
+constexpr int kSmallMax = 8;  // (16 and 32 -- bins 7 and 8 in the tiles, one resource per thread -- lost: +8 / +25 us on C2)
 static_assert(kSmallMax <= 32, "k_tile_small keeps a resource's live rows in a 32-bit mask");
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
@@ -53,10 +50,7 @@ constexpr int64_t kStreamBytes = 1LL << 30;
 // staged in LDS by the whole workgroup (coalesced), each resource's record is loaded by
 // the thread that decides it (consecutive records: coalesced too), so a tile needs one
 // memory round trip before its compute instead of the packed kernel's two.
-#ifndef DM_TILE_ROWS
-#define DM_TILE_ROWS 1024
-#endif
-constexpr int kTileRows = DM_TILE_ROWS;
+constexpr int kTileRows = 1024;  // (512-row tiles: C2 +1.7 us)
 constexpr int kTileRes = 256;
 struct Tile {
   int32_t first_seg;
@@ -198,15 +192,6 @@ struct HetRes {
   int64_t bc[kHetBuckets];  // count of the wantExtra clients
 };
 
-// The tick-done word (dm_apportion): the rest kernel of a one-class split tick -- the
-// tick's last kernel -- stores the tick's sequence number once every workgroup of it has
-// finished, so another queue can wait for the tick on the word (a stream wait on a value)
-// and the tick's own queue gets no marker packet.
-struct TickDone {
-  uint64_t* word;  // signal memory; nullptr: none
-  uint32_t* ctr;   // arrival counter (its last arriver resets it)
-  uint64_t seq;
-};
 
 // row -> resource lookup for store updates: seg_off plus, for every block of
 // 2^kRowBlkShift rows, the resource holding its first row

@@ -334,27 +334,13 @@ __global__ __launch_bounds__(G, (G <= 256 && R == 8) ? 5 : 1) void k_block(DevPa
 // alive ~2 us longer, every tick of a dense store.
 // When the host skips k_block_rest (every item of the bin verified dense in this row
 // epoch, dm_runtime.cpp), `guard` (host-mapped) is set should the dense kernel queue
-// an item after all, which the host reports as DM_E_INTERNAL instead of leaving the
-// item undecided unnoticed; the tick-done word then comes from k_tick_done (one wave
-// after the dense kernel: 10^5 workgroups on one counter took 8 ms).
-__device__ __forceinline__ void tick_done_signal(const TickDone& td) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this workgroup's stores, seen from every XCD
-    const uint32_t old = __hip_atomic_fetch_add(td.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == gridDim.x - 1) {
-      __hip_atomic_store(td.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(td.word, td.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-#ifndef DM_DENSE8_WAVES
-#define DM_DENSE8_WAVES 1
-#endif
-constexpr int kDense8Waves = DM_DENSE8_WAVES;
+// an item after all, which the host reports as DM_E_INTERNAL (and refuses the store)
+// instead of leaving the item undecided unnoticed.  The tick's last kernel (this one,
+// or the rest kernel) is launched with the tick's stop event when another queue waits
+// for the tick (dm_runtime.cpp tick_ev).
+// (128 x 8 held to 7 waves per SIMD: 71 VGPRs + 20 B of spill, C3 430 -> 590 us; round 5.)
 template <int G, int R>
-__global__ __launch_bounds__(G, (G == 128 && R == 8) ? kDense8Waves : 1) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
+__global__ __launch_bounds__(G) void k_block_dense(DevParams p, WorkItem* __restrict__ items, int nitems,
                                                    int32_t* queue, int32_t* qcnt, int par,
                                                    int32_t* general_list, int32_t* general_count,
                                                    int32_t* guard) {
@@ -374,18 +360,10 @@ __global__ __launch_bounds__(G, (G == 128 && R == 8) ? kDense8Waves : 1) void k_
   }
 }
 
-__global__ __launch_bounds__(64) void k_tick_done(TickDone td) {
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(td.word, td.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
 template <int G, int R>
 __global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restrict__ items,
                                                   const int32_t* __restrict__ queue, int32_t* qcnt, int par,
-                                                  int32_t* host_count, int32_t* general_list, int32_t* general_count,
-                                                  TickDone td) {
+                                                  int32_t* host_count, int32_t* general_list, int32_t* general_count) {
   __shared__ Lds<G> lds;
   const int count = qcnt[par];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -400,7 +378,6 @@ __global__ __launch_bounds__(G) void k_block_rest(DevParams p, WorkItem* __restr
     group_segment<G, R, kRest>(p, items[idx], items + idx, threadIdx.x, lds, general_list, general_count);
     __syncthreads();  // the next item reuses the single-use LDS slots
   }
-  if (td.word) tick_done_signal(td);  // the tick is done once every workgroup of this, its last kernel, is
 }
 
 // One workgroup: how many items of a workgroup bin are not dense after a writeback
@@ -466,26 +443,6 @@ __global__ __launch_bounds__(256, 5) void k_subs(DevParams p, SubBins sb, int32_
 // the gets go back to global memory row-parallel (coalesced), and each resource's
 // record from its thread (coalesced).
 // --------------------------------------------------------------------------
-// This wave's share of a copy of nwords 4-B words from global memory into LDS by
-// LDS-DMA (global_load_lds_dword: no VGPR destination, 256 B per wave-instruction;
-// lanes past the end re-read the last word into the slack of the last 256 B).  The
-// workgroup's next __syncthreads() waits for the copies (vmcnt(0) before the barrier).
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glob_void_t;
-__device__ __forceinline__ void glds_words(const void* src, void* lds_dst, int nwords, int wave, int nwaves) {
-  const int lane = threadIdx.x & 63;
-  for (int c = wave; c * 64 < nwords; c += nwaves) {
-    const int i = c * 64 + lane;
-    const int ii = i < nwords ? i : nwords - 1;
-    __builtin_amdgcn_global_load_lds((glob_void_t*)((const uint32_t*)src + ii), (lds_void_t*)((uint32_t*)lds_dst + c * 64),
-                                     4, 0, 0);
-  }
-}
-
-#ifndef DM_TILE_WAVES
-#define DM_TILE_WAVES 1
-#endif
-constexpr int kTileWaves = DM_TILE_WAVES;
 struct TileLds {
   double w[kTileRows];
   double h[kTileRows];  // a row's has, then its gets (only the row's own resource thread reads either)
@@ -493,7 +450,7 @@ struct TileLds {
   uint8_t lv[kTileRows];
 };
 
-__global__ __launch_bounds__(256, kTileWaves) void k_tile_small(DevParams p, const Tile* __restrict__ tiles) {
+__global__ __launch_bounds__(256) void k_tile_small(DevParams p, const Tile* __restrict__ tiles) {
   __shared__ TileLds L;
   const Tile tl = tiles[blockIdx.x];
   const int t = threadIdx.x;
@@ -506,14 +463,6 @@ __global__ __launch_bounds__(256, kTileWaves) void k_tile_small(DevParams p, con
   const int seg = tl.first_seg + (own ? t : 0);
   const int64_t lo64 = p.seg_off[seg], hi64 = p.seg_off[seg + 1];
   const Res rs = load_res(p, seg);
-#ifdef DM_TILE_GLDS
-  if (nrows > 0) {  // LDS-DMA: the rows reach LDS without VGPRs
-    const int wave = t >> 6;
-    glds_words(p.wants + row0, L.w, 2 * nrows, wave, 4);
-    glds_words(p.has + row0, L.h, 2 * nrows, wave, 4);
-    glds_words(p.sub + row0, L.sr, nrows, wave, 4);
-  }
-#else
   double wv[K], hv[K];
   int sv[K];
 #pragma unroll
@@ -535,7 +484,6 @@ __global__ __launch_bounds__(256, kTileWaves) void k_tile_small(DevParams p, con
       L.sr[i] = sv[k];
     }
   }
-#endif
   __syncthreads();
   if (own) {
     const int lo = (int)(lo64 - row0), hi = (int)(hi64 - row0);
@@ -3082,11 +3030,6 @@ hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, 
   return hipGetLastError();
 }
 
-hipError_t launch_tick_done(const TickDone& td, hipStream_t st) {
-  k_tick_done<<<1, 64, 0, st>>>(td);
-  return hipGetLastError();
-}
-
 hipError_t launch_count_undense(const WorkItem* items, int n, unsigned long long* rec, unsigned long long epoch,
                                 hipStream_t st) {
   k_count_undense<<<1, 1024, 0, st>>>(items, n, rec, epoch);
@@ -3094,17 +3037,30 @@ hipError_t launch_count_undense(const WorkItem* items, int n, unsigned long long
 }
 
 hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, const TickDone& td,
+                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipEvent_t done,
                            hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const unsigned rg = (unsigned)std::max(1, std::min(n, rest_grid));
+  const dim3 rg((unsigned)std::max(1, std::min(n, rest_grid)));
   switch (bin) {
-    case 3: k_block_rest<128, 4><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
-    case 4: k_block_rest<128, 8><<<rg, 128, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
-    case 5: k_block_rest<256, 8><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
-    case 6: k_block_rest<256, 16><<<rg, 256, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td); break;
+    case 3:
+      hipExtLaunchKernelGGL(k_block_rest<128, 4>, rg, dim3(128), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
+                            host_count, glist, gcount);
+      break;
+    case 4:
+      hipExtLaunchKernelGGL(k_block_rest<128, 8>, rg, dim3(128), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
+                            host_count, glist, gcount);
+      break;
+    case 5:
+      hipExtLaunchKernelGGL(k_block_rest<256, 8>, rg, dim3(256), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
+                            host_count, glist, gcount);
+      break;
+    case 6:
+      hipExtLaunchKernelGGL(k_block_rest<256, 16>, rg, dim3(256), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
+                            host_count, glist, gcount);
+      break;
     case kBin6Wide:
-      k_block_rest<512, 8><<<rg, 512, 0, st>>>(p, segs, queue, qcnt, par, host_count, glist, gcount, td);
+      hipExtLaunchKernelGGL(k_block_rest<512, 8>, rg, dim3(512), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
+                            host_count, glist, gcount);
       break;
     default: return hipErrorInvalidValue;
   }

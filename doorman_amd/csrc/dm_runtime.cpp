@@ -26,7 +26,6 @@ hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
 hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
                             int32_t* glist, int32_t* gcount, int32_t* guard, hipEvent_t done, hipStream_t st);
-hipError_t launch_tick_done(const TickDone& td, hipStream_t st);
 int redo_blocks_per_cu();
 hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
                              const Partials& P, const SpecArgs& S, int redo_grid, int32_t* glist, int32_t* gcount,
@@ -34,7 +33,7 @@ hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks,
 hipError_t launch_count_undense(const WorkItem* items, int n, unsigned long long* rec, unsigned long long epoch,
                                 hipStream_t st);
 hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* queue, int32_t* qcnt, int par,
-                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, const TickDone& td,
+                           int32_t* host_count, int rest_grid, int32_t* glist, int32_t* gcount, hipEvent_t done,
                            hipStream_t st);
 hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls, int nls,
                         const Partials& P, int32_t* glist, int32_t* gcount, hipStream_t st);
@@ -443,24 +442,22 @@ struct dm_ctx {
   std::vector<Staged> tpl_pending;          // oldest first
   std::vector<int> tpl_free_slots;
   int64_t ticks_issued = 0;
-  // The tick-done word (TickDone): ticks numbered by tick_seq (never reset); a one-class
-  // split tick's rest kernel stores its number when the tick is done.  Another queue
-  // waits on the word (hipStreamWaitValue64) instead of an event recorded on this queue
-  // (each marker on the leaf's queue cost a ~10-us bubble per N = 8 shard step).
-  // nullptr when the device cannot wait on stream values: events then.
-  uint64_t* tick_word = nullptr;
-  uint32_t* tick_ctr = nullptr;
+  // The tick-done signal: ticks numbered by tick_seq (never reset).  The last kernel of
+  // a one-class split tick (C1, C3: the dense kernel, or the rest kernel after it) is
+  // launched with a stop event (hipExtLaunchKernel: the kernel's own completion signal,
+  // no marker packet of its own on the leaf's queue -- each marker cost a ~10-us bubble
+  // per N = 8 shard step), one event per tick in a ring; another queue waits on it.
+  // Round 4 stored a word from a one-wave k_tick_done after the dense kernel (5 us of
+  // the leaf's queue): the N = 8 rehearsal step 60.2-60.7 -> 58.7-58.8 us (round 5,
+  // gpurun_out/r5b2shard, three alternations).
   uint64_t tick_seq = 0;          // the last tick's number
-  bool tick_flagged = false;      // ... and whether it stores it
-  bool tick_evented = false;      // ... as the completion of its dense kernel (tick_ev, DM_TICK_EVENT)
-  static constexpr int kTickEv = 8;
+  bool tick_flagged = false;      // ... and whether its last kernel completes tick_ev[tick_seq % kTickEv]
+  static constexpr int kTickEv = 16;
   hipEvent_t tick_ev[kTickEv] = {};
   // set by the first consumer on another stream (the exchange's order, a template
-  // slot's reuse): before it, no tick stores the word (k_tick_done costs ~5 us of the
-  // leaf's queue when nothing waits on it, e.g. the exchange on the leaf's own stream)
-  bool tick_word_wanted = false;
-  uint64_t tpl_free_seq[kTplSlots] = {};  // a slot is free once the word reaches this (0: use tpl_free)
-  bool tpl_free_ev[kTplSlots] = {};       // ... signalled by the tick's event (tick_ev) instead of the word
+  // slot's reuse): before it, no tick carries the event
+  bool tick_signal_wanted = false;
+  uint64_t tpl_free_seq[kTplSlots] = {};  // a slot is free once this tick's event completed (0: use tpl_free)
   uint32_t* h_flags = nullptr; // pinned host mirror of upd_flags
   // profiling
   bool profiling = false;
@@ -910,22 +907,6 @@ int dm_create(int device, dm_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
-  if (e == hipSuccess) {
-    int can = 0;
-    if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && can &&
-        hipExtMallocWithFlags((void**)&c->tick_word, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess &&
-        hipMalloc((void**)&c->tick_ctr, sizeof(uint32_t)) == hipSuccess &&
-        hipMemset(c->tick_word, 0, sizeof(uint64_t)) == hipSuccess &&
-        hipMemset(c->tick_ctr, 0, sizeof(uint32_t)) == hipSuccess) {
-      e = hipDeviceSynchronize();
-    } else {  // events only
-      (void)hipGetLastError();
-      if (c->tick_word) (void)hipFree(c->tick_word);
-      if (c->tick_ctr) (void)hipFree(c->tick_ctr);
-      c->tick_word = nullptr;
-      c->tick_ctr = nullptr;
-    }
-  }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
   for (int i = 0; i < dm_ctx::kTickEv && e == hipSuccess; ++i) e = hipEventCreate(&c->tick_ev[i]);
   if (e != hipSuccess) {
@@ -976,8 +957,6 @@ void dm_destroy(dm_ctx* c) {
   for (auto ev : c->tick_ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-  if (c->tick_word) (void)hipFree(c->tick_word);
-  if (c->tick_ctr) (void)hipFree(c->tick_ctr);
   delete c;
 }
 
@@ -1195,7 +1174,6 @@ static int commit_templates(dm_ctx* c) {
   // the next exchange into it waits for the ticks enqueued so far: on the tick-done word
   // when the last of them stores it, else on a (lazy) event
   c->tpl_free_seq[take] = c->tick_flagged ? c->tick_seq : 0;
-  c->tpl_free_ev[take] = c->tick_flagged && c->tick_evented;
   c->xs_signal_lazy(dm_ctx::XS_FREE0 + take, c->stream, &c->tpl_free[take]);
   c->tpl_free_rec[take] = true;
   c->tpl_free_slots.push_back(take);
@@ -1210,7 +1188,6 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   c->ticks_issued += 1;
   c->tick_seq += 1;
   c->tick_flagged = false;
-  c->tick_evented = false;
   const bool wb = flags & DM_WRITEBACK;
   DevParams p{};
   p.seg_off = c->seg_off.p;
@@ -1417,26 +1394,18 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
         const uint64_t* rec = c->h_rec + 2 * i;
         const bool skip = __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
                           __atomic_load_n(rec, __ATOMIC_RELAXED) == 0;
-        TickDone td{nullptr, nullptr, 0};
-        if (one_class && c->tick_word && c->tick_word_wanted) {
-          td = TickDone{c->tick_word, c->tick_ctr, c->tick_seq};
+        // the tick's last kernel (the dense kernel, or the rest kernel after it) completes
+        // the tick's event when another queue waits for the tick (tick_flagged)
+        hipEvent_t done = nullptr;
+        if (one_class && c->tick_signal_wanted) {
+          done = c->tick_ev[c->tick_seq % dm_ctx::kTickEv];
           c->tick_flagged = true;
         }
-        // the tick's last kernel: with DM_TICK_EVENT its own completion is the tick-done
-        // signal (an event in a ring, waited on by the exchange stream), else k_tick_done
-        hipEvent_t done = nullptr;
-#ifdef DM_TICK_EVENT
-        if (skip && td.word) {
-          done = c->tick_ev[c->tick_seq % dm_ctx::kTickEv];
-          c->tick_evented = true;
-        }
-#endif
         DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
                  return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc,
-                                         skip ? c->d_guard + i : nullptr, done, s);
+                                         skip ? c->d_guard + i : nullptr, skip ? done : nullptr, s);
                }),
                "group kernel (dense split)");
-        if (skip && td.word && !done) DM_HIP(c, launch_tick_done(td, s), "tick-done word");
         if (!skip) {
           // the rest kernel strides over whatever the dense kernel queues; its grid is
           // only sized from the last split tick's queue (a hint: correctness never
@@ -1444,7 +1413,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
           const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
           DM_HIP(c, timed(KC_REST3 + i, s, [&] {
                    return launch_bin_rest(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
-                                          rest_grid, gl, gc, td, s);
+                                          rest_grid, gl, gc, done, s);
                  }),
                  "group kernel (dense split)");
           c->dq_par[i] ^= 1;
@@ -2304,17 +2273,12 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     slot = leaf->tpl_free_slots.front();
     DM_HIP(root, leaf->tpl_cfg[slot].ensure((size_t)leaf->R), "template slot");
     DM_HIP(root, leaf->tpl_cold[slot].ensure((size_t)leaf->R), "template slot");
-    if (leaf->stream != root->stream) leaf->tick_word_wanted = true;
+    if (leaf->stream != root->stream) leaf->tick_signal_wanted = true;
     if (leaf->stream == root->stream) {
       // stream order: the ticks that read the slot's old templates precede this round
     } else if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0) {  // the ticks that read the slot's old
-      if (leaf->tpl_free_ev[slot])                                            // templates are done
-        DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tpl_free_seq[slot] % dm_ctx::kTickEv], 0),
-               "template slot");
-      else
-        DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tpl_free_seq[slot],
-                                          hipStreamWaitValueGte, ~0ull),
-               "template slot");
+      DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tpl_free_seq[slot] % dm_ctx::kTickEv], 0),
+             "template slot");                                                // templates are done
     }
     else if (leaf->tpl_free_rec[slot])
       DM_HIP(root, leaf->xs_wait(leaf->tpl_free[slot], root->stream), "template slot");
@@ -2498,14 +2462,11 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
     DM_HIP(root, leaf->join_aux(), "join leaf streams");
     // the exchange stream after the tick that wrote the block: on the tick-done word when
     // the tick stores it (no marker on the leaf's queue), else an event
-    if (leaf->stream != root->stream) leaf->tick_word_wanted = true;
+    if (leaf->stream != root->stream) leaf->tick_signal_wanted = true;
     if (leaf->stream == root->stream) {
       // stream order
-    } else if (leaf->tick_flagged && leaf->tick_evented)
+    } else if (leaf->tick_flagged)
       DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tick_seq % dm_ctx::kTickEv], 0),
-             "leaf->exchange order");
-    else if (leaf->tick_flagged)
-      DM_HIP(root, hipStreamWaitValue64(root->stream, leaf->tick_word, leaf->tick_seq, hipStreamWaitValueGte, ~0ull),
              "leaf->exchange order");
     else
       DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->exchange order");
