@@ -951,6 +951,7 @@ def main():
             rx = timed_steps(torch, ex, stx, kx, args.warmup, sync_ranks, extra_warm=name != "c4")
             rx["dense_frac"] = tick_dense_fraction(ex, snapx, stx)
             extra[name] = workload_line(name, snapx, rx, kx, single_kernel_tick=name == "c1")
+            extra[name]["aux_own_queues"] = bool(ex.plan_info().get("aux_own_queues", 0))
             ex.close()
             del snapx
 

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -167,6 +168,7 @@ struct dm_ctx {
   // (round 4 moved every bin to each other stream in A/Bs: this split won every one)
   static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (small class alone)
   hipStream_t aux[kAux] = {};
+  bool aux_own_queue = false;  // each auxiliary stream has a hardware queue of its own (CU mask)
   hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
   // Cross-stream order between the context's streams (fork / join of a tick's work
@@ -844,6 +846,59 @@ static hipError_t xs_setup(dm_ctx* c) {
   return hipSuccess;
 }
 
+// The auxiliary streams' sets, kept for the life of the process and reused by later
+// contexts on the same device (dm_destroy returns a context's set).  A CU-masked
+// stream gets a hardware queue of its own; streams destroyed and created again did not
+// get theirs back: in bench.py's default run the configs[2] line, measured after three
+// earlier contexts were destroyed, ran 153.6 us per tick against 110-113 us in a
+// process of its own (round 5).
+struct AuxSet {
+  int device;
+  hipStream_t s[dm_ctx::kAux];
+  bool own_queue;  // every stream got its own hardware queue (CU mask)
+};
+static std::mutex g_aux_mu;
+static std::vector<AuxSet> g_aux_free;
+
+static hipError_t take_aux(dm_ctx* c, int ncu) {
+  {
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    for (size_t i = 0; i < g_aux_free.size(); ++i)
+      if (g_aux_free[i].device == c->device) {
+        for (int k = 0; k < dm_ctx::kAux; ++k) c->aux[k] = g_aux_free[i].s[k];
+        c->aux_own_queue = g_aux_free[i].own_queue;
+        g_aux_free.erase(g_aux_free.begin() + (ptrdiff_t)i);
+        return hipSuccess;
+      }
+  }
+  const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
+  std::vector<uint32_t> mask(mwords, 0u);
+  for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
+  c->aux_own_queue = true;
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
+    e = ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, mask.data()) : hipErrorNotSupported;
+    if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
+      (void)hipGetLastError();
+      c->aux_own_queue = false;
+      e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
+    }
+  }
+  return e;
+}
+
+static void give_aux(dm_ctx* c) {
+  if (!c->aux[0]) return;
+  AuxSet a{c->device, {}, c->aux_own_queue};
+  for (int k = 0; k < dm_ctx::kAux; ++k) {
+    (void)hipStreamSynchronize(c->aux[k]);
+    a.s[k] = c->aux[k];
+    c->aux[k] = nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  g_aux_free.push_back(a);
+}
+
 int dm_create(int device, dm_ctx** out) {
   if (!out) return DM_E_INVAL;
   *out = nullptr;
@@ -894,16 +949,7 @@ int dm_create(int device, dm_ctx** out) {
   // a quarter of headroom: the other classes' streams hold slots too, and run ahead
   // (DM_DEFER_JOIN)
   c->redo_cap = (int64_t)std::max(ncu, 1) * redo_blocks_per_cu() * 3 / 4;
-  const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
-  std::vector<uint32_t> mask(mwords, 0u);
-  for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
-  for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
-    e = ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, mask.data()) : hipErrorNotSupported;
-    if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
-      (void)hipGetLastError();
-      e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
-    }
-  }
+  if (e == hipSuccess) e = take_aux(c, ncu);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
@@ -938,12 +984,7 @@ void dm_destroy(dm_ctx* c) {
   c->collect_profile();
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   c->free_all();
-  for (int i = 0; i < dm_ctx::kAux; ++i) {
-    if (c->aux[i]) {
-      (void)hipStreamSynchronize(c->aux[i]);
-      (void)hipStreamDestroy(c->aux[i]);
-    }
-  }
+  give_aux(c);  // kept for the next context on this device (take_aux)
   if (c->cpy) {
     (void)hipStreamSynchronize(c->cpy);
     (void)hipStreamDestroy(c->cpy);
@@ -2546,7 +2587,7 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[7 + kNumBins];
+  int64_t v[8 + kNumBins];
   v[0] = (int64_t)c->h_tiles.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
@@ -2555,7 +2596,8 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   v[4 + kNumBins] = c->bin6_wide ? 1 : 0;  // bin 6 on 512 x 8 workgroups (else 256 x 16)
   v[5 + kNumBins] = c->redo_cap;  // 3/4 of the redo's full-build workgroups the GPU holds at once
   v[6 + kNumBins] = 1;            // every store may speculate (the redo by teams has no bound)
-  const int n = 7 + kNumBins;
+  v[7 + kNumBins] = c->aux_own_queue ? 1 : 0;  // the work classes' streams each have a hardware queue
+  const int n = 8 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }

@@ -382,7 +382,8 @@ int dm_reset_kernel_times(dm_ctx* ctx);
  * sub8x2, sub16x2), large resources, large chunks, leases, then 1 when the
  * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), 3/4 of the redo's
  * full-build workgroups the GPU holds at once (its grid bound), and 1 (every store may
- * speculate: the redo by teams needs only 64 co-resident workgroups); returns 16 */
+ * speculate: the redo by teams needs only 64 co-resident workgroups), and 1 when the
+ * work classes' auxiliary streams each have a hardware queue of their own; returns 17 */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),
