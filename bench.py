@@ -659,6 +659,7 @@ def workload_line(name, snap, run, steps, single_kernel_tick):
             "ms_per_step": t_step * 1e3,
             "tick_hbm_frac": round(tick_bytes / t_step / 1e9 / HBM_PEAK_GBS, 4),
             "tick_algorithmic_bytes": tick_bytes,
+            "host_enqueue_us_per_step": round(run["host_enqueue_s"] / steps * 1e6, 2),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
                         for k, v in run["ktimes"].items()},
             "roofline": roofline_of(name, snap, run, steps, single_kernel_tick)}

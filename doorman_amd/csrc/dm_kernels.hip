@@ -3085,17 +3085,6 @@ hipError_t launch_large(int phase, const DevParams& p, const Chunk* chunks, int 
   return hipGetLastError();
 }
 
-#ifdef DM_EXP_REDO_NULL
-__global__ __launch_bounds__(256) void k_redo_null(SpecArgs S) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const int q = S.par ^ 1;
-    S.ring[q] = 0;
-    S.ring[2 + q] = 0;
-    __hip_atomic_store(S.seen, S.ring[S.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-#endif
-
 hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks, int nchunks, const LargeSeg* ls,
                              const Partials& P, const SpecArgs& S, int redo_grid, int32_t* glist, int32_t* gcount,
                              hipStream_t st) {
@@ -3104,13 +3093,8 @@ hipError_t launch_large_spec(int phase, const DevParams& p, const Chunk* chunks,
     k_large_spec<<<nchunks, 256, 0, st>>>(p, chunks, ls, P, S);
   else if (phase == 1)
     k_large_redo_team<false><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
-#ifdef DM_EXP_REDO_NULL
-  else  // A/B probe only: the empty redo launch's bookkeeping, without the redo (wrong if anything is marked)
-    k_redo_null<<<DM_EXP_REDO_NULL, 256, 0, st>>>(S);
-#else
   else
     k_large_redo_team<true><<<redo_grid, 256, 0, st>>>(p, chunks, ls, P, S, glist, gcount);
-#endif
   return hipGetLastError();
 }
 

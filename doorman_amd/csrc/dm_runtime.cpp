@@ -169,6 +169,7 @@ struct dm_ctx {
   static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (small class alone)
   hipStream_t aux[kAux] = {};
   bool aux_own_queue = false;  // each auxiliary stream has a hardware queue of its own (CU mask)
+  uint64_t aux_seq = 0;        // the stream set's creation order in the process (take_aux)
   hipStream_t cpy = nullptr;  // store-update column copies (overlap a running tick)
   hipEvent_t ev_stage[2] = {};  // staged update copies -> per-chunk validation
   // Cross-stream order between the context's streams (fork / join of a tick's work
@@ -846,50 +847,76 @@ static hipError_t xs_setup(dm_ctx* c) {
   return hipSuccess;
 }
 
-// The auxiliary streams' sets, kept for the life of the process and reused by later
-// contexts on the same device (dm_destroy returns a context's set).  A CU-masked
-// stream gets a hardware queue of its own; streams destroyed and created again did not
-// get theirs back: in bench.py's default run the configs[2] line, measured after three
-// earlier contexts were destroyed, ran 153.6 us per tick against 110-113 us in a
-// process of its own (round 5).
+// The context's streams (its own stream, the four auxiliary streams, the copy stream),
+// kept for the life of the process and reused by later contexts on the same device
+// (dm_destroy returns a context's set; take_aux hands out the earliest-created free
+// set).  The hardware queues behind the streams are not interchangeable: measured on
+// C2 (round 5, tools/gpu_r5_perm.sh, profiles/r05_queues.txt), which of the four
+// masked queues carries which work class moved the tick from 111 us to 157 us, and the
+// best assignment is a property of the queue's position in the process's creation
+// order (period 4, consistent with queues spread over four hardware pipes): the small
+// tiles on the last-created queue, every other assignment with the tiles elsewhere
+// 123-157 us.  Stream priority does not change it.  So the creation order below is
+// part of the tuning (own stream, the four masked streams, then the copy stream:
+// 110-112 us; the copy stream first 137 us; the masked streams first 125 us), and a
+// set is reused rather than destroyed and created again: new queues take other
+// positions (bench.py's default run measured configs[2] at 124-154 us after earlier
+// contexts were destroyed, 111-113 us with the pool).
 struct AuxSet {
   int device;
+  uint64_t seq;  // creation order: the earliest set first (its queues' positions, below)
   hipStream_t s[dm_ctx::kAux];
+  hipStream_t own, cpy;  // the context's own stream and its copy stream, pooled with them
   bool own_queue;  // every stream got its own hardware queue (CU mask)
 };
 static std::mutex g_aux_mu;
 static std::vector<AuxSet> g_aux_free;
+static uint64_t g_aux_seq = 0;
 
 static hipError_t take_aux(dm_ctx* c, int ncu) {
   {
     std::lock_guard<std::mutex> lk(g_aux_mu);
+    size_t best = g_aux_free.size();
     for (size_t i = 0; i < g_aux_free.size(); ++i)
-      if (g_aux_free[i].device == c->device) {
-        for (int k = 0; k < dm_ctx::kAux; ++k) c->aux[k] = g_aux_free[i].s[k];
-        c->aux_own_queue = g_aux_free[i].own_queue;
-        g_aux_free.erase(g_aux_free.begin() + (ptrdiff_t)i);
-        return hipSuccess;
-      }
+      if (g_aux_free[i].device == c->device && (best == g_aux_free.size() || g_aux_free[i].seq < g_aux_free[best].seq))
+        best = i;
+    if (best < g_aux_free.size()) {
+      const AuxSet& a = g_aux_free[best];
+      for (int k = 0; k < dm_ctx::kAux; ++k) c->aux[k] = a.s[k];
+      c->own_stream = a.own;
+      c->cpy = a.cpy;
+      c->aux_own_queue = a.own_queue;
+      c->aux_seq = a.seq;
+      g_aux_free.erase(g_aux_free.begin() + (ptrdiff_t)best);
+      return hipSuccess;
+    }
+    c->aux_seq = g_aux_seq++;
   }
   const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
   std::vector<uint32_t> mask(mwords, 0u);
   for (int b = 0; b < ncu; ++b) mask[(size_t)(b / 32)] |= 1u << (b % 32);
   c->aux_own_queue = true;
-  hipError_t e = hipSuccess;
+  // the creation order is measured (above)
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   for (int i = 0; i < dm_ctx::kAux && e == hipSuccess; ++i) {
-    e = ncu > 0 ? hipExtStreamCreateWithCUMask(&c->aux[i], (uint32_t)mwords, mask.data()) : hipErrorNotSupported;
+    hipStream_t* slot = &c->aux[i];
+    e = ncu > 0 ? hipExtStreamCreateWithCUMask(slot, (uint32_t)mwords, mask.data()) : hipErrorNotSupported;
     if (e != hipSuccess) {  // no CU masks here: a plain stream (correct, queue sharing as above)
       (void)hipGetLastError();
       c->aux_own_queue = false;
-      e = hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking);
+      e = hipStreamCreateWithFlags(slot, hipStreamNonBlocking);
     }
   }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
   return e;
 }
 
 static void give_aux(dm_ctx* c) {
-  if (!c->aux[0]) return;
-  AuxSet a{c->device, {}, c->aux_own_queue};
+  if (!c->aux[0] || !c->own_stream || !c->cpy) return;
+  (void)hipStreamSynchronize(c->own_stream);
+  (void)hipStreamSynchronize(c->cpy);
+  AuxSet a{c->device, c->aux_seq, {}, c->own_stream, c->cpy, c->aux_own_queue};
+  c->own_stream = c->cpy = nullptr;
   for (int k = 0; k < dm_ctx::kAux; ++k) {
     (void)hipStreamSynchronize(c->aux[k]);
     a.s[k] = c->aux[k];
@@ -929,13 +956,7 @@ int dm_create(int device, dm_ctx** out) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
   }
-  e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    g_last_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
-    delete c;
-    return DM_E_HIP;
-  }
-  c->stream = c->own_stream;
+  e = hipSuccess;
   // The auxiliary streams are created with a full CU mask, which gives each its own
   // hardware queue.  Plain streams share the process's GPU_MAX_HW_QUEUES (4) queues
   // round robin with every other stream of the process (torch's included), so which
@@ -950,7 +971,7 @@ int dm_create(int device, dm_ctx** out) {
   // (DM_DEFER_JOIN)
   c->redo_cap = (int64_t)std::max(ncu, 1) * redo_blocks_per_cu() * 3 / 4;
   if (e == hipSuccess) e = take_aux(c, ncu);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cpy, hipStreamNonBlocking);
+  c->stream = c->own_stream;
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
@@ -985,6 +1006,8 @@ void dm_destroy(dm_ctx* c) {
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   c->free_all();
   give_aux(c);  // kept for the next context on this device (take_aux)
+  for (int i = 0; i < dm_ctx::kAux; ++i)  // (a set not returned whole)
+    if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
   if (c->cpy) {
     (void)hipStreamSynchronize(c->cpy);
     (void)hipStreamDestroy(c->cpy);

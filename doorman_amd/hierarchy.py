@@ -152,6 +152,12 @@ class HierarchicalTick:
         # the exchange's kernels (gather, root round) are few and short, but beside a leaf tick
         # that fills every CU they wait for slots: a high-priority queue lets them in first
         self.xstream = torch.cuda.Stream(device=dev, priority=-1) if pipelined and own else self.stream
+        # the buffers above are zeroed on torch's current stream: the library's streams
+        # (which dm_publish_ring's flag reset and every later write run on) wait for that
+        cur = torch.cuda.current_stream(dev)
+        self.stream.wait_stream(cur)
+        if self.xstream is not self.stream:
+            self.xstream.wait_stream(cur)
         leaf.set_stream(self.stream.cuda_stream)
         root.set_stream(self.xstream.cuda_stream)
         # lag: ticks of lag of the pipelined templates (dm_hier_pipeline): default 1 with the

@@ -149,6 +149,7 @@ def test_hierarchy_rounds_match_the_reference_model(G, clients):
     roots = [root_engine(rcfg, G) for _ in range(G)]
     model = M.Root(rcfg, G)
     gathered = torch.zeros((G * (R + 1), 2), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream, written on the context's
     for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 40 * W.NS]):
         if t == 2 and G > 1:  # server 1 stops asking for a quarter of the resources
             so = leaves[1].seg_off
@@ -213,6 +214,7 @@ def test_root_round_grants_stay_within_capacity(G):
     model = M.Root(rcfg, G)
     rng = np.random.default_rng(G)
     gathered = torch.zeros((G * (R + 1), 2), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream, written on the context's
     for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 10 * W.NS]):
         sw = rng.uniform(100.0, 300.0, (G, R))  # every server wants more than C
         cnt = rng.integers(1, 40, (G, R)).astype(np.int64)
@@ -397,6 +399,7 @@ def test_publish_carries_the_roots_validation():
         snap = W.make_snapshot(sizes, wants, np.zeros(N), sub, np.full(N, NOW + 60 * W.NS), W.FAIR_SHARE, 100.0)
         R = len(sizes)
         buf = torch.full((R + 3, 2), -7.0, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()  # filled on torch's stream, written on the context's
         with Engine(0) as e:
             e.load(snap)
             for _ in range(2):  # twice: the flag accumulator returns to zero after each launch
@@ -480,6 +483,7 @@ def test_sharded_exchange_matches_the_reference_model(pipelined, large):
         roots.append(root)
     model = M.Root(rcfg, G)
     gathered = torch.zeros((G * S, 2), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream, written on the context's
     staged = []  # templates after each exchange, oldest first (pipelined)
     for t, now in enumerate([NOW, NOW + 5 * W.NS, NOW + 9 * W.NS, NOW + 30 * W.NS, NOW + 31 * W.NS]):
         lag = int(pipelined)
@@ -556,6 +560,7 @@ def test_publish_ring_matches_publish_totals():
     R = len(snap["seg_off"]) - 1
     ring = [torch.full((R + 1, 2), -1.0, dtype=torch.float64, device="cuda") for _ in range(3)]
     ref = torch.zeros((R + 1, 2), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # the fills run on torch's stream: done before the library writes the buffers
     with Engine(0) as e:
         e.load(snap)
         ptrs = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ring])
@@ -599,6 +604,7 @@ def test_stream_wait_orders_a_foreign_stream_after_the_tick():
                            300, 5)
     ring = [torch.zeros((R + 1, 2), dtype=torch.float64, device="cuda") for _ in range(3)]
     xs = torch.cuda.Stream()
+    torch.cuda.synchronize()  # the fills run on torch's stream
     with Engine(0) as e:
         e.load(snap)
         ptrs = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ring])
