@@ -873,6 +873,20 @@ static std::mutex g_aux_mu;
 static std::vector<AuxSet> g_aux_free;
 static uint64_t g_aux_seq = 0;
 
+// The pooled streams are destroyed at exit, before the HIP runtime's own teardown (an
+// atexit handler registered after the runtime came up runs first): streams left to
+// that teardown crashed the process at exit under rocprofv3.
+static void release_aux_pool() {
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  for (AuxSet& a : g_aux_free) {
+    (void)hipSetDevice(a.device);
+    for (hipStream_t s : a.s) (void)hipStreamDestroy(s);
+    (void)hipStreamDestroy(a.own);
+    (void)hipStreamDestroy(a.cpy);
+  }
+  g_aux_free.clear();
+}
+
 static hipError_t take_aux(dm_ctx* c, int ncu) {
   {
     std::lock_guard<std::mutex> lk(g_aux_mu);
@@ -891,6 +905,8 @@ static hipError_t take_aux(dm_ctx* c, int ncu) {
       return hipSuccess;
     }
     c->aux_seq = g_aux_seq++;
+    static bool registered = false;
+    if (!registered) registered = std::atexit(release_aux_pool) == 0;
   }
   const size_t mwords = (size_t)std::max(1, (ncu + 31) / 32);
   std::vector<uint32_t> mask(mwords, 0u);
