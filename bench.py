@@ -616,7 +616,8 @@ def exchange_self_check(torch, dist, ht, leaf, root, bounds, rank, world, g, now
     mism, rejected = 0, 0
     for (r, row, sums, got), o in zip(allsamp, owners):
         blk = gathered[o * S:(o + 1) * S]
-        flags = int(blk[0, 0:1].view(np.int64)[0])
+        f = int(blk[0, 0:1].view(np.uint64)[0])
+        flags = (f & 0xFFFFFFFF) | (f >> 32)  # record 0's two flags words (one per stream part)
         v = blk[1 + r - int(bounds[o])]
         res = root_round_one(now, [c[r] for c in cfg_cols], row, sums, flags, v[0], int(v[1:2].view(np.int64)[0]))
         if res is None:

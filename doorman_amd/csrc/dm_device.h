@@ -267,10 +267,26 @@ struct DevParams {
   int32_t writeback;  // rows become followers / released in the store; out_expiry unused
   // dm_publish_ring: a writeback tick also writes what dm_publish_totals would (record
   // 1 + r = {SumWants, Count} as each resource's sums are stored, the validation flags
-  // OR-ed into record 0) and clears record 0 of the ring's next buffer; nullptr: off
+  // OR-ed into record 0) and clears its flags word in record 0 of the ring's next
+  // buffer; nullptr: off.  A bin split into stream parts (dm_runtime.cpp) runs its parts
+  // unjoined from tick to tick, so each part owns a 32-bit flags word of record 0
+  // (pub_word: 0 or 1; the first 8 bytes read as one int64 hold their OR in either
+  // half) and clears only that word, from its first resource (pub_first), in the next
+  // buffer; pub_word -1: the tick's only launch that publishes the first resource
+  // (word 0, and it clears the whole record).
   double2* pub;
   double2* pub_clear;
+  int32_t pub_word;
+  int32_t pub_first;
 };
+
+// The validation flags of a published block's record 0: the OR of its two flags words
+// (DevParams::pub_word).
+__host__ __device__ inline uint32_t pub_flags(double x) {
+  long long b;
+  __builtin_memcpy(&b, &x, 8);
+  return (uint32_t)b | (uint32_t)((unsigned long long)b >> 32);
+}
 
 // dm_decide: one resource and its requests [qlo, qhi) in the caller's order; the
 // resource's rows are copied to scratch rows [scr, scr + n) that take each

@@ -345,8 +345,11 @@ __device__ __forceinline__ void write_resource(const DevParams& p, int seg, cons
     v.y = __longlong_as_double(r.count);
     p.pub[1 + seg] = v;
     if (r.sum_wants > 0.0 && (r.count < 1 || r.count > kSubMax))  // the root's validation (:863-866)
-      atomicOr((unsigned int*)p.pub, r.count < 1 ? kHierInvalid : kHierCountRange);
-    if (seg == 0) p.pub_clear[0] = double2{0.0, 0.0};  // the next tick's flags start clear
+      atomicOr((unsigned int*)p.pub + (p.pub_word < 0 ? 0 : p.pub_word), r.count < 1 ? kHierInvalid : kHierCountRange);
+    if (seg == p.pub_first) {  // the next tick's flags start clear
+      if (p.pub_word < 0) p.pub_clear[0] = double2{0.0, 0.0};
+      else ((uint32_t*)p.pub_clear)[p.pub_word] = 0u;
+    }
   }
   if (p.writeback) {  // ... and none keeps an explicit expiry
     const int had = rs.xstate;

@@ -2722,7 +2722,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
   const int rl = lane / P, g0 = lane - rl * P;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < ha.G)  // the round's per-server flags (dm_hier_status)
-    ha.status_out[threadIdx.x] = (uint32_t)__double_as_longlong(ha.gathered[(int64_t)threadIdx.x * ha.stride].x);
+    ha.status_out[threadIdx.x] = pub_flags(ha.gathered[(int64_t)threadIdx.x * ha.stride].x);
   const int64_t r = ha.r_lo + wave * per + rl;
   if (ha.r_lo + wave * per >= ha.r_hi) return;  // whole waves only
   const bool valid = g0 < K && r < ha.r_hi;
@@ -2756,7 +2756,7 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
     s = sub_value(raw);
     e = sub_released(raw) ? kReleased : (raw < 0 ? xe : rs_cfg.follow_exp);
     const double2* blk = ha.gathered + (int64_t)g * ha.stride;
-    flags = (uint32_t)__double_as_longlong(blk[0].x);
+    flags = pub_flags(blk[0].x);
     const double2 v = blk[1 + rec];
     req = flags == 0u && v.x > 0.0;  // count in [1, kSubMax] when the flags are clear
     rw = v.x;

@@ -292,6 +292,7 @@ struct dm_ctx {
   hipError_t join_aux() {
     if (!aux_pending) return hipSuccess;
     aux_pending = false;
+    aux_unjoined = 0;
     for (int i = 0; i < kAux; ++i) {
       hipError_t e = xs_order(XS_JOIN0 + i, aux[i], stream);
       if (e != hipSuccess) return e;
@@ -319,10 +320,26 @@ struct dm_ctx {
   // thousands of items).  DM_DENSE_SPLIT=0: never split.
   int dense_split = 0xF;  // bit i: bin 3+i runs in the split form (DM_DENSE_SPLIT: 0 off, 1 all, else the mask)
   static constexpr int kSplitBins = 4;  // bins 3..6
-  DBuf<int32_t> dq_list[kSplitBins], dq_cnt[kSplitBins];
-  int dq_par[kSplitBins] = {};
-  int dq_skip[kSplitBins] = {};   // ticks in the one-kernel form since the split was last tried
-  int dq_wait[kSplitBins] = {64, 64, 64, 64};  // ticks before the next try
+  // Stream parts: a workgroup bin that is the store's only work class, and small enough
+  // that a launch's ramp and drain are a visible share of it, runs as kParts launches
+  // over contiguous halves of its items on two auxiliary streams, never joined from
+  // tick to tick (DM_DEFER_JOIN): each part's next tick starts while the other part
+  // drains, so the GPU never idles between ticks (an N = 8 shard of configs[3], 12.5M
+  // leases: 57.3 -> 48.8 us per tick, tools/shard_split.py; the whole configs[3], 100M
+  // leases: 430 -> 425 us, not worth its cross-queue waits in the exchange).  Every
+  // split-bin state below is per part: slot (b - 3) * kParts + part.
+  static constexpr int kParts = 2;
+  static constexpr int kSplitSlots = kSplitBins * kParts;
+  int bin_parts[kNumBins] = {1, 1, 1, 1, 1, 1, 1, 1, 1};
+  // off for a leaf whose ticks an exchange on another stream waits for (dm_hier_attach):
+  // there the exchange's two waits and the parts' CU share cost more than the parts
+  // gain (the N = 8 rehearsal step 58.7 -> 66 us; one wait: 60-62 us; round 5)
+  bool parts_ok = true;
+  int64_t part_lo[kNumBins][kParts + 1] = {};  // item bounds of each part
+  DBuf<int32_t> dq_list[kSplitSlots], dq_cnt[kSplitSlots];
+  int dq_par[kSplitSlots] = {};
+  int dq_skip[kSplitSlots] = {};   // ticks in the one-kernel form since the split was last tried
+  int dq_wait[kSplitSlots] = {64, 64, 64, 64, 64, 64, 64, 64};  // ticks before the next try
   bool bin6_wide = false;  // bin 6 on 512 x 8 workgroups (kBin6Wide): it holds most of the rows
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
@@ -333,7 +350,7 @@ struct dm_ctx {
   uint64_t* d_rec = nullptr;
   int32_t* h_guard = nullptr;
   int32_t* d_guard = nullptr;
-  uint64_t dq_ver_epoch[kSplitBins] = {};  // the epoch each bin's check was enqueued in
+  uint64_t dq_ver_epoch[kSplitSlots] = {};  // the epoch each slot's check was enqueued in
   // large-path partials
   DBuf<int64_t> pa_cnt, pa_cnt_all, pa_smin, pa_smax, pb_w, pc_sgt;
   DBuf<double> pa_has, pa_wants, pa_has_all, pa_wants_all, pb_x, pb_y, pc_ee, pd_delta;
@@ -454,9 +471,24 @@ struct dm_ctx {
   // the leaf's queue): the N = 8 rehearsal step 60.2-60.7 -> 58.7-58.8 us (round 5,
   // gpurun_out/r5b2shard, three alternations).
   uint64_t tick_seq = 0;          // the last tick's number
-  bool tick_flagged = false;      // ... and whether its last kernel completes tick_ev[tick_seq % kTickEv]
+  bool tick_flagged = false;      // ... and whether its last kernels complete tick_ev[*][tick_seq % kTickEv]
   static constexpr int kTickEv = 16;
-  hipEvent_t tick_ev[kTickEv] = {};
+  hipEvent_t tick_ev[kParts][kTickEv] = {};  // per stream part (one part: [0])
+  int tick_nev[kTickEv] = {};                // the parts that completed each flagged tick's events
+  unsigned tick_part_mask = 0;               // auxiliary streams of the last flagged tick's parts
+  // auxiliary streams with work not yet joined into the context stream
+  unsigned aux_unjoined = 0;
+  // the last tick's events cover every auxiliary stream's unjoined work, so a consumer
+  // may wait on them instead of joining (which would make the next tick's parts wait
+  // for each other: 49 -> 74 us per tick on the N = 8 shard, tools/shard_split.py)
+  bool tick_covers() const { return tick_flagged && tick_part_mask != 0 && (aux_unjoined & ~tick_part_mask) == 0; }
+  // a stream part's auxiliary stream (part 0: the bin's class stream).  Part 1 beside
+  // bins 4-6's stream 1: stream 2 or 0 run C1 at 40.6-40.8 us per tick, stream 3 at
+  // 61.6-64.2 us (which hardware queues pair well: take_aux; profiles/r05_parts_ab.txt)
+  int part_stream(int b, int j) const {
+    if (j == 0) return class_stream[b];
+    return class_stream[b] != 2 ? 2 : 0;
+  }
   // set by the first consumer on another stream (the exchange's order, a template
   // slot's reuse): before it, no tick carries the event
   bool tick_signal_wanted = false;
@@ -482,7 +514,7 @@ struct dm_ctx {
   // that touches the store and after every host wait that may have completed a tick.
   int check_device() {
     if (!store_lost) {
-      for (int i = 0; h_guard && i < kSplitBins; ++i)
+      for (int i = 0; h_guard && i < kSplitSlots; ++i)
         if (__atomic_load_n(h_guard + i, __ATOMIC_RELAXED)) {
           store_lost = true;
           lost_msg = "a dense kernel queued an item on a tick that skipped its rest kernel";
@@ -540,7 +572,7 @@ struct dm_ctx {
     agg.release(); expl.release(); cfg.release(); cold.release();
     out_gets.release(); out_expiry.release(); res.release();
     tiles.release(); for (auto& b : bins) b.release(); chunks.release(); large.release();
-    for (int i = 0; i < kSplitBins; ++i) {
+    for (int i = 0; i < kSplitSlots; ++i) {
       dq_list[i].release();
       dq_cnt[i].release();
     }
@@ -685,14 +717,70 @@ static void build_plan(dm_ctx* c) {
   }
 }
 
-// Once per row epoch, after a writeback tick of workgroup bin b (split bin i): count
-// its items left without a dense hint (k_count_undense -> h_rec).  A count of 0 lets
-// the following ticks of the epoch skip the bin's k_block_rest.
-static hipError_t check_dense(dm_ctx* c, int i, int b, hipStream_t s) {
-  if (c->dq_ver_epoch[i] == c->row_epoch || c->h_bins[b].empty()) return hipSuccess;
+// Once per row epoch, after a writeback tick of workgroup bin b's part j (split slot
+// i): count its items left without a dense hint (k_count_undense -> h_rec).  A count
+// of 0 lets the following ticks of the epoch skip the part's k_block_rest.
+static hipError_t check_dense(dm_ctx* c, int i, int b, int j, hipStream_t s) {
+  const int64_t lo = c->part_lo[b][j], n = c->part_lo[b][j + 1] - lo;
+  if (c->dq_ver_epoch[i] == c->row_epoch || n <= 0) return hipSuccess;
   c->dq_ver_epoch[i] = c->row_epoch;
-  return launch_count_undense(c->bins[b].p, (int)c->h_bins[b].size(), (unsigned long long*)(c->d_rec + 2 * i),
+  return launch_count_undense(c->bins[b].p + lo, (int)n, (unsigned long long*)(c->d_rec + 2 * i),
                               (unsigned long long)c->row_epoch, s);
+}
+
+// Stream parts (dm_ctx::kParts): a workgroup bin holding every resource of the store
+// (no other bin, tile or chunk, no heterogeneous subclients) and at most kPartBytes of
+// rows, with enough items that each half still fills the GPU.
+constexpr int64_t kPartBytes = int64_t(1) << 30;
+constexpr int64_t kPartMinItems = 4096;
+static void plan_parts(dm_ctx* c) {
+  int nonempty = 0, only = -1;
+  for (int b = 0; b < kNumBins; ++b)
+    if (!c->h_bins[b].empty()) {
+      ++nonempty;
+      only = b;
+    }
+  for (int b = 0; b < kNumBins; ++b) {
+    const int64_t n = (int64_t)c->h_bins[b].size();
+    const bool split = c->parts_ok && nonempty == 1 && only == b && b >= 3 && b < 3 + dm_ctx::kSplitBins && c->h_tiles.empty() &&
+                       c->h_chunks.empty() && !c->maybe_general && n >= kPartMinItems && c->N * 28 <= kPartBytes;
+    c->bin_parts[b] = split ? dm_ctx::kParts : 1;
+    for (int j = 0; j <= dm_ctx::kParts; ++j)
+      c->part_lo[b][j] = split ? n * j / dm_ctx::kParts : (j == 0 ? 0 : n);
+  }
+}
+
+// The stream parts of the plan and every split slot's state: rest queues, two-slot
+// counters, the epoch checks (a new plan, or parts turned off).
+static int init_split_slots(dm_ctx* c, hipStream_t st) {
+  plan_parts(c);
+  for (int i = 0; i < dm_ctx::kSplitSlots; ++i) {
+    __atomic_store_n(c->h_rec + 2 * i + 1, (uint64_t)0, __ATOMIC_RELAXED);
+    __atomic_store_n(c->h_guard + i, 0, __ATOMIC_RELAXED);
+    c->dq_ver_epoch[i] = 0;
+    __atomic_store_n(c->h_dq + i, 0, __ATOMIC_RELAXED);
+    c->dq_skip[i] = 0;
+    c->dq_wait[i] = 64;
+    const int b = 3 + i / dm_ctx::kParts, j = i % dm_ctx::kParts;
+    const size_t nb = (size_t)std::max<int64_t>(c->part_lo[b][j + 1] - c->part_lo[b][j], 1);
+    DM_HIP(c, c->dq_list[i].ensure(nb), "dense split queue");
+    DM_HIP(c, c->dq_cnt[i].ensure(3), "dense split queue");  // two-slot count + the last count told the host
+    DM_HIP(c, hipMemsetAsync(c->dq_cnt[i].p, 0, 3 * sizeof(int32_t), st), "dense split queue");
+    c->dq_par[i] = 0;
+  }
+  return DM_OK;
+}
+
+// Stream parts allowed or not (dm_ctx::parts_ok): the plan's parts and the split slots
+// are set up again after every stream has drained.
+static int set_parts_ok(dm_ctx* c, bool ok) {
+  if (c->parts_ok == ok) return DM_OK;
+  c->parts_ok = ok;
+  if (!c->h_dq) return DM_OK;  // no plan yet: upload_plan reads the flag
+  DM_HIP(c, c->join_aux(), "join");
+  if (int rc = c->synced("stream parts")) return rc;
+  c->main_dirty = true;
+  return init_split_slots(c, c->stream);
 }
 
 static int upload_plan(dm_ctx* c) {
@@ -705,38 +793,24 @@ static int upload_plan(dm_ctx* c) {
     // fine-grained (coherent) host memory: a device store lands in host memory at once,
     // not in the GPU's L2 until a system-scope release (which a profiled dispatch under
     // rocprofv3 need not issue: the rest-skip check was never seen there)
-    DM_HIP(c, hipHostMalloc((void**)&c->h_dq, dm_ctx::kSplitBins * sizeof(int32_t),
+    DM_HIP(c, hipHostMalloc((void**)&c->h_dq, dm_ctx::kSplitSlots * sizeof(int32_t),
                             hipHostMallocMapped | hipHostMallocCoherent),
            "dense split word");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_dq, c->h_dq, 0), "dense split word");
-    DM_HIP(c, hipHostMalloc((void**)&c->h_rec, dm_ctx::kSplitBins * 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
+    DM_HIP(c, hipHostMalloc((void**)&c->h_rec, dm_ctx::kSplitSlots * 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
            "dense split check");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0), "dense split check");
-    DM_HIP(c, hipHostMalloc((void**)&c->h_guard, dm_ctx::kSplitBins * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
+    DM_HIP(c, hipHostMalloc((void**)&c->h_guard, dm_ctx::kSplitSlots * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
            "dense split guard");
     DM_HIP(c, hipHostGetDevicePointer((void**)&c->d_guard, c->h_guard, 0), "dense split guard");
   }
   c->rows_changed();  // new work items: no hints
-  for (int i = 0; i < dm_ctx::kSplitBins; ++i) {
-    __atomic_store_n(c->h_rec + 2 * i + 1, (uint64_t)0, __ATOMIC_RELAXED);
-    __atomic_store_n(c->h_guard + i, 0, __ATOMIC_RELAXED);
-    c->dq_ver_epoch[i] = 0;
-  }
   {
     int64_t rows6 = 0;
     for (const WorkItem& w : c->h_bins[6]) rows6 += w.n & 0xFFFF;
     c->bin6_wide = 2 * rows6 > c->N;
   }
-  for (int i = 0; i < dm_ctx::kSplitBins; ++i) {  // the dense split of bins 3-6: rest queues, two-slot counters
-    __atomic_store_n(c->h_dq + i, 0, __ATOMIC_RELAXED);
-    c->dq_skip[i] = 0;
-    c->dq_wait[i] = 64;
-    const size_t nb = std::max<size_t>(c->h_bins[3 + i].size(), 1);
-    DM_HIP(c, c->dq_list[i].ensure(nb), "dense split queue");
-    DM_HIP(c, c->dq_cnt[i].ensure(3), "dense split queue");  // two-slot count + the last count told the host
-    DM_HIP(c, hipMemsetAsync(c->dq_cnt[i].p, 0, 3 * sizeof(int32_t), st), "dense split queue");
-    c->dq_par[i] = 0;
-  }
+  if (int rc = init_split_slots(c, st)) return rc;
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
   DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
@@ -991,7 +1065,8 @@ int dm_create(int device, dm_ctx** out) {
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
-  for (int i = 0; i < dm_ctx::kTickEv && e == hipSuccess; ++i) e = hipEventCreate(&c->tick_ev[i]);
+  for (int j = 0; j < dm_ctx::kParts; ++j)
+    for (int i = 0; i < dm_ctx::kTickEv && e == hipSuccess; ++i) e = hipEventCreate(&c->tick_ev[j][i]);
   if (e != hipSuccess) {
     g_last_error = std::string("stream/event setup: ") + hipGetErrorString(e);
     dm_destroy(c);
@@ -1034,8 +1109,9 @@ void dm_destroy(dm_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_bat)
     if (ev) (void)hipEventDestroy(ev);
-  for (auto ev : c->tick_ev)
-    if (ev) (void)hipEventDestroy(ev);
+  for (auto& row : c->tick_ev)
+    for (auto ev : row)
+      if (ev) (void)hipEventDestroy(ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -1226,9 +1302,13 @@ static int commit_templates(dm_ctx* c) {
   for (size_t i = 0; i + 1 < n; ++i) c->tpl_free_slots.push_back(c->tpl_pending[i].slot);  // superseded
   c->tpl_pending.erase(c->tpl_pending.begin(), c->tpl_pending.begin() + (ptrdiff_t)n);
   if (take < 0) return DM_OK;
-  DM_HIP(c, c->join_aux(), "join");  // deferred class work also read the old templates
   const dm_ctx::XsTok& rt = c->tpl_ready[take];
-  if (rt.rec && rt.s && rt.s != c->stream) {
+  const bool host_wait = rt.rec && rt.s && rt.s != c->stream;
+  // deferred class work also read the old templates: joined, unless the last tick's
+  // events cover it (the slot's reuse then waits on them, below)
+  const bool keep = host_wait && c->tick_covers();
+  if (!keep) DM_HIP(c, c->join_aux(), "join");
+  if (host_wait) {
     // poll: the wake-up of a blocking wait comes too late for the next launch to be
     // queued in time.  Bounded by time (the exchange may wait on a slower rank's
     // all-gather): after 50 us of polling, a blocking wait frees the core.
@@ -1247,7 +1327,7 @@ static int commit_templates(dm_ctx* c) {
   } else {
     DM_HIP(c, c->xs_wait(rt, c->stream), "staged templates");
   }
-  c->main_dirty = true;  // the class streams fork after the wait
+  if (!keep) c->main_dirty = true;  // the class streams fork after the wait
   std::swap(c->cfg, c->tpl_cfg[take]);
   std::swap(c->cold, c->tpl_cold[take]);
   // the old templates (now in slot `take`) are free after the ticks already enqueued
@@ -1329,6 +1409,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     const int64_t n = (int64_t)c->pub_ring.size();
     p.pub = c->pub_ring[(size_t)(c->pub_k % n)];
     p.pub_clear = c->pub_ring[(size_t)((c->pub_k + 1) % n)];
+    p.pub_word = -1;  // (a split bin's parts set their own)
+    p.pub_first = 0;
     c->pub_k += 1;
   }
 
@@ -1351,15 +1433,20 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // auxiliary streams concurrently, forked from and joined back to the main stream.
   unsigned used = 0;  // auxiliary streams with work this tick
   for (int b = 0; b < kNumBins; ++b)
-    if (!c->h_bins[b].empty()) used |= 1u << c->class_stream[b];
+    if (!c->h_bins[b].empty()) {
+      used |= 1u << c->class_stream[b];
+      if (c->bin_parts[b] > 1) used |= 1u << c->part_stream(b, 1);
+    }
   if (!c->h_tiles.empty()) used |= 1u << c->class_stream[kNumBins];
   if (nch > 0) used |= 1u << c->class_stream[kNumBins + 1];
   const bool fork = __builtin_popcount(used) > 1;
   int nonempty_bins = 0;
   for (int b = 0; b < kNumBins; ++b) nonempty_bins += c->h_bins[b].empty() ? 0 : 1;
-  // one work class on the context stream, no kernel after its split bin's rest kernel:
-  // that kernel can store the tick-done word
-  const bool one_class = !fork && nch == 0 && c->h_tiles.empty() && !general && nonempty_bins == 1;
+  // one work class (on the context stream, or in stream parts), no kernel after its
+  // split bin's rest kernel: that kernel completes the tick's event
+  bool parts_only = false;
+  for (int b = 0; b < kNumBins; ++b) parts_only |= !c->h_bins[b].empty() && c->bin_parts[b] > 1;
+  const bool one_class = (!fork || parts_only) && nch == 0 && c->h_tiles.empty() && !general && nonempty_bins == 1;
   auto cls_stream = [&](int cls) { return fork ? c->aux[c->class_stream[cls]] : st; };
   hipStream_t s_large = cls_stream(kNumBins + 1), s_small = cls_stream(kNumBins);
   if (!fork) {  // everything on the context stream, after any deferred class work
@@ -1371,6 +1458,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     for (int i = 0; i < dm_ctx::kAux; ++i) DM_HIP(c, c->xs_wait(fk, c->aux[i]), "fork");
     c->main_dirty = false;
   }
+  if (fork) c->aux_unjoined |= used;
   {
     const int nls = (int)c->h_large.size();
     // heterogeneous-subclient FairShare is decided on the chain when the store may
@@ -1455,56 +1543,76 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     }
   }
   for (int b = kNumBins - 1; b >= 0; --b) {
-    const int n = (int)c->h_bins[b].size();
-    if (n == 0) continue;
+    if (c->h_bins[b].empty()) continue;
     if (b == 7 || b == 8 || b <= 2) continue;  // k_subs
-    hipStream_t s = cls_stream(b);
     const int lb = (b == 6 && c->bin6_wide) ? kBin6Wide : b;  // the launchers' bin (shape)
-    if (b >= 3 && b < 3 + dm_ctx::kSplitBins && ((c->dense_split >> (b - 3)) & 1) && split_dense) {
-      // only a writeback tick sets hints, so the split form follows one
-      const int i = b - 3, par = c->dq_par[i];
-      const int64_t queued = __atomic_load_n(c->h_dq + i, __ATOMIC_RELAXED);
-      const bool good = 4 * queued <= n;
-      if (good) c->dq_wait[i] = 64;
-      if (good || ++c->dq_skip[i] >= c->dq_wait[i]) {
-        if (!good) c->dq_wait[i] = std::min(2 * c->dq_wait[i], 4096);
-        c->dq_skip[i] = 0;
-        // Every item verified dense in this row epoch: nothing can be queued, so the
-        // dense kernel is the bin's only launch (the guard catches the impossible).
-        const uint64_t* rec = c->h_rec + 2 * i;
-        const bool skip = __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
-                          __atomic_load_n(rec, __ATOMIC_RELAXED) == 0;
-        // the tick's last kernel (the dense kernel, or the rest kernel after it) completes
-        // the tick's event when another queue waits for the tick (tick_flagged)
-        hipEvent_t done = nullptr;
-        if (one_class && c->tick_signal_wanted) {
-          done = c->tick_ev[c->tick_seq % dm_ctx::kTickEv];
-          c->tick_flagged = true;
-        }
-        DM_HIP(c, timed(KC_DENSE3 + i, s, [&] {
-                 return launch_bin_dense(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc,
-                                         skip ? c->d_guard + i : nullptr, skip ? done : nullptr, s);
-               }),
-               "group kernel (dense split)");
-        if (!skip) {
-          // the rest kernel strides over whatever the dense kernel queues; its grid is
-          // only sized from the last split tick's queue (a hint: correctness never
-          // depends on it): an empty queue costs 16 workgroups that read one count
-          const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
-          DM_HIP(c, timed(KC_REST3 + i, s, [&] {
-                   return launch_bin_rest(lb, p, c->bins[b].p, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
-                                          rest_grid, gl, gc, done, s);
+    const int nparts = c->bin_parts[b];
+    if (one_class && c->tick_signal_wanted) {
+      c->tick_flagged = true;
+      c->tick_nev[c->tick_seq % dm_ctx::kTickEv] = nparts;
+      c->tick_part_mask = 0;
+    }
+    for (int j = 0; j < nparts; ++j) {
+      const int64_t lo = c->part_lo[b][j];
+      const int n = (int)(c->part_lo[b][j + 1] - lo);
+      if (n == 0) continue;
+      WorkItem* items = c->bins[b].p + lo;
+      hipStream_t s = j == 0 ? cls_stream(b) : c->aux[c->part_stream(b, j)];
+      DevParams pj = p;
+      if (nparts > 1 && p.pub) {  // the part's own flags word (DevParams::pub_word)
+        pj.pub_word = j;
+        pj.pub_first = c->h_bins[b][(size_t)lo].seg;
+      }
+      // the tick's last kernel of this part (the dense kernel, or the rest kernel after
+      // it) completes the part's tick event when another queue waits for the tick
+      hipEvent_t done = nullptr;
+      if (one_class && c->tick_signal_wanted) {
+        done = c->tick_ev[j][c->tick_seq % dm_ctx::kTickEv];
+        c->tick_part_mask |= fork ? 1u << (j == 0 ? c->class_stream[b] : c->part_stream(b, j)) : 0u;
+      }
+      const int i = (b - 3) * dm_ctx::kParts + j;  // split slot (bins 3-6)
+      if (b >= 3 && b < 3 + dm_ctx::kSplitBins && ((c->dense_split >> (b - 3)) & 1) && split_dense) {
+        // only a writeback tick sets hints, so the split form follows one
+        const int par = c->dq_par[i];
+        const int64_t queued = __atomic_load_n(c->h_dq + i, __ATOMIC_RELAXED);
+        const bool good = 4 * queued <= n;
+        if (good) c->dq_wait[i] = 64;
+        if (good || ++c->dq_skip[i] >= c->dq_wait[i]) {
+          if (!good) c->dq_wait[i] = std::min(2 * c->dq_wait[i], 4096);
+          c->dq_skip[i] = 0;
+          // Every item verified dense in this row epoch: nothing can be queued, so the
+          // dense kernel is the part's only launch (the guard catches the impossible).
+          const uint64_t* rec = c->h_rec + 2 * i;
+          const bool skip = __atomic_load_n(rec + 1, __ATOMIC_ACQUIRE) == c->row_epoch &&
+                            __atomic_load_n(rec, __ATOMIC_RELAXED) == 0;
+          DM_HIP(c, timed(KC_DENSE3 + (b - 3), s, [&] {
+                   return launch_bin_dense(lb, pj, items, n, c->dq_list[i].p, c->dq_cnt[i].p, par, gl, gc,
+                                           skip ? c->d_guard + i : nullptr, skip ? done : nullptr, s);
                  }),
                  "group kernel (dense split)");
-          c->dq_par[i] ^= 1;
+          if (!skip) {
+            // the rest kernel strides over whatever the dense kernel queues; its grid is
+            // only sized from the last split tick's queue (a hint: correctness never
+            // depends on it): an empty queue costs 16 workgroups that read one count
+            const int rest_grid = (int)std::min<int64_t>(512, std::max<int64_t>(16, queued));
+            DM_HIP(c, timed(KC_REST3 + (b - 3), s, [&] {
+                     return launch_bin_rest(lb, pj, items, n, c->dq_list[i].p, c->dq_cnt[i].p, par, c->d_dq + i,
+                                            rest_grid, gl, gc, done, s);
+                   }),
+                   "group kernel (dense split)");
+            c->dq_par[i] ^= 1;
+          }
+          if (wb) DM_HIP(c, check_dense(c, i, b, j, s), "dense split check");
+          continue;
         }
-        if (wb) DM_HIP(c, check_dense(c, i, b, s), "dense split check");
-        continue;
       }
+      if (done) {  // (a tick in the one-kernel form carries no event: consumers join instead)
+        c->tick_flagged = false;
+        c->tick_part_mask = 0;
+      }
+      DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(lb, pj, items, n, gl, gc, s); }), "group kernel");
+      if (b >= 3 && b < 3 + dm_ctx::kSplitBins && wb) DM_HIP(c, check_dense(c, i, b, j, s), "dense split check");
     }
-    DM_HIP(c, timed(KC_BIN0 + b, s, [&] { return launch_bin(lb, p, c->bins[b].p, n, gl, gc, s); }),
-           "group kernel");
-    if (b >= 3 && b < 3 + dm_ctx::kSplitBins && wb) DM_HIP(c, check_dense(c, b - 3, b, s), "dense split check");
   }
   if (!c->h_tiles.empty())
     DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_tile_small(p, c->tiles.p, (int)c->h_tiles.size(), s_small); }),
@@ -2249,7 +2357,10 @@ int dm_publish_ring(dm_ctx* c, int n, void* const* bufs) {
   c->pub_ring.clear();
   for (int i = 0; i < n; ++i) c->pub_ring.push_back((double2*)bufs[i]);
   c->pub_k = 0;
-  if (n > 0) DM_HIP(c, hipMemsetAsync(bufs[0], 0, sizeof(double2), c->stream), "publish ring");
+  // every buffer's record 0 starts clear: a tick clears only its own flags words of
+  // the next buffer (DevParams::pub_word)
+  for (int i = 0; i < n; ++i) DM_HIP(c, hipMemsetAsync(bufs[i], 0, sizeof(double2), c->stream), "publish ring");
+  if (n > 0) c->main_dirty = true;
   return DM_OK;
 }
 
@@ -2309,6 +2420,16 @@ int dm_hier_pipeline(dm_ctx* leaf, int on) {
 // its leaf -- in place, or into a staged slot the leaf takes one tick later
 // (dm_hier_pipeline).  Stream-ordered: the all-gather that produced `gathered`
 // must precede it on the root's stream.
+// The exchange's stream after leaf tick `seq`: its parts' events (dm_ctx::tick_ev).
+static hipError_t wait_tick(dm_ctx* leaf, uint64_t seq, hipStream_t s) {
+  const int k = (int)(seq % dm_ctx::kTickEv);
+  for (int j = 0; j < std::max(leaf->tick_nev[k], 1); ++j) {
+    hipError_t e = hipStreamWaitEvent(s, leaf->tick_ev[j][k], 0);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t now_ns, dm_ctx* leaf, int server) {
   DM_ENTER(root);
   DM_STORE_OK(root);
@@ -2334,13 +2455,20 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
   if (!leaf->cfg_loaded || leaf->R != leaf_R)
     return root->fail(DM_E_STATE, "the leaf must hold exactly this server's resources");
   const int64_t stride = root->hier_G != 0 ? root->hier_stride : 1 + root->R;
-  DM_HIP(root, leaf->join_aux(), "join leaf streams");
-  leaf->main_dirty = true;
+  const bool same = root->stream == leaf->stream;
+  // A pipelined leaf whose last tick's events cover its streams stays unjoined (the
+  // round writes a free template slot, and waits on those events); otherwise the leaf's
+  // streams join first.
+  const bool cover = !same && leaf->tpl_pipe && leaf->tick_covers();
+  if (!cover) {
+    DM_HIP(root, leaf->join_aux(), "join leaf streams");
+    leaf->main_dirty = true;
+  }
   DM_HIP(root, root->hier_status.ensure((size_t)kHierMaxServers), "hierarchy status");
   root->hier_servers = n_servers;
-  const bool same = root->stream == leaf->stream;
   if (!same && !root->hs_ordered) {  // the root round after the leaf's prior work (its publish)
-    DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->root order");
+    if (cover) DM_HIP(root, wait_tick(leaf, leaf->tick_seq, root->stream), "leaf->root order");
+    else DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->root order");
   }
   ResCfg* tcfg = leaf->cfg.p;
   ResCold* tcold = leaf->cold.p;
@@ -2357,8 +2485,16 @@ int dm_hier_root_tick(dm_ctx* root, const void* gathered, int n_servers, int64_t
     if (leaf->stream == root->stream) {
       // stream order: the ticks that read the slot's old templates precede this round
     } else if (leaf->tpl_free_rec[slot] && leaf->tpl_free_seq[slot] > 0) {  // the ticks that read the slot's old
-      DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tpl_free_seq[slot] % dm_ctx::kTickEv], 0),
-             "template slot");                                                // templates are done
+      if (cover && root->hs_ordered && leaf->tpl_free_seq[slot] <= leaf->tick_seq) {  // templates are done
+        // this round already waits for the leaf's last tick, whose events cover every
+        // earlier tick on the same streams
+      } else if (leaf->tick_seq - leaf->tpl_free_seq[slot] < (uint64_t)dm_ctx::kTickEv - 1) {
+        DM_HIP(root, wait_tick(leaf, leaf->tpl_free_seq[slot], root->stream), "template slot");
+      } else {  // that tick's events were recorded again since: everything the leaf holds
+        DM_HIP(root, leaf->join_aux(), "join leaf streams");
+        leaf->main_dirty = true;
+        DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "template slot");
+      }
     }
     else if (leaf->tpl_free_rec[slot])
       DM_HIP(root, leaf->xs_wait(leaf->tpl_free[slot], root->stream), "template slot");
@@ -2522,6 +2658,8 @@ int dm_hier_attach(dm_ctx* leaf, dm_ctx* root, int server, void* const* ring, in
   if (rc) return rc;
   if ((rc = dm_hier_pipeline(leaf, leaf->tpl_pipe ? leaf->tpl_lag : 1))) return rc;
   if ((rc = dm_set_stream(root, exchange_stream ? exchange_stream : leaf->stream))) return rc;
+  // an exchange on a stream of its own waits for every leaf tick: no stream parts
+  if ((rc = set_parts_ok(leaf, root->stream == leaf->stream))) return rc;
   root->hs_leaf = leaf;
   root->hs_server = server;
   root->hs_ring.assign(ring, ring + nring);
@@ -2539,15 +2677,16 @@ int dm_hier_step(dm_ctx* leaf, dm_ctx* root, int64_t now_ns) {
   const int G = root->hier_G;
   const void* gathered = block;
   if (G > 1) {
-    DM_HIP(root, leaf->join_aux(), "join leaf streams");
-    // the exchange stream after the tick that wrote the block: on the tick-done word when
-    // the tick stores it (no marker on the leaf's queue), else an event
+    // the exchange stream after the tick that wrote the block: on the tick's events when
+    // its last kernels complete them (no marker on the leaf's queues; the leaf's stream
+    // parts stay unjoined), else after a join, on an event
+    const bool cover = leaf->stream != root->stream && leaf->tick_covers();
+    if (!cover) DM_HIP(root, leaf->join_aux(), "join leaf streams");
     if (leaf->stream != root->stream) leaf->tick_signal_wanted = true;
     if (leaf->stream == root->stream) {
       // stream order
-    } else if (leaf->tick_flagged)
-      DM_HIP(root, hipStreamWaitEvent(root->stream, leaf->tick_ev[leaf->tick_seq % dm_ctx::kTickEv], 0),
-             "leaf->exchange order");
+    } else if (cover || (leaf->tick_flagged && leaf->tick_part_mask == 0))
+      DM_HIP(root, wait_tick(leaf, leaf->tick_seq, root->stream), "leaf->exchange order");
     else
       DM_HIP(root, leaf->xs_order(dm_ctx::XS_LEAF, leaf->stream, root->stream), "leaf->exchange order");
     const size_t bytes = (size_t)root->hier_stride * 16;
@@ -2626,7 +2765,7 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[8 + kNumBins];
+  int64_t v[9 + kNumBins];
   v[0] = (int64_t)c->h_tiles.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
@@ -2636,7 +2775,10 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   v[5 + kNumBins] = c->redo_cap;  // 3/4 of the redo's full-build workgroups the GPU holds at once
   v[6 + kNumBins] = 1;            // every store may speculate (the redo by teams has no bound)
   v[7 + kNumBins] = c->aux_own_queue ? 1 : 0;  // the work classes' streams each have a hardware queue
-  const int n = 8 + kNumBins;
+  int64_t parts = 1;  // the stream parts of the store's one workgroup bin (dm_ctx::kParts), else 1
+  for (int b = 0; b < kNumBins; ++b) parts = std::max<int64_t>(parts, c->bin_parts[b]);
+  v[8 + kNumBins] = parts;
+  const int n = 9 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }

@@ -40,8 +40,9 @@ extern "C" {
 
 /* 4 (round 5): dm_kernel_class_names, dm_hier_comm_info; dm_plan_info's slot 14 is the
    redo's co-resident workgroup bound (was the per-chunk redo's chunk bound), slot 15
-   always 1; the DM_* environment switches other than the test hooks are gone
-   (INTEGRATION.md §5).  3 (round 4): dm_hier_attach / dm_hier_step / dm_rccl_unique_id /
+   always 1, slot 16 the aux queues flag, slot 17 the stream parts; a published block's
+   record 0 holds two 32-bit flags words (their OR is the request's flags); the DM_*
+   environment switches other than the test hooks are gone.  3 (round 4): dm_hier_attach / dm_hier_step / dm_rccl_unique_id /
    dm_hier_comm_init and DM_E_INTERNAL added, dm_set_large_path and DM_LARGE_* removed. */
 #define DM_ABI_VERSION 4
 
@@ -262,7 +263,11 @@ int dm_publish_totals(dm_ctx* ctx, void* dev_dst);
  * its running sums, the validation flags OR-ed into record 0 -- and clears record 0 of
  * bufs[(k + 1) % n] for the next tick.  Three buffers keep a tick's block intact while
  * the pipelined exchange of the tick before (dm_hier_pipeline) still reads it.
- * n = 0 turns it off. */
+ * A store whose one workgroup bin runs in two stream parts (dm_plan_info slot 17) keeps
+ * one 32-bit flags word per part in record 0's first 8 bytes (part 0 the low word,
+ * part 1 the high word): the request's flags are their OR, and the int64 read of those
+ * bytes is nonzero exactly when the flags are.  This call clears record 0 of every
+ * buffer (stream-ordered).  n = 0 turns it off. */
 int dm_publish_ring(dm_ctx* ctx, int n, void* const* dev_bufs);
 
 /* Layout of the exchange, set once on the root context (default: replicated, with
@@ -383,7 +388,9 @@ int dm_reset_kernel_times(dm_ctx* ctx);
  * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), 3/4 of the redo's
  * full-build workgroups the GPU holds at once (its grid bound), and 1 (every store may
  * speculate: the redo by teams needs only 64 co-resident workgroups), and 1 when the
- * work classes' auxiliary streams each have a hardware queue of their own; returns 17 */
+ * work classes' auxiliary streams each have a hardware queue of their own, and the
+ * stream parts of the store's one workgroup bin (2: its halves run on two auxiliary
+ * streams, unjoined from tick to tick; else 1); returns 18 */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),

@@ -93,7 +93,8 @@ def published(gathered, G, R, stride=None):
     out = []
     for g in range(G):
         b = rec[g * S:g * S + 1 + R]
-        out.append((b[1:, 0].copy(), b[1:, 1].copy().view(np.int64), int(b[0, 0:1].view(np.int64)[0])))
+        f = int(b[0, 0:1].view(np.uint64)[0])  # the OR of record 0's two flags words (DevParams::pub_word)
+        out.append((b[1:, 0].copy(), b[1:, 1].copy().view(np.int64), (f & 0xFFFFFFFF) | (f >> 32)))
     return out
 
 
@@ -688,3 +689,73 @@ def test_native_step_matches_the_python_step(G, native):
             assert a[2][k].tobytes() == b[2][k].tobytes(), f"step {t}: root {k}"
         for k in ("count", "sum_has", "sum_wants"):
             assert a[3][k].tobytes() == b[3][k].tobytes(), f"step {t}: root running {k}"
+
+
+def test_native_step_with_stream_parts_matches_the_python_step():
+    """The N = 8 rehearsal's shape with a leaf whose one workgroup bin qualifies for two
+    stream parts (dm_plan_info "stream_parts"): the Python sequence (HierarchicalTick
+    without `native`, its exchange on a stream of its own) keeps the parts -- ticks in
+    two unjoined parts, the root round waiting on both parts' tick events, the template
+    slots' reuse likewise -- while dm_hier_attach turns them off (the exchange's waits
+    cost more than the parts gain).  dm_hier_step issued back to back with nothing read
+    between the steps, and synced after each, against the Python sequence synced after
+    each: leases, templates in use, root rows and running sums bit for bit."""
+    import torch
+    from doorman_amd.engine import Engine
+    from doorman_amd.hierarchy import HierarchicalTick, partition, root_snapshot
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(808)
+    G = 3
+    sizes = rng.integers(257, 400, G * 4200)
+    R = len(sizes)
+    lo = partition(sizes, G)
+    S = 1 + int(np.diff(lo).max())
+    rcfg = root_config(R, rng)
+    full = W.make_snapshot(sizes, rng.uniform(0.2, 3.0, int(sizes.sum())) * 1000.0 / np.repeat(sizes, sizes),
+                           0.0, 1, NOW + 60 * W.NS, W.FAIR_SHARE, 1000.0)
+    others = np.zeros((G * S, 2))
+    for j in range(1, G):
+        sj = W.subset(full, np.arange(lo[j], lo[j + 1]))
+        n = int(lo[j + 1] - lo[j])
+        others[j * S + 1:j * S + 1 + n, 0] = sj["agg_sum_wants"]
+        others[j * S + 1:j * S + 1 + n, 1] = np.asarray(sj["agg_count"], np.int64).view(np.float64)
+    shard = W.subset(full, np.arange(lo[0], lo[1]))
+    steps = [NOW + t * W.NS for t in (0, 2, 5, 9, 14, 15, 19, 24, 30, 31)]
+    runs = {}
+    for mode, sync_each in (("local", False), ("local", True), (None, True)):
+        leaf, root = Engine(0), Engine(0)
+        leaf.load(M.with_config(shard, M.default_config(int(lo[1] - lo[0]))))
+        root.load(M.with_config(root_snapshot(R, 1, W.FAIR_SHARE, 1.0), rcfg))
+        assert leaf.plan_info()["stream_parts"] == 2
+
+        def gather(src, dst):
+            dst[0:S].copy_(src)
+        ht = HierarchicalTick(torch, leaf, root, R, G, 0, gather, shard_lo=lo, pipelined=True, native=mode)
+        assert leaf.plan_info()["stream_parts"] == (1 if mode else 2)
+        ht.gathered[0].copy_(torch.from_numpy(others).to(ht.gathered[0].device))
+        torch.cuda.synchronize()
+        out = []
+        for now in steps:
+            ht.tick(now, asynchronous=not sync_each)
+            if sync_each:
+                ht.sync()
+                out.append((leaf.leases(), leaf.config(), root.read_store(), root.resources(safe=False)))
+        ht.sync()
+        ht.check()
+        out.append((leaf.leases(), leaf.config(), root.read_store(), root.resources(safe=False)))
+        runs[(mode, sync_each)] = out
+        leaf.close()
+        root.close()
+
+    def same(a, b, label):
+        for x, y in zip(a[0], b[0]):
+            assert x.tobytes() == y.tobytes(), f"{label}: leases"
+        assert_cfg_equal(a[1], b[1], f"{label}: templates")
+        for k in ("has", "wants", "subclients", "expiry_ns"):
+            assert a[2][k].tobytes() == b[2][k].tobytes(), f"{label}: root {k}"
+        for k in ("count", "sum_has", "sum_wants"):
+            assert a[3][k].tobytes() == b[3][k].tobytes(), f"{label}: root running {k}"
+    py = runs[(None, True)]
+    for t, (a, b) in enumerate(zip(runs[("local", True)], py)):
+        same(a, b, f"synced step {t}")
+    same(runs[("local", False)][-1], py[-1], "back-to-back steps, after the last")
