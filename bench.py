@@ -412,7 +412,13 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
     name, (launches, total_ms) = max(ktimes.items(), key=lambda kv: kv[1][1])
     avg_s = total_ms / launches / 1e3
     single = single_kernel_tick and len(ktimes) == 1 and launches == steps
-    if single:  # one kernel per tick: HIP events around the timed region itself
+    # stream parts (dm_plan_info): the store's one workgroup bin runs as `parts` concurrent
+    # launches over its halves, unjoined from tick to tick; its roofline is the whole bin's
+    # bytes per tick over the tick's time (both launches together), not one half over a
+    # launch that shares the GPU with the other
+    parts = int(run.get("parts", 1))
+    in_parts = parts > 1 and len(ktimes) == 1 and launches == parts * steps
+    if single or in_parts:  # one kernel class per tick: HIP events around the timed region itself
         avg_s = run["stream_ms"] / steps / 1e3
     units = kernel_units(snap)
     if name not in units:
@@ -428,6 +434,8 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
             traffic = json.load(open(pmc_path)).get(name, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+        if traffic is not None and in_parts:  # the PMC passes count per launch: per tick, both parts
+            traffic = traffic * parts
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
             "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
@@ -457,7 +465,11 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
                                       "exchange's publish and root round included; concurrent classes overlap)",
             "timed_region_stream_us_per_step": round(run["stream_ms"] * 1e3 / steps, 2),
             "duration_source": ("HIP event pair around the timed region on the kernel's stream (one kernel "
-                                "per tick)" if single else "HIP events around every launch, profiled region")}
+                                "per tick)" if single else
+                                f"HIP event pair around the timed region (the bin's {parts} concurrent stream-part "
+                                f"launches per tick, joined at its end; bytes and traffic per tick)" if in_parts else
+                                "HIP events around every launch, profiled region"),
+            "stream_parts": parts}
 
 
 # ---------------------------------------------------------------------------
@@ -890,6 +902,7 @@ def main():
         run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4",
                           also=[root] if root is not None else [])
         run["dense_frac"] = tick_dense_fraction(eng, snap, step)
+        run["parts"] = int(eng.plan_info().get("stream_parts", 1))
         if ht is not None:
             ht.sync()
             ht.check()  # any server whose request the root rejected (server.go:863-866) fails loudly
@@ -952,6 +965,7 @@ def main():
                 stx = lambda: ex.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
             rx = timed_steps(torch, ex, stx, kx, args.warmup, sync_ranks, extra_warm=name != "c4")
             rx["dense_frac"] = tick_dense_fraction(ex, snapx, stx)
+            rx["parts"] = int(ex.plan_info().get("stream_parts", 1))
             extra[name] = workload_line(name, snapx, rx, kx, single_kernel_tick=name == "c1")
             extra[name]["aux_own_queues"] = bool(ex.plan_info().get("aux_own_queues", 0))
             ex.close()

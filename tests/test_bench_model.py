@@ -73,6 +73,24 @@ def test_large_spec_roofline_counts_the_large_class_only():
     assert 6.0e6 < r["leases_per_launch"] < 6.2e6 and r["resources_per_launch"] == 244
 
 
+def test_stream_parts_roofline_is_per_tick():
+    """C1's one bin in two stream parts: two concurrent launches per tick, each over half
+    the bin.  The roofline takes the whole bin's bytes over the tick's time (the timed
+    region's events), and the PMC traffic (recorded per launch) times the parts."""
+    snap = bench.make_workload("c1", 0)
+    steps = 10
+    run = {"ktimes": {"block128x8_dense": (2 * steps, 0.6)}, "stream_ms": 0.4, "dense_frac": 1.0, "parts": 2}
+    r = bench.roofline_of("c1", snap, run, steps, True)
+    N, R = len(snap["wants"]), len(snap["seg_off"]) - 1
+    assert r["stream_parts"] == 2 and r["leases_per_launch"] == N
+    assert r["avg_launch_us"] == 40.0  # 0.4 ms over 10 ticks, not 0.6 ms over 20 launches
+    assert abs(r["achieved"] - (24 * N + 97 * R) / 40e-6 / 1e9) < 0.1
+    if r["traffic"] is not None:
+        import json
+        per_launch = json.load(open(os.path.join(ROOT, "profiles", "pmc_c1.json")))["block128x8_dense"]
+        assert r["traffic"] == 2 * per_launch["hbm_bytes_per_launch"]
+
+
 def test_self_check_root_round_matches_the_reference_model():
     """bench.root_round_one (the N > 1 exchange self-check's restatement of the sharded
     root round, one row per resource) against the hierarchy model (tests/hier_model.py:

@@ -28,7 +28,7 @@ CLASS = [
     (r"k_block_rest<256, 16>", "block2k4k_rest"),
     (r"k_large_t\b", "large_t"), (r"k_large_c_het\b", "large_c_het"), (r"k_large_e\b", "large_e"),
     (r"k_large_map_het\b", "large_map_het"),
-    (r"k_block<128, 4(, \d)?>", "block128x4_mixed"), (r"k_block<128, 8(, \d)?>", "block128x8_mixed"), (r"k_block<256, 2(, \d)?>", "block256x2"), (r"k_block<256, 4(, \d)?>", "block256x4"),
+    (r"k_block<128, 4(, \d)?>", "block128x4"), (r"k_block<128, 8(, \d)?>", "block128x8"), (r"k_block<256, 2(, \d)?>", "block256x2"), (r"k_block<256, 4(, \d)?>", "block256x4"),
     (r"k_block<256, 8(, \d)?>", "block256x8"), (r"k_block<512, 8(, \d)?>", "block2k4k"), (r"k_block<256, 16(, \d)?>", "block2k4k"), (r"k_block<512, 4(, \d)?>", "block512x4"), (r"k_block<1024, 4(, \d)?>", "block1024x4"),
     (r"k_wave<4(, \d)?>", "wave64x4"), (r"k_sub<16, 4>", "sub16x4"), (r"k_sub<32, 4>", "sub32x4"),
     (r"k_sub<8, 2>", "sub8x2"), (r"k_sub<16, 2>", "sub16x2"),
