@@ -1020,7 +1020,8 @@ def main():
                                        else f"resource-sharded x{world} (no data-path collective)"),
                        "writeback": True},
             "exchange": exchange_used["mode"] if hier else None,
-            "dist": dist_fields(dist_info, run) if world > 1 else None,
+            # (a rehearsal reports its exchange self-check too: one rank of the rehearsed node)
+            "dist": dist_fields(dist_info, run) if world > 1 or args.rehearse_shard else None,
             "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
             "host_enqueue_us_per_step": round(run["host_enqueue_s"] / args.steps * 1e6, 2),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
