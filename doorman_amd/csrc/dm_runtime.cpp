@@ -166,10 +166,9 @@ struct dm_ctx {
   static constexpr int kAux = 4;
   // auxiliary stream of each work class: bins 0..kNumBins-1, small tiles, large chain
   // (round 4 moved every bin to each other stream in A/Bs: this split won every one)
-#ifndef DM_CLASS_STREAMS
-#define DM_CLASS_STREAMS 2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0
-#endif
-  static constexpr int class_stream[kNumBins + 2] = {DM_CLASS_STREAMS};  // C2: 200 -> 189 us (small class alone)
+  // (round 5, with the small tiles: bin 3 on stream 3 112.8-117.3 us, on stream 1
+  // 112.8-114.2, bin 6 on stream 3 127-129, against 111.0-112.4 us; profiles/r05_c2_classes.md)
+  static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (small class alone)
   hipStream_t aux[kAux] = {};
   bool aux_own_queue = false;  // each auxiliary stream has a hardware queue of its own (CU mask)
   uint64_t aux_seq = 0;        // the stream set's creation order in the process (take_aux)
