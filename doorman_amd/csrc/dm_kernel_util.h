@@ -382,9 +382,11 @@ __device__ __forceinline__ const T* col_at(const T* base, uint32_t i) {
 // Store a decided live row (row0 + i; row0 wave-uniform where the caller can): its
 // gets, and in a writeback tick it becomes a follower (only an explicit row's
 // subclients word changes); otherwise its expiry.
+template <bool NT = true>
 __device__ __forceinline__ void put_live(const DevParams& p, int64_t row0, uint32_t i, double g, const Res& rs,
                                          int32_t raw) {
-  __builtin_nontemporal_store(g, col_at(p.out_gets + row0, i));
+  if constexpr (NT) __builtin_nontemporal_store(g, col_at(p.out_gets + row0, i));
+  else *col_at(p.out_gets + row0, i) = g;
   if (p.writeback) {
     if (raw < 0) *col_at(p.out_sub + row0, i) = raw & 0x7FFFFFFF;
   } else {
@@ -393,8 +395,10 @@ __device__ __forceinline__ void put_live(const DevParams& p, int64_t row0, uint3
 }
 // Store a row Clean released: no lease; in a writeback tick the row is zeroed and
 // marked released (once: an already released row is left alone).
+template <bool NT = true>
 __device__ __forceinline__ void put_released(const DevParams& p, int64_t row0, uint32_t i, int32_t raw) {
-  __builtin_nontemporal_store(0.0, col_at(p.out_gets + row0, i));
+  if constexpr (NT) __builtin_nontemporal_store(0.0, col_at(p.out_gets + row0, i));
+  else *col_at(p.out_gets + row0, i) = 0.0;
   if (p.writeback) {
     if (!sub_released(raw)) {
       *col_at(p.out_wants + row0, i) = 0.0;

@@ -30,6 +30,14 @@ namespace dm {
 // all; a stale hint queues the item for k_block_rest and returns), kRest = queued
 // items (k_block_rest: the column is read, the hint rewritten).
 enum { kMixed = 0, kDenseOnly = 1, kRest = 2 };
+// Gets stores: non-temporal for the workgroup bins and the large chain (long contiguous
+// spans: whole lines); plain for the sub-wave groups, whose spans are short and
+// unaligned, so that L2 merges the partial sectors two groups write at a resource
+// boundary (C2 112.2-112.5 -> 109.6-111.1 us, three interleaved rounds; the chain's
+// stores plain: no change; profiles/r05_ab/c2_gets_stores.txt)
+template <int G> constexpr bool kGroupNT = G >= 128;
+constexpr bool kSpecNT = true;
+
 template <int G, int R, int MODE = kMixed>
 __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem wi, WorkItem* item, int t,
                                               Lds<G>& lds, int32_t* general_list, int32_t* general_count,
@@ -260,7 +268,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     if (!(valid >> k & 1)) continue;
     const unsigned u = (unsigned)(k * G + t);
     if (!(live >> k & 1)) {  // released by Clean: no lease
-      put_released(p, lo, u, (relm >> k & 1) ? (int)kSubReleased : sr[k]);
+      put_released<kGroupNT<G>>(p, lo, u, (relm >> k & 1) ? (int)kSubReleased : sr[k]);
       continue;
     }
     double g;
@@ -278,7 +286,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     } else {
       g = fs_uniform_row(w[k], h[k], C, cl.sum_has, fu);
     }
-    put_live(p, lo, u, g, rs, sr[k]);
+    put_live<kGroupNT<G>>(p, lo, u, g, rs, sr[k]);
     delta.v += g - h[k];
   }
 
@@ -2229,7 +2237,7 @@ __global__ __launch_bounds__(256) void k_large_map_het(DevParams p, const Chunk*
     const unsigned u = (unsigned)(k * 256 + t);
     const double w = rw.w[k], h = rw.h[k];
     if (!(rw.live >> k & 1)) {
-      put_released(p, ch.row0, u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
+      put_released<kSpecNT>(p, ch.row0, u, (rw.rel >> k & 1) ? (int32_t)kSubReleased : 0);
       continue;
     }
     const long long s = rw.s[k];
@@ -2242,7 +2250,7 @@ __global__ __launch_bounds__(256) void k_large_map_het(DevParams p, const Chunk*
       }
       g = fs_stage2(w, h, s, C, st.cl.sum_has, eq, b.x, b.i, Tr, c);
     }
-    put_live(p, ch.row0, u, g, st.rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
+    put_live<kSpecNT>(p, ch.row0, u, g, st.rs, (rw.expl >> k & 1) ? (p.sub[ch.row0 + u] | (int32_t)kSubExplicit) : 0);
     delta.v += g - h;
   }
   delta = group_reduce<256>(delta, OpSumD(), lds.d);
