@@ -1,6 +1,8 @@
 #!/bin/bash
 # GPU call (round 5): the N=8 rehearsal step per stream choice of the hierarchy
 # (DM_PROBE_HIER, a probe build of doorman_amd/hierarchy.py), REPS rounds interleaved
+# (round-5 probe: the probe builds come from tools/attempts/r05_parts_exchange_probes.patch /
+#  r05_queue_probes.patch applied on the round-5 source; results in profiles/r05_parts_ab.txt)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

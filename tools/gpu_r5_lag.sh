@@ -1,3 +1,11 @@
+#!/bin/bash
+# GPU call (round 5, probe): the N=8 rehearsal step with two, three and four ticks of template
+# lag (DM_PROBE_LAG in a probe build of doorman_amd/hierarchy.py, template slots from a
+# DM_TPL_SLOTS=6 library build)
+# (round-5 probe: the probe builds come from tools/attempts/r05_parts_exchange_probes.patch /
+#  r05_queue_probes.patch applied on the round-5 source; results in profiles/r05_parts_ab.txt)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/r5lag
 for rep in 1 2; do
 for cfg in "2 base" "3 slots6" "4 slots6"; do

@@ -2,6 +2,8 @@
 # GPU call (round 5, probe): single-context workloads with the CU bits DM_PROBE_RESBITS
 # left out of the library's auxiliary streams (tools/ab_libs/res.so), then the N=8
 # rehearsal with the exchange stream masked to those CUs (DM_PROBE_HIER=xres)
+# (round-5 probe: the probe builds come from tools/attempts/r05_parts_exchange_probes.patch /
+#  r05_queue_probes.patch applied on the round-5 source; results in profiles/r05_parts_ab.txt)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/r5res2
