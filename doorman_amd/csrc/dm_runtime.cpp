@@ -180,9 +180,9 @@ struct dm_ctx {
   // idles the consuming queue ~12-20 us on the box (tools/xs_probe.py); stream-memory
   // tokens (hipStreamWriteValue64 / WaitValue64, which this ROCm runs as blit kernels
   // of 3-5 us each plus a dispatch gap) measured no cheaper per step (round 4: 75.0 vs
-  // 72.2 us per N = 8 shard step) and were retired in round 5.  The one stream-memory
-  // signal kept is the tick-done word (below).  A wait on a token signalled on the
-  // waiting stream itself is skipped (stream order).
+  // 72.2 us per N = 8 shard step) and were retired in round 5, as was the tick-done
+  // word (the tick's last kernels' stop events replaced it: tick_ev below).  A wait on
+  // a token signalled on the waiting stream itself is skipped (stream order).
   static constexpr int kTplSlots = 4;  // staged templates: in use + pending (lag 2) + the one being written
   enum : int {
     XS_FORK = 0,
@@ -1333,8 +1333,9 @@ static int commit_templates(dm_ctx* c) {
   std::swap(c->cfg, c->tpl_cfg[take]);
   std::swap(c->cold, c->tpl_cold[take]);
   // the old templates (now in slot `take`) are free after the ticks already enqueued
-  // the next exchange into it waits for the ticks enqueued so far: on the tick-done word
-  // when the last of them stores it, else on a (lazy) event
+  // the next exchange into it waits for the ticks enqueued so far: on the last tick's
+  // events (tick_ev, every stream part's) when its last kernels complete them, else on
+  // a (lazy) event
   c->tpl_free_seq[take] = c->tick_flagged ? c->tick_seq : 0;
   c->xs_signal_lazy(dm_ctx::XS_FREE0 + take, c->stream, &c->tpl_free[take]);
   c->tpl_free_rec[take] = true;
