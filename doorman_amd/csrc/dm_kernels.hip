@@ -2513,7 +2513,7 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
                                                     const int32_t* __restrict__ word_pre,
                                                     const double* __restrict__ wants, RowIndex ix,
                                                     const int32_t* __restrict__ s_sub, double* s_wants, ResAgg* agg,
-                                                    uint32_t* flags) {
+                                                    uint32_t* flags, int64_t vlo, int64_t vhi) {
   if (*flags & kUpdReject) return;  // uniform over the grid
   const int lane = threadIdx.x & 63;
   const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kMaskWords;
@@ -2521,15 +2521,25 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
   const int nw = nwords - w0 < kMaskWords ? (int)(nwords - w0) : kMaskWords;
   uint64_t my_m = 0ull;
   int64_t my_off = 0, my_end = 0;
-  int my_seg = 0;
   if (lane < nw) {
     const int64_t w = w0 + lane;
     my_m = mask[w];
     my_off = block_offs[w >> 8] + word_pre[w];
-    my_seg = seg_of_row(ix, first_row + 64 * w);
+  }
+  // only the values [vlo, vhi) have landed (dm_store_apply copies them in chunks): a
+  // wave whose words' values all lie outside is done
+  {
+    const int64_t first = readlane_any(my_off, 0);
+    const int64_t last = readlane_any(my_off, nw - 1) + __popcll(readlane_any(my_m, nw - 1));  // one past
+    if (last <= vlo || first >= vhi) return;
+  }
+  int my_seg = 0;
+  if (lane < nw) {
+    my_seg = seg_of_row(ix, first_row + 64 * (w0 + lane));
     my_end = ix.seg_off[my_seg + 1];  // the word lies in one resource iff its last row < my_end
   }
   const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t inr = 0;  // bit q: this lane's row of word q is set and its value in [vlo, vhi)
   double v[kMaskWords], old[kMaskWords];
   uint32_t freed = 0;  // bit q: this lane's row of word q is released (k_update_wants: left alone)
 #pragma unroll
@@ -2538,8 +2548,10 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
     old[q] = 0.0;
     if (q < nw) {
       const uint64_t m = readlane_any(my_m, q);
-      if ((m >> lane) & 1ull) {
-        v[q] = wants[readlane_any(my_off, q) + __popcll(m & below)];
+      const int64_t vi = readlane_any(my_off, q) + __popcll(m & below);
+      if (((m >> lane) & 1ull) && vi >= vlo && vi < vhi) {
+        inr |= 1u << q;
+        v[q] = wants[vi];
         old[q] = s_wants[first_row + 64 * (w0 + q) + lane];
         freed |= (sub_released(s_sub[first_row + 64 * (w0 + q) + lane]) ? 1u : 0u) << q;
       }
@@ -2553,7 +2565,7 @@ __global__ __launch_bounds__(256) void k_mask_apply(int64_t nwords, const uint64
     const uint64_t m = q < nw ? readlane_any(my_m, q) : 0ull;
     if (m != 0ull) {  // uniform
       const int64_t row0 = first_row + 64 * (w0 + q);
-      const bool act = ((m >> lane) & 1ull) && !(freed >> q & 1u);
+      const bool act = (inr >> q & 1u) && !(freed >> q & 1u);
       const int s0 = __builtin_amdgcn_readlane(my_seg, q);
       const bool single = readlane_any(my_end, q) > row0 + 63 - __builtin_clzll(m);
       double d = 0.0;
@@ -3184,14 +3196,18 @@ hipError_t launch_publish(int64_t R, const ResAgg* agg, void* dst, uint32_t* syn
 hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
                                     int64_t n_values, const double* wants, int64_t* block_sums, int32_t* word_pre,
                                     const RowIndex& ix, const int32_t* s_sub, double* s_wants, ResAgg* agg,
-                                    uint32_t* flags, hipStream_t st) {
+                                    uint32_t* flags, hipStream_t st, int phase, int64_t vlo, int64_t vhi) {
   if (nwords <= 0) return hipSuccess;
   const int64_t nb = (nwords + 255) / 256;
-  k_mask_count<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, N, block_sums, word_pre, flags);
-  k_mask_scan<<<1, 1024, 0, st>>>(nb, block_sums, n_values, flags);
-  const int64_t waves = (nwords + kMaskWords - 1) / kMaskWords;
-  k_mask_apply<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(nwords, mask, first_row, block_sums, word_pre, wants, ix,
-                                                            s_sub, s_wants, agg, flags);
+  if (phase != 1) {  // the mask's counts and value offsets (the mask alone)
+    k_mask_count<<<(unsigned)nb, 256, 0, st>>>(nwords, mask, first_row, N, block_sums, word_pre, flags);
+    k_mask_scan<<<1, 1024, 0, st>>>(nb, block_sums, n_values, flags);
+  }
+  if (phase != 0) {  // the rows whose values [vlo, vhi) have landed
+    const int64_t waves = (nwords + kMaskWords - 1) / kMaskWords;
+    k_mask_apply<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(nwords, mask, first_row, block_sums, word_pre, wants, ix,
+                                                              s_sub, s_wants, agg, flags, vlo, vhi);
+  }
   return hipGetLastError();
 }
 

@@ -62,7 +62,7 @@ hipError_t launch_update_wants(int64_t n, const int64_t* rows, const double* wan
 hipError_t launch_update_wants_mask(int64_t nwords, const uint64_t* mask, int64_t first_row, int64_t N,
                                     int64_t n_values, const double* wants, int64_t* block_sums, int32_t* word_pre,
                                     const RowIndex& ix, const int32_t* s_sub, double* s_wants, ResAgg* agg,
-                                    uint32_t* flags, hipStream_t st);
+                                    uint32_t* flags, hipStream_t st, int phase, int64_t vlo, int64_t vhi);
 hipError_t launch_carry_reject(const uint32_t* from, uint32_t* to, hipStream_t st);
 hipError_t launch_decide(const DevParams& p, const ReqItem* items, int nitems, const ReqArgs& q, hipStream_t st);
 hipError_t fd_rows(const DevParams& p, const ReqItem& it, const FastItem& fi, int slot, const ReqArgs& q,
@@ -403,6 +403,8 @@ struct dm_ctx {
   DBuf<uint32_t> bat_flags; // dm_store_apply: one flags word per part
   uint32_t* h_bat_flags = nullptr;
   hipEvent_t ev_bat[3] = {};
+  static constexpr int kWChunks = 4;  // dm_store_apply: the refresh values' copy chunks
+  hipEvent_t ev_wchunk[kWChunks] = {};
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
   // dm_decide: a round's requests (grouped by resource), per-resource work items, results
@@ -1067,6 +1069,8 @@ int dm_create(int device, dm_ctx** out) {
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
+  for (int i = 0; i < dm_ctx::kWChunks && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&c->ev_wchunk[i], hipEventDisableTiming);
   for (int j = 0; j < dm_ctx::kParts; ++j)
     for (int i = 0; i < dm_ctx::kTickEv && e == hipSuccess; ++i) e = hipEventCreate(&c->tick_ev[j][i]);
   if (e != hipSuccess) {
@@ -1110,6 +1114,8 @@ void dm_destroy(dm_ctx* c) {
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_bat)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : c->ev_wchunk)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& row : c->tick_ev)
     for (auto ev : row)
@@ -2139,7 +2145,7 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
   DM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_stage[0], 0), "stage update");
   DM_HIP(c, launch_update_wants_mask(nwords, c->st_mask.p, first_row, c->N, n, c->st_wants.p, c->st_blk.p,
                                      c->st_wpre.p, c->row_index(), c->sub.p, c->wants.p, c->agg.p, c->upd_flags.p,
-                                     c->stream),
+                                     c->stream, 2, 0, INT64_MAX),
          "masked update");
   DM_HIP(c, hipMemcpyAsync(c->h_flags, c->upd_flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream),
          "update flags");
@@ -2216,6 +2222,8 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
   }
   DM_HIP(c, hipMemsetAsync(c->bat_flags.p, 0, 3 * sizeof(uint32_t), st), "batch flags");
   uint32_t* F = c->bat_flags.p;
+  // the refresh's packed values cross in up to kWChunks chunks of >= 2^21 values
+  const int nchunk = nw > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(dm_ctx::kWChunks, nm >> 21)) : 0;
   // copies, back to back
   if (nw > 0) {
     DM_HIP(c, c->st_mask.ensure((size_t)nw), "stage mask");
@@ -2223,9 +2231,16 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     DM_HIP(c, c->st_blk.ensure((size_t)((nw + 255) / 256)), "stage block sums");
     DM_HIP(c, c->st_wpre.ensure((size_t)nw), "stage word offsets");
     DM_HIP(c, hipMemcpyAsync(c->st_mask.p, b->wants_mask, (size_t)nw * 8, hipMemcpyHostToDevice, cp), "stage mask");
-    if (nm > 0)
-      DM_HIP(c, hipMemcpyAsync(c->st_mwants.p, b->wants, (size_t)nm * 8, hipMemcpyHostToDevice, cp), "stage wants");
     DM_HIP(c, hipEventRecord(c->ev_bat[0], cp), "stage");
+    // the packed values in chunks, each applied as soon as it has landed (the apply
+    // of one chunk overlaps the next one's copy): C4 3.2 -> ~3.0 ms per step
+    for (int k = 0; k < nchunk; ++k) {
+      const int64_t v0 = nm * k / nchunk, v1 = nm * (k + 1) / nchunk;
+      if (v1 > v0)
+        DM_HIP(c, hipMemcpyAsync(c->st_mwants.p + v0, b->wants + v0, (size_t)(v1 - v0) * 8, hipMemcpyHostToDevice, cp),
+               "stage wants");
+      DM_HIP(c, hipEventRecord(c->ev_wchunk[k], cp), "stage");
+    }
   }
   if (nr > 0) {
     DM_HIP(c, c->st_rel.ensure((size_t)nr), "stage release rows");
@@ -2248,12 +2263,22 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
         DM_HIP(c, hipMemcpyAsync(col.dst, col.src, (size_t)nu * col.elem, hipMemcpyHostToDevice, cp), "stage upsert");
     DM_HIP(c, hipEventRecord(c->ev_bat[2], cp), "stage");
   }
-  // part 1: wants refresh (validated by its count/scan passes before the apply)
+  // part 1: wants refresh (validated by its count/scan passes over the mask, then
+  // applied chunk by chunk as the values land)
   if (nw > 0) {
     DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[0], 0), "stage");
     DM_HIP(c, launch_update_wants_mask(nw, c->st_mask.p, b->wants_first_row, c->N, nm, c->st_mwants.p, c->st_blk.p,
-                                       c->st_wpre.p, c->row_index(), c->sub.p, c->wants.p, c->agg.p, F + 0, st),
+                                       c->st_wpre.p, c->row_index(), c->sub.p, c->wants.p, c->agg.p, F + 0, st, 0, 0, 0),
            "masked update");
+    for (int k = 0; k < nchunk; ++k) {
+      const int64_t v0 = nm * k / nchunk, v1 = nm * (k + 1) / nchunk;
+      DM_HIP(c, hipStreamWaitEvent(st, c->ev_wchunk[k], 0), "stage");
+      if (v1 > v0)
+        DM_HIP(c, launch_update_wants_mask(nw, c->st_mask.p, b->wants_first_row, c->N, nm, c->st_mwants.p,
+                                           c->st_blk.p, c->st_wpre.p, c->row_index(), c->sub.p, c->wants.p, c->agg.p,
+                                           F + 0, st, 1, v0, v1),
+               "masked update");
+    }
   }
   // part 2: departures
   if (nr > 0) {

@@ -748,6 +748,51 @@ def test_store_apply_matches_sequential_calls(eng):
         other.close()
 
 
+def test_store_apply_chunked_refresh_matches_sequential_calls(eng):
+    """A refresh of more than 2^23 values crosses PCIe in four chunks, each applied as it
+    lands (dm_store_apply): the same store as dm_store_update_wants_mask + release +
+    upsert one after another (wants bit for bit, sums within 1e-12), with updated rows
+    in every chunk and in every resource, departures and arrivals after them, and a
+    refreshed row that also departs (the departure wins in both)."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(43)
+    sizes = rng.integers(700, 1300, 10_000)
+    N = int(sizes.sum())
+    snap = W.make_snapshot(sizes, rng.uniform(0.5, 2.0, N), rng.uniform(0.0, 1.0, N), 1,
+                           np.full(N, NOW + 600 * W.NS), W.FAIR_SHARE, 1000.0)
+    cap = np.maximum(snap["capacity"], 1.0)
+    upd = np.arange(1, N, 1, dtype=np.int64)[rng.random(N - 1) < 0.9]  # ~9M values: four chunks
+    assert len(upd) > 4 << 21
+    w = rng.uniform(0.5, 1.5, len(upd))
+    gone = np.sort(rng.choice(upd, 20_000, replace=False))  # refreshed, then departing
+    free = np.setdiff1d(np.arange(N), upd)[:5000]
+    k = len(free)
+    ups = (free, None, rng.uniform(0.5, 1.5, k), np.ones(k, np.int64), np.full(k, NOW + 900 * W.NS))
+    other = Engine(0)
+    try:
+        eng.load(snap)
+        other.load(snap)
+        eng.apply(W.rows_to_mask(upd, N), w, gone, ups, now_ns=NOW)
+        other.update_wants_mask(W.rows_to_mask(upd, N), w)
+        other.release(gone)
+        other.upsert(free, np.zeros(k), ups[2], ups[3], ups[4])
+        s1, s2 = eng.read_store(), other.read_store()
+        for key in ("has", "wants", "subclients", "expiry_ns"):
+            assert s1[key].tobytes() == s2[key].tobytes(), key
+        r1, r2 = eng.resources(safe=False), other.resources(safe=False)
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        for key in ("sum_has", "sum_wants"):
+            assert float_close(r1[key], r2[key], cap, 1e-12).all(), key
+        live = s1["expiry_ns"] != W.RELEASED
+        want = snap["wants"].copy()
+        want[upd] = w
+        want[gone] = 0.0
+        want[free] = ups[2]
+        assert s1["wants"][live].tobytes() == want[live].tobytes()
+    finally:
+        other.close()
+
+
 def test_store_apply_stops_at_the_first_rejected_part(eng):
     """A rejected part (duplicate departure rows) returns its error; the refresh before
     it stays applied, the arrivals after it are not; a bad mask rejects everything."""
