@@ -2404,8 +2404,8 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex 
     ds = -(long long)sub_value(s_sub[r]);
     s_has[r] = 0.0;
     s_wants[r] = 0.0;
-    s_sub[r] = (int32_t)kSubReleased;
-    s_exp[r] = kReleased;
+    s_sub[r] = (int32_t)kSubReleased;  // the mark every reader decodes first: the expiry column is left alone
+    (void)s_exp;
     if (expl[seg] >= 2) expl[seg] = 0;  // no longer dense: the next tick reads the subclients column
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
