@@ -40,6 +40,11 @@ constexpr int kNumBins = 9;  // sub16x4, sub32x4, wave64x4, block128x{4,8}, bloc
 // event time) or, when it holds most of the store's rows, on 512 x 8 (12.7 against
 // 15.2 us alone): launch_bin* take kBin6Wide for the latter.
 constexpr int kBin6Wide = 9;
+// Bin 4 (513-1024 rows) on one wave per resource (64 lanes x 16 rows: every reduction a
+// wave reduction, no LDS round or barrier) when most of its resources are FairShare,
+// whose round 2 is one more reduction than ProportionalShare's (C1 FairShare 41.0-41.8
+// -> 38.1-38.7 us; ProportionalShare 37.7-38.0 -> 39.0: profiles/r05_ab/b4_one_wave.txt).
+constexpr int kBin4Wave = 10;
 // Lease-table footprint (48 B per lease) above which a tick is taken to stream
 // from HBM rather than partly from the 256 MiB Infinity Cache (launch_bin).
 constexpr int64_t kStreamBytes = 1LL << 30;

@@ -45,7 +45,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
                                               int32_t qidx = 0, int32_t* guard = nullptr, int qcap = 0) {
   // the dense state (below): every workgroup kernel tracks it and writes the hints;
   // only the 128-thread mixed kernel and the dense-only kernels load by the hint
-  constexpr bool kDense = G >= 128;
+  constexpr bool kDense = G >= 128 || (G == 64 && R >= 16);  // (64 x 16: kBin4Wave)
   constexpr bool kHintLoad = (G == 128 && MODE == kMixed) || MODE == kDenseOnly;
   const int seg = wi.seg;
   const int64_t lo = wi.lo;
@@ -2999,6 +2999,7 @@ hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_
   switch (bin) {
     case 3: k_block<128, 4><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
     case 4: k_block<128, 8><<<n, 128, 0, st>>>(p, segs, n, glist, gcount); break;
+    case kBin4Wave: k_block<64, 16><<<n, 64, 0, st>>>(p, segs, n, glist, gcount); break;
     case 5: k_block<256, 8><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case 6: k_block<256, 16><<<n, 256, 0, st>>>(p, segs, n, glist, gcount); break;
     case kBin6Wide: k_block<512, 8><<<n, 512, 0, st>>>(p, segs, n, glist, gcount); break;
@@ -3031,6 +3032,10 @@ hipError_t launch_bin_dense(int bin, const DevParams& p, WorkItem* segs, int n, 
       break;
     case 4:
       hipExtLaunchKernelGGL(k_block_dense<128, 8>, grid, dim3(128), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
+                            par, glist, gcount, guard);
+      break;
+    case kBin4Wave:
+      hipExtLaunchKernelGGL(k_block_dense<64, 16>, grid, dim3(64), 0, st, nullptr, done, 0, p, segs, n, queue, qcnt,
                             par, glist, gcount, guard);
       break;
     case 5:
@@ -3068,6 +3073,10 @@ hipError_t launch_bin_rest(int bin, const DevParams& p, WorkItem* segs, int n, i
       break;
     case 4:
       hipExtLaunchKernelGGL(k_block_rest<128, 8>, rg, dim3(128), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
+                            host_count, glist, gcount);
+      break;
+    case kBin4Wave:
+      hipExtLaunchKernelGGL(k_block_rest<64, 16>, rg, dim3(64), 0, st, nullptr, done, 0, p, segs, queue, qcnt, par,
                             host_count, glist, gcount);
       break;
     case 5:

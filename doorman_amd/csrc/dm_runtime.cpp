@@ -343,6 +343,8 @@ struct dm_ctx {
   int dq_skip[kSplitSlots] = {};   // ticks in the one-kernel form since the split was last tried
   int dq_wait[kSplitSlots] = {64, 64, 64, 64, 64, 64, 64, 64};  // ticks before the next try
   bool bin6_wide = false;  // bin 6 on 512 x 8 workgroups (kBin6Wide): it holds most of the rows
+  bool bin4_wave = false;  // bin 4 on one wave per resource (kBin4Wave): most of its resources FairShare
+  std::vector<int32_t> h_kind;  // the loaded configuration's kinds (bin 4's shape)
   int32_t* h_dq = nullptr;   // host-mapped: items the last split tick queued, per bin
   int32_t* d_dq = nullptr;
   // host-mapped, per split bin: {undense count, epoch} of the epoch's check
@@ -754,6 +756,15 @@ static void plan_parts(dm_ctx* c) {
   }
 }
 
+// kBin4Wave (dm_device.h): most of bin 4's resources FairShare by the loaded kinds.
+static bool bin4_prefers_wave(const dm_ctx* c) {
+  const std::vector<WorkItem>& items = c->h_bins[4];
+  if (items.empty() || (int64_t)c->h_kind.size() != c->R) return false;
+  int64_t fs = 0;
+  for (const WorkItem& w : items) fs += c->h_kind[(size_t)w.seg] == DM_FAIR_SHARE ? 1 : 0;
+  return 2 * fs > (int64_t)items.size();
+}
+
 // The stream parts of the plan and every split slot's state: rest queues, two-slot
 // counters, the epoch checks (a new plan, or parts turned off).
 static int init_split_slots(dm_ctx* c, hipStream_t st) {
@@ -814,6 +825,7 @@ static int upload_plan(dm_ctx* c) {
     for (const WorkItem& w : c->h_bins[6]) rows6 += w.n & 0xFFFF;
     c->bin6_wide = 2 * rows6 > c->N;
   }
+  c->bin4_wave = bin4_prefers_wave(c);
   if (int rc = init_split_slots(c, st)) return rc;
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
@@ -1286,6 +1298,16 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   DM_HIP(c, upload(c->cfg, rc.data(), (size_t)R, st), "upload config");
   DM_HIP(c, upload(c->cold, rcold.data(), (size_t)R, st), "upload config");
   c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
+  c->h_kind.assign(cfg->kind, cfg->kind + R);
+  if (c->store_loaded && R == c->R) {  // bin 4's shape by the new kinds
+    const bool wave = bin4_prefers_wave(c);
+    if (wave != c->bin4_wave) {
+      // the dense hints and released-row masks are the shape's own: the items go up
+      // again without hints (the next writeback tick sets them in the new shape)
+      c->bin4_wave = wave;
+      DM_HIP(c, upload(c->bins[4], c->h_bins[4].data(), c->h_bins[4].size(), st), "plan bins");
+    }
+  }
   DM_HIP(c, hipStreamSynchronize(st), "config load");
   c->cfg_loaded = true;
   return DM_OK;
@@ -1554,7 +1576,9 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   for (int b = kNumBins - 1; b >= 0; --b) {
     if (c->h_bins[b].empty()) continue;
     if (b == 7 || b == 8 || b <= 2) continue;  // k_subs
-    const int lb = (b == 6 && c->bin6_wide) ? kBin6Wide : b;  // the launchers' bin (shape)
+    const int lb = (b == 6 && c->bin6_wide)   ? kBin6Wide
+                   : (b == 4 && c->bin4_wave) ? kBin4Wave
+                                              : b;  // the launchers' bin (shape)
     const int nparts = c->bin_parts[b];
     if (one_class && c->tick_signal_wanted) {
       c->tick_flagged = true;
@@ -2799,7 +2823,7 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   v[1 + kNumBins] = (int64_t)c->h_large.size();
   v[2 + kNumBins] = (int64_t)c->h_chunks.size();
   v[3 + kNumBins] = c->N;
-  v[4 + kNumBins] = c->bin6_wide ? 1 : 0;  // bin 6 on 512 x 8 workgroups (else 256 x 16)
+  v[4 + kNumBins] = (c->bin6_wide ? 1 : 0) | (c->bin4_wave ? 2 : 0);  // bit 0: bin 6 on 512 x 8 (else 256 x 16); bit 1: bin 4 on 64 x 16
   v[5 + kNumBins] = c->redo_cap;  // 3/4 of the redo's full-build workgroups the GPU holds at once
   v[6 + kNumBins] = 1;            // every store may speculate (the redo by teams has no bound)
   v[7 + kNumBins] = c->aux_own_queue ? 1 : 0;  // the work classes' streams each have a hardware queue

@@ -384,8 +384,9 @@ int dm_kernel_class_names(const char** names, int max);
 int dm_reset_kernel_times(dm_ctx* ctx);
 /* plan summary of the loaded store: small-resource tiles, items per dispatch bin (sub16x4,
  * sub32x4, wave64x4, block128x4, block128x8, block256x8, the 2049-4096-row bin,
- * sub8x2, sub16x2), large resources, large chunks, leases, then 1 when the
- * 2049-4096-row bin runs on 512 x 8 workgroups (else 256 x 16), 3/4 of the redo's
+ * sub8x2, sub16x2), large resources, large chunks, leases, then the bins' shapes (bit 0:
+ * the 2049-4096-row bin runs on 512 x 8 workgroups, else 256 x 16; bit 1: the
+ * 513-1024-row bin on one wave per resource, 64 x 16, else 128 x 8), 3/4 of the redo's
  * full-build workgroups the GPU holds at once (its grid bound), and 1 (every store may
  * speculate: the redo by teams needs only 64 co-resident workgroups), and 1 when the
  * work classes' auxiliary streams each have a hardware queue of their own, and the

@@ -50,14 +50,15 @@ def _check(eng, host, label):
         assert float_close(res[k], ref, np.maximum(scale, np.abs(ref))).all(), f"{label}: {k}"
 
 
-@pytest.mark.parametrize("lo,hi", [(257, 420), (513, 700)])
-def test_parts_back_to_back_ticks_match_the_oracle(lo, hi):
+@pytest.mark.parametrize("lo,hi,kinds", [(257, 420, (0, 1, 2, 3)), (513, 700, (0, 1, 2, 3)), (513, 1024, (3,))])
+def test_parts_back_to_back_ticks_match_the_oracle(lo, hi, kinds):
+    """(513-1024 rows, FairShare only: bin 4 on one wave per resource, kBin4Wave)"""
     import torch
     from doorman_amd.engine import Engine
     torch.cuda.set_device(0)
-    rng = np.random.default_rng(lo)
+    rng = np.random.default_rng(lo + len(kinds))
     sizes = rng.integers(lo, hi + 1, 4600)
-    snap = snapshot_with_sizes(rng, sizes, expired_frac=0.02, learning_frac=0.05)
+    snap = snapshot_with_sizes(rng, sizes, kinds=kinds, expired_frac=0.02, learning_frac=0.05)
     W.add_store_sums(snap)
     host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
     N = len(snap["wants"])
@@ -65,6 +66,7 @@ def test_parts_back_to_back_ticks_match_the_oracle(lo, hi):
         eng.load(snap)
         info = eng.plan_info()
         assert info["stream_parts"] == 2, info
+        assert bool(info["bin_shapes"] & 2) == (kinds == (3,)), info  # bin 4's shape
         now = NOW
         for seg in range(3):
             if seg == 2:  # a wants refresh of every seventh row: a new row epoch
@@ -135,3 +137,34 @@ def test_parts_publish_their_own_flags_words():
                     assert words[expect[k] - 1] != 0 and words[2 - expect[k]] == 0, f"tick {k}: words {words.tolist()}"
                 nxt = ring[(k + 1) % 3].cpu().numpy()[0:1].view(np.uint32)[0]
                 assert nxt[0] == 0 and nxt[1] == 0, f"tick {k}: next buffer's flags words {nxt.tolist()}"
+
+
+def test_bin4_shape_follows_the_loaded_kinds():
+    """Bin 4 (513-1024 rows) takes one wave per resource when most of its resources are
+    FairShare (kBin4Wave).  A configuration reload that flips the majority after
+    writeback ticks have set dense hints and released-row masks in one shape switches
+    the shape (the items go up again without hints); ticks on either side of each switch
+    match the oracle."""
+    import torch
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(91)
+    sizes = rng.integers(513, 1025, 900)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(3,), expired_frac=0.03, learning_frac=0.0)
+    W.add_store_sums(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    R = len(sizes)
+    with Engine(0) as eng:
+        eng.load(snap)
+        now = NOW
+        for step, kind in enumerate([W.FAIR_SHARE, W.PROPORTIONAL_SHARE, W.FAIR_SHARE]):
+            if step > 0:  # the other kind for every resource: the majority flips
+                host["kind"] = np.full(R, kind, np.int32)
+                eng.load_config(host)
+            assert bool(eng.plan_info()["bin_shapes"] & 2) == (kind == W.FAIR_SHARE)
+            for _ in range(4):
+                now += int(rng.integers(0, 20)) * W.NS
+                eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
+                _host_tick(host, now)
+            eng.sync()
+            _check(eng, host, f"kind {kind}")

@@ -17,18 +17,18 @@ import sys
 
 CLASS = [
     # template args <G, R[, BATCH]>: BATCH 2 is the HBM-streaming variant of the same bin
-    (r"k_block_dense<128, 4>", "block128x4_dense"), (r"k_block_dense<128, 8>", "block128x8_dense"),
+    (r"k_block_dense<128, 4>", "block128x4_dense"), (r"k_block_dense<128, 8>", "block128x8_dense"), (r"k_block_dense<64, 16>", "block128x8_dense"),
     (r"k_block_dense<256, 8>", "block256x8_dense"), (r"k_block_dense<512, 8>", "block2k4k_dense"),
     (r"k_block_dense<256, 16>", "block2k4k_dense"),
     (r"k_publish\b", "hier_publish"), (r"k_hier_tick\b", "hier_root"),
     (r"k_tick_done\b", "tick_done"), (r"k_count_undense\b", "count_undense"),
     (r"k_large_spec\b", "large_spec"), (r"k_large_redo(_team)?\b", "large_redo"),
-    (r"k_block_rest<128, 4>", "block128x4_rest"), (r"k_block_rest<128, 8>", "block128x8_rest"),
+    (r"k_block_rest<128, 4>", "block128x4_rest"), (r"k_block_rest<128, 8>", "block128x8_rest"), (r"k_block_rest<64, 16>", "block128x8_rest"),
     (r"k_block_rest<256, 8>", "block256x8_rest"), (r"k_block_rest<512, 8>", "block2k4k_rest"),
     (r"k_block_rest<256, 16>", "block2k4k_rest"),
     (r"k_large_t\b", "large_t"), (r"k_large_c_het\b", "large_c_het"), (r"k_large_e\b", "large_e"),
     (r"k_large_map_het\b", "large_map_het"),
-    (r"k_block<128, 4(, \d)?>", "block128x4"), (r"k_block<128, 8(, \d)?>", "block128x8"), (r"k_block<256, 2(, \d)?>", "block256x2"), (r"k_block<256, 4(, \d)?>", "block256x4"),
+    (r"k_block<128, 4(, \d)?>", "block128x4"), (r"k_block<128, 8(, \d)?>", "block128x8"), (r"k_block<64, 16>", "block128x8"), (r"k_block<256, 2(, \d)?>", "block256x2"), (r"k_block<256, 4(, \d)?>", "block256x4"),
     (r"k_block<256, 8(, \d)?>", "block256x8"), (r"k_block<512, 8(, \d)?>", "block2k4k"), (r"k_block<256, 16(, \d)?>", "block2k4k"), (r"k_block<512, 4(, \d)?>", "block512x4"), (r"k_block<1024, 4(, \d)?>", "block1024x4"),
     (r"k_wave<4(, \d)?>", "wave64x4"), (r"k_sub<16, 4>", "sub16x4"), (r"k_sub<32, 4>", "sub32x4"),
     (r"k_sub<8, 2>", "sub8x2"), (r"k_sub<16, 2>", "sub16x2"),
