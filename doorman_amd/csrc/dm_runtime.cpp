@@ -756,13 +756,26 @@ static void plan_parts(dm_ctx* c) {
   }
 }
 
-// kBin4Wave (dm_device.h): most of bin 4's resources FairShare by the loaded kinds.
+// kBin4Wave (dm_device.h): bin 4 in stream parts and most of its resources FairShare
+// by the loaded kinds.  (Without parts the shape did not pay: configs[3]'s N = 8 shard
+// and the whole configs[3] unchanged, its N = 4 shard +3 %, profiles/r05_ab/b4_one_wave.txt.)
 static bool bin4_prefers_wave(const dm_ctx* c) {
   const std::vector<WorkItem>& items = c->h_bins[4];
-  if (items.empty() || (int64_t)c->h_kind.size() != c->R) return false;
+  if (items.empty() || c->bin_parts[4] < 2 || (int64_t)c->h_kind.size() != c->R) return false;
   int64_t fs = 0;
   for (const WorkItem& w : items) fs += c->h_kind[(size_t)w.seg] == DM_FAIR_SHARE ? 1 : 0;
   return 2 * fs > (int64_t)items.size();
+}
+
+// Bin 4's shape after a new plan, new kinds or parts turned off: a change re-uploads the
+// bin's items without their hints (the dense hints and released-row masks are the
+// shape's own; the next writeback tick sets them in the new shape).
+static int update_bin4_shape(dm_ctx* c, hipStream_t st) {
+  const bool wave = bin4_prefers_wave(c);
+  if (wave == c->bin4_wave) return DM_OK;
+  c->bin4_wave = wave;
+  DM_HIP(c, upload(c->bins[4], c->h_bins[4].data(), c->h_bins[4].size(), st), "plan bins");
+  return DM_OK;
 }
 
 // The stream parts of the plan and every split slot's state: rest queues, two-slot
@@ -795,7 +808,8 @@ static int set_parts_ok(dm_ctx* c, bool ok) {
   DM_HIP(c, c->join_aux(), "join");
   if (int rc = c->synced("stream parts")) return rc;
   c->main_dirty = true;
-  return init_split_slots(c, c->stream);
+  if (int rc = init_split_slots(c, c->stream)) return rc;
+  return update_bin4_shape(c, c->stream);
 }
 
 static int upload_plan(dm_ctx* c) {
@@ -825,8 +839,8 @@ static int upload_plan(dm_ctx* c) {
     for (const WorkItem& w : c->h_bins[6]) rows6 += w.n & 0xFFFF;
     c->bin6_wide = 2 * rows6 > c->N;
   }
-  c->bin4_wave = bin4_prefers_wave(c);
   if (int rc = init_split_slots(c, st)) return rc;
+  if (int rc = update_bin4_shape(c, st)) return rc;
   const size_t nc = std::max<size_t>(c->h_chunks.size(), 1);
   DM_HIP(c, c->pa_cnt.ensure(nc), "partials");
   DM_HIP(c, c->pa_cnt_all.ensure(nc), "partials");
@@ -1300,13 +1314,7 @@ int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   c->h_refresh_s.assign(cfg->refresh_interval_s, cfg->refresh_interval_s + R);
   c->h_kind.assign(cfg->kind, cfg->kind + R);
   if (c->store_loaded && R == c->R) {  // bin 4's shape by the new kinds
-    const bool wave = bin4_prefers_wave(c);
-    if (wave != c->bin4_wave) {
-      // the dense hints and released-row masks are the shape's own: the items go up
-      // again without hints (the next writeback tick sets them in the new shape)
-      c->bin4_wave = wave;
-      DM_HIP(c, upload(c->bins[4], c->h_bins[4].data(), c->h_bins[4].size(), st), "plan bins");
-    }
+    if (int rc2 = update_bin4_shape(c, st)) return rc2;
   }
   DM_HIP(c, hipStreamSynchronize(st), "config load");
   c->cfg_loaded = true;

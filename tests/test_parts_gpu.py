@@ -140,16 +140,16 @@ def test_parts_publish_their_own_flags_words():
 
 
 def test_bin4_shape_follows_the_loaded_kinds():
-    """Bin 4 (513-1024 rows) takes one wave per resource when most of its resources are
-    FairShare (kBin4Wave).  A configuration reload that flips the majority after
-    writeback ticks have set dense hints and released-row masks in one shape switches
-    the shape (the items go up again without hints); ticks on either side of each switch
-    match the oracle."""
+    """Bin 4 (513-1024 rows) in stream parts takes one wave per resource when most of its
+    resources are FairShare (kBin4Wave).  A configuration reload that flips the majority
+    after writeback ticks have set dense hints and released-row masks in one shape
+    switches the shape (the items go up again without hints); ticks on either side of
+    each switch match the oracle.  Without parts the bin keeps 128 x 8."""
     import torch
     from doorman_amd.engine import Engine
     torch.cuda.set_device(0)
     rng = np.random.default_rng(91)
-    sizes = rng.integers(513, 1025, 900)
+    sizes = rng.integers(513, 700, 4300)  # >= 4096 items: stream parts
     snap = snapshot_with_sizes(rng, sizes, kinds=(3,), expired_frac=0.03, learning_frac=0.0)
     W.add_store_sums(snap)
     host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
@@ -161,10 +161,25 @@ def test_bin4_shape_follows_the_loaded_kinds():
             if step > 0:  # the other kind for every resource: the majority flips
                 host["kind"] = np.full(R, kind, np.int32)
                 eng.load_config(host)
-            assert bool(eng.plan_info()["bin_shapes"] & 2) == (kind == W.FAIR_SHARE)
+            info = eng.plan_info()
+            assert info["stream_parts"] == 2 and bool(info["bin_shapes"] & 2) == (kind == W.FAIR_SHARE), info
             for _ in range(4):
                 now += int(rng.integers(0, 20)) * W.NS
                 eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
                 _host_tick(host, now)
             eng.sync()
             _check(eng, host, f"kind {kind}")
+
+
+def test_bin4_without_parts_keeps_its_shape():
+    """A FairShare bin 4 that does not run in stream parts (fewer than 4096 items) keeps
+    128 x 8 workgroups."""
+    import torch
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(92)
+    snap = snapshot_with_sizes(rng, rng.integers(513, 1025, 900), kinds=(3,))
+    with Engine(0) as eng:
+        eng.load(snap)
+        info = eng.plan_info()
+        assert info["stream_parts"] == 1 and not info["bin_shapes"] & 2, info
