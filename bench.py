@@ -62,6 +62,17 @@ def c3_bounds(world: int):
     return partition(np.full(C3_R, C3_CLIENTS), world)
 
 
+def c2_bounds(world: int, snap=None):
+    """configs[2] over N GPUs: contiguous resource-id ranges of the one Zipf snapshot,
+    balanced by predicted tick cost (hierarchy.tick_cost: bytes per lease and per
+    resource), not by lease count -- a lease-count split leaves the 500k singletons'
+    97-B records on the last shard (2.2x the mean bytes at N = 8)."""
+    from doorman_amd import workloads as W
+    from doorman_amd.hierarchy import partition
+    sizes = np.diff(snap["seg_off"]) if snap is not None else W.zipf_sizes()
+    return partition(sizes, world)
+
+
 def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicated"):
     from doorman_amd import workloads as W
     if name == "c1":
@@ -69,6 +80,10 @@ def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicate
     if name == "c1ps":
         return W.c1(seed=1 + 1000 * rank, kind=W.PROPORTIONAL_SHARE)
     if name == "c2":
+        if layout == "sharded":  # this rank's range of the one 1M-resource Zipf snapshot
+            snap = W.c2(seed=2)
+            b = c2_bounds(world, snap)
+            return W.subset_range(snap, int(b[rank]), int(b[rank + 1]))
         return W.c2(seed=2 + 1000 * rank)
     if name == "c3":
         if layout == "sharded":  # this rank's range of the one 100M-lease snapshot
@@ -109,6 +124,28 @@ def algorithmic_bytes(n_leases: int, n_resources: int, dense_leases: float = 0) 
     not counted."""
     return int(round(LEASE_BYTES * n_leases - (LEASE_BYTES - DENSE_LEASE_BYTES) * dense_leases
                      + RESOURCE_BYTES * n_resources))
+
+
+L3_BYTES = 256 << 20    # MI355X Infinity Cache (MALL), MI355X_MICROARCH.md chip-level parameters
+STREAM_BYTES = 1 << 30  # dm_device.h kStreamBytes: a store with 48 * N above it writes gets to an alternate column
+
+
+def tick_footprint_bytes(snap, dense_leases: float = 0.0) -> dict:
+    """Distinct bytes one writeback tick touches (each line once, reads and writes of the
+    same line together): wants, has, the subclients column except for dense rows, the
+    alternate gets column when the tick writes one (dm_runtime.cpp: a store with 48 * N >
+    kStreamBytes, or one with a > 4096-row resource, whose speculative chain writes gets
+    before they are verified), and per resource the 32-B config, 32-B sums and state byte.
+    At or below the 256 MiB Infinity Cache the tick's lines stay cache-resident from tick
+    to tick, so the rocprof FETCH_SIZE / WRITE_SIZE counts (which include Infinity-Cache
+    hits, MI355X_MICROARCH.md HBM/rocprofv3 section) and any GB/s over these bytes
+    measure cache bandwidth, not HBM."""
+    sizes = np.diff(snap["seg_off"])
+    N, R = int(sizes.sum()), len(sizes)
+    alternate = 48 * N > STREAM_BYTES or bool((sizes > 4096).any())
+    b = 16 * N + 4 * (N - dense_leases) + (8 * N if alternate else 0) + 65 * R
+    return {"tick_footprint_bytes": int(round(b)), "alternate_gets_column": alternate,
+            "l3_resident": bool(b <= L3_BYTES)}
 
 
 def dense_fraction(eng, snap) -> float:
@@ -427,6 +464,8 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
     dense_k = kernel_lease_bytes(name, leases_k, run.get("dense_frac", 0.0))
     alg = algorithmic_bytes(leases_k, res_k, dense_k)
     achieved = alg / avg_s / 1e9
+    fp = tick_footprint_bytes(snap, tick_dense_leases(snap, run.get("dense_frac", 0.0)))
+    l3 = fp["l3_resident"]
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if os.path.exists(pmc_path):
@@ -437,8 +476,17 @@ def roofline_of(workload, snap, run, steps, single_kernel_tick):
         if traffic is not None and in_parts:  # the PMC passes count per launch: per tick, both parts
             traffic = traffic * parts
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "frac_of_copy_ceiling": round(achieved / HBM_COPY_CEIL_GBS, 4), "traffic": traffic,
+            "unit": "GB/s",
+            # a cache-resident tick (footprint <= 256 MiB) is not HBM evidence: no HBM fraction
+            "frac": None if l3 else round(achieved / HBM_PEAK_GBS, 4),
+            "frac_of_copy_ceiling": None if l3 else round(achieved / HBM_COPY_CEIL_GBS, 4),
+            **fp,
+            "frac_l3": round(achieved / HBM_PEAK_GBS, 4) if l3 else None,
+            "l3_note": ("the tick's distinct bytes fit the 256 MiB Infinity Cache: they stay cache-resident from "
+                        "tick to tick, so achieved and the PMC traffic (FETCH_SIZE counts Infinity-Cache hits) "
+                        "measure cache bandwidth; frac_l3 is achieved over the HBM spec for comparison only"
+                        if l3 else None),
+            "traffic": traffic,
             "traffic_source": f"profiles/pmc_{workload}.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, calibrated)",
             "algorithmic_bytes_per_launch": alg,
             "leases_per_launch": leases_k, "resources_per_launch": res_k,
@@ -659,19 +707,33 @@ def tick_dense_fraction(eng, snap, step) -> float:
     return dense_fraction(eng, snap)
 
 
+def tick_dense_leases(snap, dense_frac) -> float:
+    """Rows of dense resources in a tick: dense_frac of the workgroup bins' rows."""
+    sizes = np.diff(snap["seg_off"])
+    return dense_frac * int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
+
+
+def tick_fracs(snap, dense_frac, t_step) -> dict:
+    """The tick's algorithmic bytes over its step time against the HBM spec -- null for a
+    cache-resident tick (tick_footprint_bytes), whose rate goes to tick_frac_l3."""
+    R, N = len(snap["seg_off"]) - 1, int(snap["seg_off"][-1])
+    dense = tick_dense_leases(snap, dense_frac)
+    tick_bytes = algorithmic_bytes(N, R, dense)
+    f = round(tick_bytes / t_step / 1e9 / HBM_PEAK_GBS, 4)
+    fp = tick_footprint_bytes(snap, dense)
+    return {"tick_hbm_frac": None if fp["l3_resident"] else f, "tick_frac_l3": f if fp["l3_resident"] else None,
+            "tick_algorithmic_bytes": tick_bytes, **fp}
+
+
 def workload_line(name, snap, run, steps, single_kernel_tick):
     """One workload's numbers for the bench line's `extra` (or the line itself): rate,
     step time, the tick's fraction of HBM spec over its algorithmic bytes, per-class
     event times, the dominant kernel's roofline."""
-    R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
-    sizes = np.diff(snap["seg_off"])
-    group_leases = int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
+    N = len(snap["wants"])
     t_step = run["elapsed"] / steps
-    tick_bytes = algorithmic_bytes(N, R, run["dense_frac"] * group_leases)
     return {"workload": WORKLOADS[name], "value": N / t_step, "unit": "leases/s", "steps": steps,
             "ms_per_step": t_step * 1e3,
-            "tick_hbm_frac": round(tick_bytes / t_step / 1e9 / HBM_PEAK_GBS, 4),
-            "tick_algorithmic_bytes": tick_bytes,
+            **tick_fracs(snap, run["dense_frac"], t_step),
             "host_enqueue_us_per_step": round(run["host_enqueue_s"] / steps * 1e6, 2),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
                         for k, v in run["ktimes"].items()},
@@ -695,6 +757,71 @@ def dist_fields(dist_info, run):
         d.update({"consistent": run["self_check"]["consistent"], "check_sample": run["self_check"]["sample"],
                   "exchange_check": run["self_check"]})
     return d
+
+
+def c2_shard_step(torch, Engine, dev_index, args, world, rank, sync_ranks, steps):
+    """One rank's range of configs[2] (c2_bounds): back-to-back writeback ticks timed as
+    every bench step (timed_steps); returns the rank's numbers."""
+    from doorman_amd import workloads as W
+    from doorman_amd.hierarchy import tick_cost
+    snap = make_workload("c2", rank, world, "sharded")
+    eng = Engine(dev_index, args.lib)
+    try:
+        eng.load(snap)
+        now = W.NOW_NS
+        step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
+        run = timed_steps(torch, eng, step, steps, args.warmup, sync_ranks)
+        sizes = np.diff(snap["seg_off"])
+        return {"rank": rank, "resources": len(sizes), "leases": int(sizes.sum()),
+                "predicted_bytes": int(tick_cost(sizes).sum()),
+                "step_us": round(run["elapsed"] / steps * 1e6, 2),
+                "kernels": {k: round(v[1] / max(v[0], 1) * 1e3, 2) for k, v in run["ktimes"].items()},
+                "elapsed_s": run["elapsed"]}
+    finally:
+        eng.close()
+
+
+def shard_summary(world, per_rank, steps):
+    """Whole-node numbers of a sharded configs[2] run from every rank's own numbers."""
+    t = [r["step_us"] for r in per_rank]
+    pb = [r["predicted_bytes"] for r in per_rank]
+    n = sum(r["leases"] for r in per_rank)
+    return {"node_gpus": world, "leases_total": n,
+            "bounds": [int(x) for x in c2_bounds(world)],
+            "step_us_max": max(t), "step_us_min": min(t), "step_max_over_min": round(max(t) / min(t), 4),
+            "predicted_bytes_max_over_mean": round(max(pb) / (sum(pb) / len(pb)), 4),
+            "partition": "contiguous resource-id ranges balanced by hierarchy.tick_cost (28 B per lease + 97 B per "
+                         "resource), not lease count",
+            "ranks": per_rank}
+
+
+def rehearse_c2_shards(torch, Engine, dev_index, args, world, ranks):
+    """--workload c2 --rehearse-shard N: the listed ranks' shards of an N-GPU configs[2]
+    node, one after another on this GPU (each alone on the GPU, as on its own GPU of the
+    node; no collective: the shards are independent)."""
+    per = [c2_shard_step(torch, Engine, dev_index, args, world, k, lambda w, v: v, args.steps) for k in ranks]
+    out = {"metric": "rehearsal: every rank's step of an N-GPU configs[2] node, one after another on one GPU "
+                     "(not a bench line)", "steps": args.steps, "warmup": args.warmup,
+           "workload": WORKLOADS["c2"] + f"; one snapshot sharded by resource id over {world} GPUs"}
+    out.update(shard_summary(world, per, args.steps) if len(per) == world else {"ranks": per})
+    if len(per) == world:
+        out["projected_node_leases_per_s"] = out["leases_total"] / (out["step_us_max"] * 1e-6)
+    return out
+
+
+def c2_sharded_line(torch, Engine, dev_index, args, world, rank, sync_ranks, dist, red_dev):
+    """N > 1: configs[2] over the node, every rank its range (strong scaling, no
+    collective on the data path); value = all ranks' leases / the max over ranks of the
+    timed region (barrier + synchronize on both sides, as the main line)."""
+    mine = c2_shard_step(torch, Engine, dev_index, args, world, rank, sync_ranks, args.steps)
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    t = max(r["elapsed_s"] for r in allr)
+    out = {"workload": WORKLOADS["c2"] + f"; one snapshot sharded by resource id over {world} GPUs",
+           "value": sum(r["leases"] for r in allr) * args.steps / t, "unit": "leases/s",
+           "ms_per_step": t / args.steps * 1e3, "scaling": "strong"}
+    out.update(shard_summary(world, allr, args.steps))
+    return out
 
 
 def spawn_ranks(args) -> int:
@@ -749,12 +876,17 @@ def main():
                          "dist.consistent false)")
     args = ap.parse_args()
     if args.rehearse_shard:
-        if args.workload != "c3" or args.gpus != 1 or args.rehearse_shard < 2:
-            raise SystemExit("--rehearse-shard N (N >= 2) rehearses one rank of configs[3] on one GPU: --workload c3, "
-                             "--gpus 1")
-        if not 0 <= args.rehearse_rank < args.rehearse_shard:
-            raise SystemExit("--rehearse-rank must be in [0, N)")
-        args.layout, args.hier = "sharded", "on"
+        if args.workload not in ("c2", "c3") or args.gpus != 1 or args.rehearse_shard < 2:
+            raise SystemExit("--rehearse-shard N (N >= 2) rehearses ranks of an N-GPU configs[3] (c3) or configs[2] "
+                             "(c2) node on one GPU: --workload c3|c2, --gpus 1")
+        if args.workload == "c2":
+            if not -1 <= args.rehearse_rank < args.rehearse_shard:
+                raise SystemExit("--rehearse-rank must be in [0, N), or -1 for every rank in turn")
+            args.layout, args.hier = "sharded", "off"
+        else:
+            if not 0 <= args.rehearse_rank < args.rehearse_shard:
+                raise SystemExit("--rehearse-rank must be in [0, N)")
+            args.layout, args.hier = "sharded", "on"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
@@ -765,9 +897,11 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     hier = args.hier == "on" or (args.hier == "auto" and args.workload == "c3")
-    layout = args.layout if args.layout != "auto" else ("sharded" if args.workload == "c3" else "replicated")
-    if layout == "sharded" and args.workload != "c3":
-        raise SystemExit("--layout sharded is configs[3]'s layout (--workload c3)")
+    layout = args.layout if args.layout != "auto" else ("sharded" if args.workload in ("c2", "c3") else "replicated")
+    if layout == "sharded" and args.workload not in ("c2", "c3"):
+        raise SystemExit("--layout sharded splits one snapshot by resource id: configs[3] (c3) or configs[2] (c2)")
+    if layout == "sharded" and args.workload == "c2" and hier:
+        raise SystemExit("configs[2] has no hierarchy: --hier off")
 
     import torch  # loaded first: libdoorman_hip then binds to torch's HIP runtime
     import torch.distributed as dist
@@ -931,6 +1065,11 @@ def main():
         run["t_max"], run["n_total"] = float(t.item()), float(n.item())
         return run, snap, eng, root
 
+    if args.rehearse_shard and args.workload == "c2":
+        ranks = range(s_world) if args.rehearse_rank < 0 else [s_rank]
+        print(json.dumps(rehearse_c2_shards(torch, Engine, dev_index, args, s_world, ranks)), flush=True)
+        return
+
     run, snap, eng, root = measure(layout)
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])
     t_max, n_total = run["t_max"], run["n_total"]
@@ -986,10 +1125,12 @@ def main():
         if rootw is not None:
             rootw.close()
 
+    if world > 1 and args.workload == "c3" and not args.no_extra:
+        # configs[2]'s Zipf population over the node: every rank its cost-balanced range of
+        # the one 1M-resource snapshot, no data-path collective (strong scaling)
+        extra["c2_sharded"] = c2_sharded_line(torch, Engine, dev_index, args, world, rank, sync_ranks, dist, red_dev)
+
     if rank == 0:
-        sizes = np.diff(snap["seg_off"])
-        group_leases = int(sizes[(sizes >= 257) & (sizes <= 4096)].sum())
-        tick_bytes = algorithmic_bytes(N, R, run["dense_frac"] * group_leases)
         line = {
             "metric": METRIC,
             "value": n_total * args.steps / t_max,
@@ -1022,7 +1163,7 @@ def main():
             "exchange": exchange_used["mode"] if hier else None,
             # (a rehearsal reports its exchange self-check too: one rank of the rehearsed node)
             "dist": dist_fields(dist_info, run) if world > 1 or args.rehearse_shard else None,
-            "tick_hbm_frac": round(tick_bytes / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            **tick_fracs(snap, run["dense_frac"], t_max / args.steps),
             "host_enqueue_us_per_step": round(run["host_enqueue_s"] / args.steps * 1e6, 2),
             "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)}
                         for k, v in run["ktimes"].items()},

@@ -37,14 +37,36 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
-def partition(seg_sizes, world: int) -> np.ndarray:
-    """Contiguous resource ranges balanced by lease count: boundaries b[0..world]
-    with shard k = resources [b[k], b[k+1])."""
+# What one writeback tick moves per lease and per resource (bench.LEASE_BYTES /
+# RESOURCE_BYTES): read wants, has, int32 subclients, write gets; the
+# resource's config record, running sums in and out and its state byte.
+LEASE_COST_B = 28.0
+RESOURCE_COST_B = 97.0
+
+
+def tick_cost(seg_sizes) -> np.ndarray:
+    """Predicted cost of each resource in one tick, in bytes moved.  A tick is HBM-bound
+    and its kernel classes share the HBM (profiles/r05_c2_classes.md: the C2 tick is the
+    classes' shared HBM time), so bytes predict time.  Per resource, not per lease: a
+    Zipf population's singletons cost 97 B of record against 28 B of row each, and a
+    lease-count split leaves them all on the last shard (2.2x the mean bytes at N = 8 on
+    configs[2])."""
+    sizes = np.asarray(seg_sizes, dtype=np.float64)
+    return LEASE_COST_B * sizes + RESOURCE_COST_B
+
+
+def partition(seg_sizes, world: int, cost=None) -> np.ndarray:
+    """Contiguous resource ranges balanced by predicted tick cost (tick_cost, or the
+    given per-resource cost): boundaries b[0..world] with shard k = resources
+    [b[k], b[k+1]).  With one size for every resource (configs[3]) this is the even
+    lease-count split."""
     sizes = np.asarray(seg_sizes, dtype=np.int64)
     R = len(sizes)
     if world <= 1 or R == 0:
         return np.array([0, R], dtype=np.int64)
-    csum = np.concatenate([[0], np.cumsum(sizes)])
+    c = tick_cost(sizes) if cost is None else np.asarray(cost, dtype=np.float64)
+    assert len(c) == R
+    csum = np.concatenate([[0.0], np.cumsum(c)])
     total = csum[-1]
     bounds = [0]
     for k in range(1, world):
@@ -61,9 +83,10 @@ def partition(seg_sizes, world: int) -> np.ndarray:
     return np.asarray(bounds, dtype=np.int64)
 
 
-def shard(snap: dict, world: int, rank: int) -> dict:
-    b = partition(np.diff(snap["seg_off"]), world)
-    return W.subset(snap, np.arange(b[rank], b[rank + 1]))
+def shard(snap: dict, world: int, rank: int, cost=None) -> dict:
+    """This rank's contiguous range of the snapshot's resources (partition)."""
+    b = partition(np.diff(snap["seg_off"]), world, cost)
+    return W.subset_range(snap, int(b[rank]), int(b[rank + 1]))
 
 
 def root_snapshot(n_resources: int, n_servers: int, kind, capacity, lease_length_s=20, refresh_interval_s=5) -> dict:

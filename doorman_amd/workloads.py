@@ -106,6 +106,20 @@ def subset(snap: dict, resources) -> dict:
     return out
 
 
+def subset_range(snap: dict, r0: int, r1: int) -> dict:
+    """Snapshot restricted to the contiguous resources [r0, r1) (a shard): slices, no
+    per-resource gather."""
+    so = snap["seg_off"]
+    a, z = int(so[r0]), int(so[r1])
+    out = {"seg_off": np.ascontiguousarray(so[r0:r1 + 1] - so[r0])}
+    for k in ("wants", "has", "subclients", "expiry_ns"):
+        out[k] = np.ascontiguousarray(snap[k][a:z])
+    for k in CFG_FIELDS + ("agg_count", "agg_sum_has", "agg_sum_wants"):
+        if k in snap:
+            out[k] = np.ascontiguousarray(snap[k][r0:r1])
+    return out
+
+
 # ---------------------------------------------------------------------------
 # SURVEY.md §8(d) synthetic workloads
 # ---------------------------------------------------------------------------

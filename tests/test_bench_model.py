@@ -133,3 +133,28 @@ def test_self_check_root_round_matches_the_reference_model():
             checked += 1
     assert checked == 8 * R
     assert bench.root_round_one(now, [c[0] for c in cols], (0.0, 0.0, 0, W.RELEASED), (0, 0.0, 0.0), 1, 5.0, 1) is None
+
+
+def test_l3_resident_flag_c1_not_c3():
+    """A tick whose distinct bytes fit the 256 MiB Infinity Cache (C1: 10M leases written
+    in place, 160-200 MB) is flagged l3_resident and reports no HBM fraction; C3 (100M
+    leases, 2.4 GB per tick) and C2 (14M leases with an alternate gets column) are HBM
+    lines."""
+    c1 = {"seg_off": np.arange(0, 10_000_001, 1000, dtype=np.int64)}
+    c3 = {"seg_off": np.arange(0, 100_000_001, 1000, dtype=np.int64)}
+    c2 = {"seg_off": np.concatenate([[0], np.cumsum(W.zipf_sizes())])}
+    f1 = bench.tick_footprint_bytes(c1, 10_000_000)
+    assert f1["l3_resident"] and not f1["alternate_gets_column"] and f1["tick_footprint_bytes"] < 256 << 20
+    assert bench.tick_footprint_bytes(c1, 0)["l3_resident"]  # 200 MB even with the subclients column
+    assert not bench.tick_footprint_bytes(c3, 100_000_000)["l3_resident"]
+    f2 = bench.tick_footprint_bytes(c2, 0)
+    assert f2["alternate_gets_column"] and not f2["l3_resident"]
+    # the fractions: C1's goes to tick_frac_l3, C3's stays an HBM fraction
+    t1 = bench.tick_fracs(c1, 1.0, 40e-6)
+    assert t1["tick_hbm_frac"] is None and t1["tick_frac_l3"] > 0
+    t3 = bench.tick_fracs(c3, 1.0, 440e-6)
+    assert t3["tick_frac_l3"] is None and abs(t3["tick_hbm_frac"] - 2_409_700_000 / 440e-6 / 8e12) < 1e-4
+    snap = bench.make_workload("c1", 0)
+    run = {"ktimes": {"block128x8_dense": (20, 0.6)}, "stream_ms": 0.4, "dense_frac": 1.0, "parts": 2}
+    r = bench.roofline_of("c1", snap, run, 10, True)
+    assert r["l3_resident"] and r["frac"] is None and r["frac_l3"] > 0 and r["frac_of_copy_ceiling"] is None

@@ -18,9 +18,38 @@ def test_partition_balanced_contiguous(world):
     sizes = W.zipf_sizes(50_000, 50_000)
     b = H.partition(sizes, world)
     assert b[0] == 0 and b[-1] == len(sizes) and np.all(np.diff(b) >= 0)
-    loads = np.add.reduceat(sizes, b[:-1]) if world > 1 else [sizes.sum()]
+    cost = H.tick_cost(sizes)
+    loads = np.add.reduceat(cost, b[:-1]) if world > 1 else [cost.sum()]
     # a shard can exceed the mean only by the single resource straddling its boundary
-    assert max(loads) <= sizes.sum() / world + sizes.max()
+    assert max(loads) <= cost.sum() / world + cost.max()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_partition_balances_predicted_bytes_on_configs2(world):
+    """configs[2] (1M resources, Zipf 1..1M clients): the cost-model split keeps every
+    shard's predicted tick bytes (28 B per lease + 97 B per resource) within 10 % of the
+    mean.  A lease-count split left the last shard all 500k singletons' records: 2.20x
+    the mean at N = 8 (What's weak 1)."""
+    sizes = W.zipf_sizes(1_000_000, 1_000_000)
+    b = H.partition(sizes, world)
+    by = np.add.reduceat(28.0 * sizes + 97.0, b[:-1])
+    assert by.max() / by.mean() <= 1.10, (b, by)
+    leases_only = H.partition(sizes, world, cost=sizes)  # the old lease-count split, for contrast
+    by_old = np.add.reduceat(28.0 * sizes + 97.0, leases_only[:-1])
+    if world == 8:
+        assert by_old.max() / by_old.mean() > 2.0
+    import bench
+    np.testing.assert_array_equal(bench.c2_bounds(world), b)
+
+
+def test_subset_range_is_subset():
+    rng = np.random.default_rng(5)
+    snap = W.random_snapshot(rng, 30, 12)
+    for r0, r1 in ((0, 30), (3, 17), (29, 30), (5, 5)):
+        a, c = W.subset_range(snap, r0, r1), W.subset(snap, np.arange(r0, r1))
+        assert a.keys() == c.keys()
+        for k in a:
+            np.testing.assert_array_equal(a[k], c[k], err_msg=k)
 
 
 def test_partition_uniform_is_even():
