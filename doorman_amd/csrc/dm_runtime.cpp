@@ -168,7 +168,11 @@ struct dm_ctx {
   // (round 4 moved every bin to each other stream in A/Bs: this split won every one)
   // (round 5, with the small tiles: bin 3 on stream 3 112.8-117.3 us, on stream 1
   // 112.8-114.2, bin 6 on stream 3 127-129, against 111.0-112.4 us; profiles/r05_c2_classes.md)
-  static constexpr int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (small class alone)
+  static constexpr int kClassStream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};  // C2: 200 -> 189 us (small class alone)
+  // this store's assignment (plan_streams): kClassStream, except that on a store that
+  // leaves some auxiliary stream without work, classes that would share a stream move
+  // onto the idle ones (a shard of a Zipf population holds only some classes)
+  int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};
   hipStream_t aux[kAux] = {};
   bool aux_own_queue = false;  // each auxiliary stream has a hardware queue of its own (CU mask)
   uint64_t aux_seq = 0;        // the stream set's creation order in the process (take_aux)
@@ -734,6 +738,57 @@ static hipError_t check_dense(dm_ctx* c, int i, int b, int j, hipStream_t s) {
                               (unsigned long long)c->row_epoch, s);
 }
 
+// The auxiliary stream of each launch unit of a tick (the sub-wave launch of bins 7, 8,
+// 0, 1, 2; the workgroup bins 3-6, each a launch; the small tiles; the large chain).
+// dm_ctx::kClassStream is the measured assignment for a store holding every class
+// (configs[2]: bins 3-6 share stream 1 with bin 3 beside the sub-wave launch on stream 2,
+// all hidden behind the large chain's critical path).  A store holding only some classes
+// (a resource-id shard of a Zipf population: the head shards hold the large and
+// workgroup classes, the tail shards the small ones) would then run classes one after
+// another on a shared stream while another stream idles: the N = 8 shard of bins 3-6
+// ran 36.6 us against 24-26 for its neighbours (profiles/r06_c2_shard8_ranks_base.json).
+// So, while some stream holds no unit of this store, the largest unit (by rows and
+// records) of a stream holding several moves to it.
+static void plan_streams(dm_ctx* c) {
+  for (int i = 0; i < kNumBins + 2; ++i) c->class_stream[i] = dm_ctx::kClassStream[i];
+  for (int b = 0; b < kNumBins; ++b)
+    if (c->bin_parts[b] > 1) return;  // one bin in stream parts: its own two streams
+  constexpr int kUnits = 7;  // 0 sub-wave launch, 1-4 bins 3-6, 5 tiles, 6 large chain
+  auto unit_of_bin = [](int b) { return (b >= 3 && b <= 6) ? b - 2 : 0; };
+  double bytes[kUnits] = {};
+  bool present[kUnits] = {};
+  const std::vector<int64_t>& off = c->h_seg_off;
+  for (int b = 0; b < kNumBins; ++b)
+    for (const WorkItem& w : c->h_bins[b]) {
+      present[unit_of_bin(b)] = true;
+      bytes[unit_of_bin(b)] += 28.0 * (double)(off[(size_t)w.seg + 1] - off[(size_t)w.seg]) + 97.0;
+    }
+  for (const Tile& t : c->h_tiles) {
+    present[5] = true;
+    bytes[5] += 28.0 * t.nrows + 97.0 * t.nseg;
+  }
+  for (const LargeSeg& L : c->h_large) {
+    present[6] = true;
+    bytes[6] += 28.0 * (double)(off[(size_t)L.seg + 1] - off[(size_t)L.seg]) + 97.0;
+  }
+  int us[kUnits];
+  for (int u = 0; u < kUnits; ++u) us[u] = dm_ctx::kClassStream[u == 0 ? 0 : u <= 4 ? u + 2 : u == 5 ? kNumBins : kNumBins + 1];
+  for (;;) {
+    int load[dm_ctx::kAux] = {};
+    for (int u = 0; u < kUnits; ++u) load[us[u]] += present[u] ? 1 : 0;
+    int idle = -1, mover = -1;
+    for (int k = 0; k < dm_ctx::kAux && idle < 0; ++k)
+      if (load[k] == 0) idle = k;
+    for (int u = 0; u < kUnits; ++u)
+      if (present[u] && load[us[u]] > 1 && (mover < 0 || bytes[u] > bytes[mover])) mover = u;
+    if (idle < 0 || mover < 0) break;
+    us[mover] = idle;
+  }
+  for (int b = 0; b < kNumBins; ++b) c->class_stream[b] = us[unit_of_bin(b)];
+  c->class_stream[kNumBins] = us[5];
+  c->class_stream[kNumBins + 1] = us[6];
+}
+
 // Stream parts (dm_ctx::kParts): a workgroup bin holding every resource of the store
 // (no other bin, tile or chunk, no heterogeneous subclients) and at most kPartBytes of
 // rows, with enough items that each half still fills the GPU.
@@ -754,6 +809,7 @@ static void plan_parts(dm_ctx* c) {
     for (int j = 0; j <= dm_ctx::kParts; ++j)
       c->part_lo[b][j] = split ? n * j / dm_ctx::kParts : (j == 0 ? 0 : n);
   }
+  plan_streams(c);
 }
 
 // kBin4Wave (dm_device.h): bin 4 in stream parts and most of its resources FairShare
