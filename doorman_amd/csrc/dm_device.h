@@ -73,13 +73,22 @@ struct WorkItem {  // one resource of a size bin: no dependent load before its r
   int64_t lo;
 };
 
-// The sub-wave bins of one tick for k_subs, in launch order: 8x2 (9-16 rows),
-// 16x2 (17-32), 16x4 (33-64), 32x4 (65-128), 64x4 (129-256); blocks[k] workgroups
-// of 256 threads each (256 / G resources per workgroup).
+// The sub-wave bins of one tick for k_subs, in launch order, each bin in two shapes
+// (its items ordered lower shape first, build_plan): bin 7 (9-16 rows) 4x3 (9-12) and
+// 8x2 (13-16); bin 8 (17-32) 8x3 / 16x2; bin 0 (33-64) 16x3 / 16x4; bin 1 (65-128) 32x3 /
+// 32x4; bin 2 (129-256) 64x3 / 64x4.  blocks[k] workgroups of 256 threads each (256 / G
+// resources per workgroup).  Power-of-two shapes alone leave a Zipf population's lanes
+// mostly idle: its resources crowd at the low edge of every bin (a 9-row resource in 16
+// slots), and a sub-wave tick is bound by rows in flight, padded slots included
+// (tools/size_sweep.py: 9 rows 2.94 TB/s, 16 rows 4.23 TB/s of the byte model).
+constexpr int kSubShapes = 10;
+constexpr int kSubShapeG[kSubShapes] = {4, 8, 8, 16, 16, 16, 32, 32, 64, 64};
+constexpr int kSubShapeR[kSubShapes] = {3, 2, 3, 2, 3, 4, 3, 4, 3, 4};
+constexpr int kSubShapeBin[kSubShapes] = {7, 7, 8, 8, 0, 0, 1, 1, 2, 2};
 struct SubBins {
-  WorkItem* items[5];
-  int32_t n[5];
-  int32_t blocks[5];
+  WorkItem* items[kSubShapes];
+  int32_t n[kSubShapes];
+  int32_t blocks[kSubShapes];
 };
 
 struct Chunk {  // kChunkRows rows of one large resource

@@ -427,18 +427,19 @@ __device__ __forceinline__ void sub_part(const DevParams& p, WorkItem* __restric
   group_segment<G, R>(p, items[i], items + i, threadIdx.x & (G - 1), lds, general_list, general_count);
 }
 
+template <int K>
+__device__ __forceinline__ void sub_shape(const DevParams& p, const SubBins& sb, int b, int32_t* general_list,
+                                          int32_t* general_count) {
+  if constexpr (K < kSubShapes) {
+    if (b < sb.blocks[K])
+      return sub_part<kSubShapeG[K], kSubShapeR[K]>(p, sb.items[K], sb.n[K], b, general_list, general_count);
+    sub_shape<K + 1>(p, sb, b - sb.blocks[K], general_list, general_count);
+  }
+}
+
 __global__ __launch_bounds__(256, 5) void k_subs(DevParams p, SubBins sb, int32_t* general_list,
                                               int32_t* general_count) {
-  int b = blockIdx.x;
-  if (b < sb.blocks[0]) return sub_part<8, 2>(p, sb.items[0], sb.n[0], b, general_list, general_count);
-  b -= sb.blocks[0];
-  if (b < sb.blocks[1]) return sub_part<16, 2>(p, sb.items[1], sb.n[1], b, general_list, general_count);
-  b -= sb.blocks[1];
-  if (b < sb.blocks[2]) return sub_part<16, 4>(p, sb.items[2], sb.n[2], b, general_list, general_count);
-  b -= sb.blocks[2];
-  if (b < sb.blocks[3]) return sub_part<32, 4>(p, sb.items[3], sb.n[3], b, general_list, general_count);
-  b -= sb.blocks[3];
-  if (b < sb.blocks[4]) return sub_part<64, 4>(p, sb.items[4], sb.n[4], b, general_list, general_count);
+  sub_shape<0>(p, sb, (int)blockIdx.x, general_list, general_count);
 }
 
 // --------------------------------------------------------------------------
@@ -3010,7 +3011,7 @@ hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_
 
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st) {
   unsigned blocks = 0;
-  for (int k = 0; k < 5; ++k) blocks += (unsigned)sb.blocks[k];
+  for (int k = 0; k < kSubShapes; ++k) blocks += (unsigned)sb.blocks[k];
   if (blocks == 0) return hipSuccess;
   k_subs<<<blocks, 256, 0, st>>>(p, sb, glist, gcount);
   return hipGetLastError();

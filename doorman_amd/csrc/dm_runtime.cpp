@@ -173,6 +173,7 @@ struct dm_ctx {
   // leaves some auxiliary stream without work, classes that would share a stream move
   // onto the idle ones (a shard of a Zipf population holds only some classes)
   int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};
+  int64_t h_sub_lo[kNumBins] = {};  // a sub-wave bin's items of its lower shape (first in the bin)
   hipStream_t aux[kAux] = {};
   bool aux_own_queue = false;  // each auxiliary stream has a hardware queue of its own (CU mask)
   uint64_t aux_seq = 0;        // the stream set's creation order in the process (take_aux)
@@ -710,6 +711,16 @@ static void build_plan(dm_ctx* c) {
     }
   }
   tclose();
+  // the sub-wave bins: items of the bin's lower shape (kSubShapeG x kSubShapeR slots,
+  // dm_device.h) first, each part in resource order
+  for (int k = 0; k < kSubShapes; ++k) {
+    const int b = kSubShapeBin[k];
+    if (k > 0 && kSubShapeBin[k - 1] == b) continue;
+    const int cap = kSubShapeG[k] * kSubShapeR[k];
+    std::vector<WorkItem>& v = c->h_bins[b];
+    auto mid = std::stable_partition(v.begin(), v.end(), [&](const WorkItem& w) { return (w.n & 0xFFFF) <= cap; });
+    c->h_sub_lo[b] = (int64_t)(mid - v.begin());
+  }
   // Large resources largest first: a resource is verified by its last-arriving chunk,
   // and the largest's verification (the longest canonical trees) then overlaps the
   // other chunks instead of trailing the launch.  Each resource's chunks stay
@@ -1620,14 +1631,15 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // the workgroup bins split by the dense hint after a writeback tick (hints set)
   const bool split_dense = c->have_result && c->last_writeback;
   // the sub-wave bins (8x2, 16x2, 16x4, 32x4, 64x4) in one launch on bin 0's stream
-  static constexpr int kSubBins[5] = {7, 8, 0, 1, 2}, kSubG[5] = {8, 16, 16, 32, 64};
   {
     SubBins sb{};
     int nonempty = 0;
-    for (int k = 0; k < 5; ++k) {
-      const int b = kSubBins[k], n = (int)c->h_bins[b].size();
-      const int per = 256 / kSubG[k];
-      sb.items[k] = c->bins[b].p;
+    for (int k = 0; k < kSubShapes; ++k) {  // each sub-wave bin: its lower shape's items first
+      const int b = kSubShapeBin[k], nb = (int)c->h_bins[b].size(), nlo = (int)c->h_sub_lo[b];
+      const bool lower = k == 0 || kSubShapeBin[k - 1] != b;
+      const int n = lower ? nlo : nb - nlo;
+      const int per = 256 / kSubShapeG[k];
+      sb.items[k] = c->bins[b].p + (lower ? 0 : nlo);
       sb.n[k] = n;
       sb.blocks[k] = (n + per - 1) / per;
       nonempty += n > 0;
