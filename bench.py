@@ -157,7 +157,10 @@ def dense_fraction(eng, snap) -> float:
     return eng.store_stats()["dense_leases"] / group if group else 0.0
 
 
-_SUB_EDGES = [("sub8x2", 9, 16), ("sub16x2", 17, 32), ("sub16x4", 33, 64), ("sub32x4", 65, 128),
+SMALL_MAX = 4  # dm_device.h kSmallMax: resources of at most this many rows run in the tiles
+# the sub-wave bins by row range (their names are the library's bin names; each runs in
+# several G x R shapes inside the one k_subs launch, dm_device.h SubBins)
+_SUB_EDGES = [("sub8x2", 5, 16), ("sub16x2", 17, 32), ("sub16x4", 33, 64), ("sub32x4", 65, 128),
               ("wave64x4", 129, 256)]
 _GROUP_EDGES = [("block128x4", 257, 512), ("block128x8", 513, 1024), ("block256x8", 1025, 2048),
                 ("block2k4k", 2049, 4096)]
@@ -177,11 +180,11 @@ def kernel_units(snap):
     def rng(lo, hi):
         m = (sizes >= lo) & (sizes <= hi)
         return int(sizes[m].sum()), int(m.sum())
-    small = sizes <= 8
+    small = sizes <= SMALL_MAX
     units["small_tiles"] = (int(sizes[small].sum()), int(small.sum()))
     for name, lo, hi in _SUB_EDGES + _GROUP_EDGES:
         units[name] = rng(lo, hi)
-    units["subs_merged"] = rng(9, 256)  # the sub-wave bins in one launch (k_subs)
+    units["subs_merged"] = rng(SMALL_MAX + 1, 256)  # the sub-wave bins in one launch (k_subs)
     for name, _, _ in _GROUP_EDGES:  # the split form's two kernels
         units[name + "_dense"] = units[name]
         units[name + "_rest"] = (0, 0)  # only what the dense kernel queued; counted with the dense kernel
@@ -194,7 +197,7 @@ def kernel_units(snap):
     # the redo rewrites only the resources whose speculation failed (none in a steady tick:
     # its launch then reads one word per workgroup)
     units["large_redo"] = (0, 0)
-    units["general"] = rng(9, 1 << 62)  # heterogeneous FairShare: any resource above 8 rows may land there
+    units["general"] = rng(SMALL_MAX + 1, 1 << 62)  # heterogeneous FairShare: any resource above the tiles may land there
     units["hier_publish"] = (0, R)
     units["hier_root"] = (0, R)
     units["hier_gather"] = (0, 0)  # 16 B per resource per server: a collective, not HBM streaming

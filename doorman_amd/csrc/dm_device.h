@@ -23,14 +23,14 @@ constexpr int64_t kSubMax = 0x7FFFFFFE;  // largest subclients value a row holds
 
 // Dispatch bins.  A segment of n rows goes to:
 //   n <= kSmallMax            : tiles of consecutive resources, one resource per thread (k_tile_small)
-//   n <= 16 / 32              : 8- / 16-lane groups, 2 rows per lane, 8 / 4 resources per wave (bins 7, 8)
+//   n <= 16 / 32              : 2- to 8-lane groups, 3-4 rows per lane (bins 7, 8; SubBins below)
 //   n <= 64 / 128             : 16- / 32-lane groups, 4 rows per lane, 4 / 2 resources per wave (bins 0, 1)
 //   n <= 256                  : one wave per resource, 4 rows per lane (4 resources per workgroup)
 //   n <= 512 / 1024           : one 128-thread workgroup, 4 / 8 rows per thread in VGPRs (bins 3, 4)
 //   n <= 2048                 : one 256-thread workgroup, 8 rows per thread (bin 5)
 //   n <= 4096                 : one 256 x 16 or 512 x 8 workgroup (bin 6, kBin6Wide below)
 //   n >  kLargeMin            : multi-workgroup chunks of kChunkRows rows
-constexpr int kSmallMax = 8;  // (16 and 32 -- bins 7 and 8 in the tiles, one resource per thread -- lost: +8 / +25 us on C2)
+constexpr int kSmallMax = 4;  // (8: 5-8 rows in the tiles, 2.9 TB/s at 8 rows, one resource per thread; 16 and 32 lost +8 / +25 us on C2)
 static_assert(kSmallMax <= 32, "k_tile_small keeps a resource's live rows in a 32-bit mask");
 constexpr int kLargeMin = 4096;
 constexpr int kChunkRows = 2048;
@@ -73,18 +73,19 @@ struct WorkItem {  // one resource of a size bin: no dependent load before its r
   int64_t lo;
 };
 
-// The sub-wave bins of one tick for k_subs, in launch order, each bin in two shapes
-// (its items ordered lower shape first, build_plan): bin 7 (9-16 rows) 4x3 (9-12) and
-// 8x2 (13-16); bin 8 (17-32) 8x3 / 16x2; bin 0 (33-64) 16x3 / 16x4; bin 1 (65-128) 32x3 /
-// 32x4; bin 2 (129-256) 64x3 / 64x4.  blocks[k] workgroups of 256 threads each (256 / G
-// resources per workgroup).  Power-of-two shapes alone leave a Zipf population's lanes
-// mostly idle: its resources crowd at the low edge of every bin (a 9-row resource in 16
-// slots), and a sub-wave tick is bound by rows in flight, padded slots included
-// (tools/size_sweep.py: 9 rows 2.94 TB/s, 16 rows 4.23 TB/s of the byte model).
-constexpr int kSubShapes = 10;
-constexpr int kSubShapeG[kSubShapes] = {4, 8, 8, 16, 16, 16, 32, 32, 64, 64};
-constexpr int kSubShapeR[kSubShapes] = {3, 2, 3, 2, 3, 4, 3, 4, 3, 4};
-constexpr int kSubShapeBin[kSubShapes] = {7, 7, 8, 8, 0, 0, 1, 1, 2, 2};
+// The sub-wave bins of one tick for k_subs, in launch order, each bin in several
+// shapes G x R (G lanes per resource, R rows per lane; a bin's items ordered by shape,
+// build_plan): bin 7 (5-16 rows) 2x3 (5-6), 2x4 (7-8), 4x3 (9-12), 4x4 (13-16); bin 8 (17-32) 8x3 /
+// 8x4; bin 0 (33-64) 16x3 / 16x4; bin 1 (65-128) 32x3 / 32x4; bin 2 (129-256) 64x3 / 64x4.
+// blocks[k] workgroups of 256 threads each (256 / G resources per workgroup).
+// Power-of-two shapes alone leave a Zipf population's lanes mostly idle: its resources
+// crowd at the low edge of every bin (a 9-row resource in 16 slots), and a sub-wave tick
+// is bound by rows in flight, padded slots included; more rows per lane also beat wider
+// groups at equal slots (tools/size_sweep.py, profiles/r06_size_sweep.md).
+constexpr int kSubShapes = 12;
+constexpr int kSubShapeG[kSubShapes] = {2, 2, 4, 4, 8, 8, 16, 16, 32, 32, 64, 64};
+constexpr int kSubShapeR[kSubShapes] = {3, 4, 3, 4, 3, 4, 3, 4, 3, 4, 3, 4};
+constexpr int kSubShapeBin[kSubShapes] = {7, 7, 7, 7, 8, 8, 0, 0, 1, 1, 2, 2};
 struct SubBins {
   WorkItem* items[kSubShapes];
   int32_t n[kSubShapes];

@@ -112,8 +112,9 @@ __device__ __forceinline__ T readlane_any(const T& v, int lane) {
 // wave) reduce within themselves: every lane of the group gets its group's total.
 template <int G, typename T, typename Op>
 __device__ __forceinline__ T wave_reduce_g(T v, Op op) {
-  static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "sub-wave group");
-  v = op(v, dpp_any<0xB1>(v));   // quad_perm [1,0,3,2]
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "sub-wave group");
+  v = op(v, dpp_any<0xB1>(v));   // quad_perm [1,0,3,2]: 2-lane totals
+  if constexpr (G == 2) return v;
   v = op(v, dpp_any<0x4E>(v));   // quad_perm [2,3,0,1]: 4-lane totals
   if constexpr (G == 4) return v;
   v = op(v, dpp_any<0x141>(v));  // row_half_mirror: 8-lane totals

@@ -173,7 +173,7 @@ struct dm_ctx {
   // leaves some auxiliary stream without work, classes that would share a stream move
   // onto the idle ones (a shard of a Zipf population holds only some classes)
   int class_stream[kNumBins + 2] = {2, 2, 2, 2, 1, 1, 1, 2, 2, 3, 0};
-  int64_t h_sub_lo[kNumBins] = {};  // a sub-wave bin's items of its lower shape (first in the bin)
+  int64_t h_shape_lo[kSubShapes] = {}, h_shape_n[kSubShapes] = {};  // sub-wave shapes' items within their bins
   hipStream_t aux[kAux] = {};
   bool aux_own_queue = false;  // each auxiliary stream has a hardware queue of its own (CU mask)
   uint64_t aux_seq = 0;        // the stream set's creation order in the process (take_aux)
@@ -711,15 +711,17 @@ static void build_plan(dm_ctx* c) {
     }
   }
   tclose();
-  // the sub-wave bins: items of the bin's lower shape (kSubShapeG x kSubShapeR slots,
-  // dm_device.h) first, each part in resource order
+  // the sub-wave bins: items ordered by shape (the narrowest kSubShapeG x kSubShapeR
+  // that holds the resource, dm_device.h), each shape's items in resource order
   for (int k = 0; k < kSubShapes; ++k) {
     const int b = kSubShapeBin[k];
-    if (k > 0 && kSubShapeBin[k - 1] == b) continue;
-    const int cap = kSubShapeG[k] * kSubShapeR[k];
+    const bool first = k == 0 || kSubShapeBin[k - 1] != b;
+    const int64_t lo = first ? 0 : c->h_shape_lo[k - 1] + c->h_shape_n[k - 1];
     std::vector<WorkItem>& v = c->h_bins[b];
-    auto mid = std::stable_partition(v.begin(), v.end(), [&](const WorkItem& w) { return (w.n & 0xFFFF) <= cap; });
-    c->h_sub_lo[b] = (int64_t)(mid - v.begin());
+    const int cap = kSubShapeG[k] * kSubShapeR[k];
+    auto mid = std::stable_partition(v.begin() + lo, v.end(), [&](const WorkItem& w) { return (w.n & 0xFFFF) <= cap; });
+    c->h_shape_lo[k] = lo;
+    c->h_shape_n[k] = (int64_t)(mid - v.begin()) - lo;
   }
   // Large resources largest first: a resource is verified by its last-arriving chunk,
   // and the largest's verification (the longest canonical trees) then overlaps the
@@ -1634,12 +1636,10 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   {
     SubBins sb{};
     int nonempty = 0;
-    for (int k = 0; k < kSubShapes; ++k) {  // each sub-wave bin: its lower shape's items first
-      const int b = kSubShapeBin[k], nb = (int)c->h_bins[b].size(), nlo = (int)c->h_sub_lo[b];
-      const bool lower = k == 0 || kSubShapeBin[k - 1] != b;
-      const int n = lower ? nlo : nb - nlo;
+    for (int k = 0; k < kSubShapes; ++k) {  // each sub-wave bin's items by shape (build_plan)
+      const int b = kSubShapeBin[k], n = (int)c->h_shape_n[k];
       const int per = 256 / kSubShapeG[k];
-      sb.items[k] = c->bins[b].p + (lower ? 0 : nlo);
+      sb.items[k] = c->bins[b].p + c->h_shape_lo[k];
       sb.n[k] = n;
       sb.blocks[k] = (n + per - 1) / per;
       nonempty += n > 0;

@@ -62,7 +62,7 @@ def binned_sizes(rng, per_bin=3, large=True):
     for lo, hi in edges:
         sizes += list(rng.integers(lo, hi + 1, per_bin))
     sizes += [8, 9, 16, 17, 32, 33, 64, 65, 128, 129, 256, 257, 512, 513, 1024, 1025, 2048, 2049, 4096]
-    sizes += [12, 13, 24, 25, 48, 49, 96, 97, 192, 193]  # the sub-wave bins' two shapes (dm_device.h kSubShape*)
+    sizes += [4, 5, 6, 7, 12, 13, 24, 25, 48, 49, 96, 97, 192, 193]  # the sub-wave shapes' edges (dm_device.h kSubShape*)
     if large:  # chunk edges of the large path (kChunkRows = 2048): 1-row tail, exact multiples
         sizes += [4097, 6144, 8192, 10241]
     rng.shuffle(sizes)

@@ -9,7 +9,8 @@ released-row masks and no rest kernel, the alternate gets column.  This test run
 exactly those ticks on bench.make_workload("c2") and, after every synchronised
 segment, compares a sample of resources from every size class with the oracle
 (O.apportion) applied tick by tick on a host copy of their rows:
-  * the 10 largest resources, both sides of every bin edge (8/9 ... 4096/4097),
+  * the 10 largest resources, both sides of every bin and sub-wave shape edge
+    (4/5, 6/7, 8/9, 12/13 ... 4096/4097),
     learning, Static and NoAlgorithm resources, and random resources of every class;
   * segment 0 from the load (the first tick takes the four-launch chain: loaded rows
     carry explicit expiries, 1 % of them already past), segment 1 the steady state;
@@ -42,14 +43,14 @@ def _pick(snap, rng):
     sizes = np.diff(snap["seg_off"])
     R = len(sizes)
     pick = list(range(10))  # the largest (sizes fall with the Zipf rank)
-    for e in (8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096):  # both sides of every bin edge
+    for e in (4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 512, 1024, 2048, 4096):  # every bin and shape edge
         above = np.flatnonzero(sizes > e)
         below = np.flatnonzero(sizes <= e)
         if len(above):
             pick.append(int(above[-1]))
         if len(below):
             pick.append(int(below[0]))
-    classes = [(1, 1), (2, 8), (9, 256), (257, 4096), (4097, 1 << 40)]
+    classes = [(1, 1), (2, 4), (5, 16), (17, 256), (257, 4096), (4097, 1 << 40)]
     learning = snap["learning_end_ns"] != W.INT64_MIN
     for lo, hi in classes:
         ids = np.flatnonzero((sizes >= lo) & (sizes <= hi))

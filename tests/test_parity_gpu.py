@@ -118,10 +118,10 @@ def test_fair_share_heavy_contention(eng, seed):
 
 @pytest.mark.parametrize("seed", range(5))
 def test_small_resources_bit_exact(eng, seed):
-    """Resources of <= kSmallMax (8) rows go through the wave-packed literal path, which
+    """Resources of <= kSmallMax (4) rows go through the tiles' literal path, which
     sums in row order like the oracle: results are bit-identical, per-resource sums too."""
     rng = np.random.default_rng(3000 + seed)
-    snap = snapshot_with_sizes(rng, rng.integers(0, 9, 3000), hetero=seed % 2 == 1, edge=seed >= 3)
+    snap = snapshot_with_sizes(rng, rng.integers(0, 5, 3000), hetero=seed % 2 == 1, edge=seed >= 3)
     if seed == 2:
         for k in ("agg_count", "agg_sum_has", "agg_sum_wants"):
             snap.pop(k)
