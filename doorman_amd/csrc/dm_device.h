@@ -57,12 +57,23 @@ constexpr int64_t kStreamBytes = 1LL << 30;
 // memory round trip before its compute instead of the packed kernel's two.
 constexpr int kTileRows = 1024;  // (512-row tiles: C2 +1.7 us)
 constexpr int kTileRes = 256;
+// A run of fewer than kTileMinRun consecutive small resources (a store whose small and
+// larger resources interleave, as resource ids are handed out in no particular order)
+// does not get a tile of its own (a workgroup for a handful of resources: a random mix
+// of 2-6-row resources ran 314 us against 15 + 10 for its two classes alone,
+// tools/overlap_probe.py): its resources go to list tiles, which name up to kTileRes
+// scattered small resources (TileEntry) and stage each one's rows by its own thread.
+constexpr int kTileMinRun = 64;
 struct Tile {
-  int32_t first_seg;
+  int32_t first_seg;  // list tile: its first entry in the tile list
   int32_t nseg;    // <= kTileRes
-  int64_t row0;
+  int64_t row0;    // list tile: unused
   int32_t nrows;   // <= kTileRows
-  int32_t pad;
+  int32_t list;    // 1: a list tile
+};
+struct TileEntry {
+  int32_t seg;
+  int32_t lds;  // the resource's first row in the tile's LDS rows
 };
 
 struct WorkItem {  // one resource of a size bin: no dependent load before its rows

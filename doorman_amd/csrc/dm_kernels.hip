@@ -459,38 +459,68 @@ struct TileLds {
   uint8_t lv[kTileRows];
 };
 
-__global__ __launch_bounds__(256) void k_tile_small(DevParams p, const Tile* __restrict__ tiles) {
+__global__ __launch_bounds__(256) void k_tile_small(DevParams p, const Tile* __restrict__ tiles,
+                                                    const TileEntry* __restrict__ list) {
   __shared__ TileLds L;
   const Tile tl = tiles[blockIdx.x];
   const int t = threadIdx.x;
-  const int64_t row0 = tl.row0;
+  const bool lst = tl.list != 0;  // (uniform)
   const int nrows = tl.nrows, nseg = tl.nseg;
   constexpr int K = kTileRows / 256;
   // the records first, then the rows: every load of the tile is in flight before the
   // first is consumed (the LDS stores below)
   const bool own = t < nseg;
-  const int seg = tl.first_seg + (own ? t : 0);
-  const int64_t lo64 = p.seg_off[seg], hi64 = p.seg_off[seg + 1];
-  const Res rs = load_res(p, seg);
-  double wv[K], hv[K];
-  int sv[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if (k * 256 < nrows) {  // uniform
-      const int i = k * 256 + t;
-      const unsigned u = (unsigned)(i < nrows ? i : nrows - 1);
-      wv[k] = *col_at(p.wants + row0, u);
-      hv[k] = *col_at(p.has + row0, u);
-      sv[k] = *col_at(p.sub + row0, u);
-    }
+  int seg, ldo = 0;
+  if (lst) {
+    const TileEntry e = list[tl.first_seg + (own ? t : 0)];
+    seg = e.seg;
+    ldo = e.lds;
+  } else {
+    seg = tl.first_seg + (own ? t : 0);
   }
+  const int64_t lo64 = p.seg_off[seg], hi64 = p.seg_off[seg + 1];
+  // a row's global index is base + its LDS index (a list tile: per resource)
+  const int64_t row0 = lst ? lo64 - ldo : tl.row0;
+  const Res rs = load_res(p, seg);
+  if (lst) {  // each thread its own resource's rows (n <= kSmallMax)
+    const int n = own ? (int)(hi64 - lo64) : 0;
+    double wv[kSmallMax], hv[kSmallMax];
+    int sv[kSmallMax];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int i = k * 256 + t;
-    if (k * 256 < nrows && i < nrows) {
-      L.w[i] = wv[k];
-      L.h[i] = hv[k];
-      L.sr[i] = sv[k];
+    for (int j = 0; j < kSmallMax; ++j)
+      if (j < n) {
+        wv[j] = p.wants[lo64 + j];
+        hv[j] = p.has[lo64 + j];
+        sv[j] = p.sub[lo64 + j];
+      }
+#pragma unroll
+    for (int j = 0; j < kSmallMax; ++j)
+      if (j < n) {
+        L.w[ldo + j] = wv[j];
+        L.h[ldo + j] = hv[j];
+        L.sr[ldo + j] = sv[j];
+      }
+  } else {
+    double wv[K], hv[K];
+    int sv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (k * 256 < nrows) {  // uniform
+        const int i = k * 256 + t;
+        const unsigned u = (unsigned)(i < nrows ? i : nrows - 1);
+        wv[k] = *col_at(p.wants + row0, u);
+        hv[k] = *col_at(p.has + row0, u);
+        sv[k] = *col_at(p.sub + row0, u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = k * 256 + t;
+      if (k * 256 < nrows && i < nrows) {
+        L.w[i] = wv[k];
+        L.h[i] = hv[k];
+        L.sr[i] = sv[k];
+      }
     }
   }
   __syncthreads();
@@ -605,6 +635,24 @@ __global__ __launch_bounds__(256) void k_tile_small(DevParams p, const Tile* __r
       osh += g - h;
     }
     write_resource(p, seg, rs, Clean{count, osh, sw}, 0.0);
+  }
+  if (lst) {  // a list tile: each thread its own resource's leases
+    if (own) {
+      for (int i = (int)(lo64 - row0); i < (int)(hi64 - row0); ++i) {
+        const int32_t raw = L.sr[i];
+        if (L.lv[i]) {
+          __builtin_nontemporal_store(L.h[i], col_at(p.out_gets + row0, (uint32_t)i));
+          if (p.writeback && raw < 0) *col_at(p.out_sub + row0, (uint32_t)i) = raw & 0x7FFFFFFF;
+        } else {
+          __builtin_nontemporal_store(0.0, col_at(p.out_gets + row0, (uint32_t)i));
+          if (p.writeback && !sub_released(raw)) {
+            *col_at(p.out_wants + row0, (uint32_t)i) = 0.0;
+            *col_at(p.out_sub + row0, (uint32_t)i) = (int32_t)kSubReleased;
+          }
+        }
+      }
+    }
+    return;
   }
   __syncthreads();
   // the leases, row-parallel (put_live / put_released of the packed kernel)
@@ -2987,9 +3035,9 @@ __global__ __launch_bounds__(256) void k_hier_tick(DevParams p, HierArgs ha) {
 // --------------------------------------------------------------------------
 // host-side launchers (called by dm_runtime.cpp)
 // --------------------------------------------------------------------------
-hipError_t launch_tile_small(const DevParams& p, const Tile* tiles, int n, hipStream_t st) {
+hipError_t launch_tile_small(const DevParams& p, const Tile* tiles, const TileEntry* list, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_tile_small<<<n, 256, 0, st>>>(p, tiles);
+  k_tile_small<<<n, 256, 0, st>>>(p, tiles, list);
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@
 #include "dm_device.h"
 
 namespace dm {
-hipError_t launch_tile_small(const DevParams& p, const Tile* tiles, int n, hipStream_t st);
+hipError_t launch_tile_small(const DevParams& p, const Tile* tiles, const TileEntry* list, int n, hipStream_t st);
 hipError_t launch_bin(int bin, const DevParams& p, WorkItem* segs, int n, int32_t* glist, int32_t* gcount,
                       hipStream_t st);
 hipError_t launch_subs(const DevParams& p, const SubBins& sb, int32_t* glist, int32_t* gcount, hipStream_t st);
@@ -308,6 +308,8 @@ struct dm_ctx {
   }
   // plan
   std::vector<Tile> h_tiles;  // small resources (n <= kSmallMax) in tiles (k_tile_small)
+  std::vector<TileEntry> h_tile_list;  // the list tiles' resources
+  DBuf<TileEntry> tile_list;
   std::vector<WorkItem> h_bins[kNumBins];
   std::vector<Chunk> h_chunks;
   std::vector<LargeSeg> h_large;
@@ -684,33 +686,59 @@ static void build_plan(dm_ctx* c) {
   c->h_large.clear();
   const std::vector<int64_t>& off = c->h_seg_off;
   std::vector<int64_t> large;
-  // runs of consecutive small resources: tiles of at most kTileRes resources and kTileRows rows
-  Tile tc{};
-  bool topen = false;
-  auto tclose = [&]() {
-    if (topen) c->h_tiles.push_back(tc);
-    topen = false;
-  };
-  for (int64_t r = 0; r < c->R; ++r) {
-    const int64_t n = off[r + 1] - off[r];
-    if (n <= kSmallMax) {
-      if (topen && (tc.nrows + n > kTileRows || tc.nseg >= kTileRes)) tclose();
+  c->h_tile_list.clear();
+  // runs of at least kTileMinRun consecutive small resources: tiles of at most kTileRes
+  // resources and kTileRows rows; the small resources of shorter runs: list tiles
+  std::vector<int32_t> scattered;
+  auto run_tiles = [&](int64_t r0, int64_t r1) {
+    if (r1 - r0 < kTileMinRun) {
+      for (int64_t r = r0; r < r1; ++r) scattered.push_back((int32_t)r);
+      return;
+    }
+    Tile tc{};
+    bool topen = false;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t n = off[r + 1] - off[r];
+      if (topen && (tc.nrows + n > kTileRows || tc.nseg >= kTileRes)) {
+        c->h_tiles.push_back(tc);
+        topen = false;
+      }
       if (!topen) {
         tc = Tile{(int32_t)r, 0, off[r], 0, 0};
         topen = true;
       }
       tc.nseg += 1;
       tc.nrows += (int32_t)n;
+    }
+    if (topen) c->h_tiles.push_back(tc);
+  };
+  int64_t run0 = -1;
+  for (int64_t r = 0; r < c->R; ++r) {
+    const int64_t n = off[r + 1] - off[r];
+    if (n <= kSmallMax) {
+      if (run0 < 0) run0 = r;
       continue;
     }
-    tclose();
+    if (run0 >= 0) run_tiles(run0, r);
+    run0 = -1;
     if (n <= kLargeMin) {
       c->h_bins[bin_of(n)].push_back(WorkItem{(int32_t)r, (int32_t)n, off[r]});
     } else {
       large.push_back(r);
     }
   }
-  tclose();
+  if (run0 >= 0) run_tiles(run0, c->R);
+  static_assert(kTileRes * kSmallMax <= kTileRows, "a list tile of kTileRes resources fits its LDS rows");
+  for (size_t i = 0; i < scattered.size(); i += kTileRes) {
+    const size_t e = std::min(scattered.size(), i + (size_t)kTileRes);
+    Tile tc{(int32_t)c->h_tile_list.size(), (int32_t)(e - i), 0, 0, 1};
+    for (size_t j = i; j < e; ++j) {
+      const int32_t r = scattered[j];
+      c->h_tile_list.push_back(TileEntry{r, tc.nrows});
+      tc.nrows += (int32_t)(off[(size_t)r + 1] - off[(size_t)r]);
+    }
+    c->h_tiles.push_back(tc);
+  }
   // the sub-wave bins: items ordered by shape (the narrowest kSubShapeG x kSubShapeR
   // that holds the resource, dm_device.h), each shape's items in resource order
   for (int k = 0; k < kSubShapes; ++k) {
@@ -884,6 +912,7 @@ static int set_parts_ok(dm_ctx* c, bool ok) {
 static int upload_plan(dm_ctx* c) {
   hipStream_t st = c->stream;
   DM_HIP(c, upload(c->tiles, c->h_tiles.data(), c->h_tiles.size(), st), "plan tiles");
+  DM_HIP(c, upload(c->tile_list, c->h_tile_list.data(), c->h_tile_list.size(), st), "plan tiles");
   for (int b = 0; b < kNumBins; ++b) DM_HIP(c, upload(c->bins[b], c->h_bins[b].data(), c->h_bins[b].size(), st), "plan bins");
   DM_HIP(c, upload(c->chunks, c->h_chunks.data(), c->h_chunks.size(), st), "plan chunks");
   DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
@@ -1724,7 +1753,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     }
   }
   if (!c->h_tiles.empty())
-    DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_tile_small(p, c->tiles.p, (int)c->h_tiles.size(), s_small); }),
+    DM_HIP(c, timed(KC_SMALL, s_small, [&] { return launch_tile_small(p, c->tiles.p, c->tile_list.p, (int)c->h_tiles.size(), s_small); }),
            "small kernel");
   if (fork) {
     c->aux_pending = true;

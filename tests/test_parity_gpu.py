@@ -116,6 +116,32 @@ def test_fair_share_heavy_contention(eng, seed):
     assert_resources_match(snap, res, ref)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_scattered_small_resources_list_tiles(eng, seed):
+    """Small resources interleaved with larger ones (runs shorter than kTileMinRun = 64,
+    as in a store whose resource ids come in no size order) go to list tiles: each
+    thread stages its own resource's rows.  The small resources' leases and sums are
+    still bit-exact (row-order sums); long runs beside them keep the contiguous tiles."""
+    rng = np.random.default_rng(3100 + seed)
+    small = rng.integers(0, 5, 2000)
+    other = rng.integers(5, 300, 2000)
+    mix = np.where(rng.random(2000) < 0.5, small, other)
+    sizes = np.concatenate([mix, rng.integers(1, 5, 700), mix[::-1]])  # a long run in the middle
+    snap = snapshot_with_sizes(rng, sizes, hetero=seed == 1, edge=seed == 2)
+    gets, exp, res = run(eng, snap)
+    ref = O.apportion(snap, NOW)
+    assert_leases_match(snap, gets, exp, ref, f"seed={seed}")
+    assert_resources_match(snap, res, ref)
+    so = snap["seg_off"]
+    sm = np.flatnonzero(np.diff(so) <= 4)
+    rows = np.concatenate([np.arange(so[r], so[r + 1]) for r in sm])
+    assert float_close(gets[rows], ref["gets"][rows], 0.0, tol=0.0).all()
+    for a, b in (("sum_has", "res_sum_has"), ("sum_wants", "res_sum_wants")):
+        assert float_close(res[a][sm], ref[b][sm], 0.0, tol=0.0).all(), a
+    info = eng.plan_info()
+    assert info["small_tiles"] > 1
+
+
 @pytest.mark.parametrize("seed", range(5))
 def test_small_resources_bit_exact(eng, seed):
     """Resources of <= kSmallMax (4) rows go through the tiles' literal path, which
