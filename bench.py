@@ -73,17 +73,36 @@ def c2_bounds(world: int, snap=None):
     return partition(sizes, world)
 
 
-def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicated"):
+C2_PARTITIONS = ("lpt", "contiguous")
+
+
+def c2_shard_ids(world: int, rank: int, partition: str = "lpt", snap=None) -> np.ndarray:
+    """configs[2]'s resource ids of one rank: lpt (default) -- hierarchy.assign_lpt, every
+    rank the same mix of size classes; contiguous -- c2_bounds' range."""
+    from doorman_amd import workloads as W
+    from doorman_amd.hierarchy import assign_lpt
+    sizes = np.diff(snap["seg_off"]) if snap is not None else W.zipf_sizes()
+    if partition == "contiguous":
+        b = c2_bounds(world, snap)
+        return np.arange(int(b[rank]), int(b[rank + 1]), dtype=np.int64)
+    return np.flatnonzero(assign_lpt(sizes, world) == rank).astype(np.int64)
+
+
+def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicated", partition: str = "lpt"):
     from doorman_amd import workloads as W
     if name == "c1":
         return W.c1(seed=1 + 1000 * rank, kind=W.FAIR_SHARE)
     if name == "c1ps":
         return W.c1(seed=1 + 1000 * rank, kind=W.PROPORTIONAL_SHARE)
     if name == "c2":
-        if layout == "sharded":  # this rank's range of the one 1M-resource Zipf snapshot
+        if layout == "sharded":  # this rank's resources of the one 1M-resource Zipf snapshot
             snap = W.c2(seed=2)
-            b = c2_bounds(world, snap)
-            return W.subset_range(snap, int(b[rank]), int(b[rank + 1]))
+            if world <= 1:
+                return snap
+            if partition == "contiguous":
+                b = c2_bounds(world, snap)
+                return W.subset_range(snap, int(b[rank]), int(b[rank + 1]))
+            return W.subset(snap, c2_shard_ids(world, rank, partition, snap))
         return W.c2(seed=2 + 1000 * rank)
     if name == "c3":
         if layout == "sharded":  # this rank's range of the one 100M-lease snapshot
@@ -767,7 +786,7 @@ def c2_shard_step(torch, Engine, dev_index, args, world, rank, sync_ranks, steps
     every bench step (timed_steps); returns the rank's numbers."""
     from doorman_amd import workloads as W
     from doorman_amd.hierarchy import tick_cost
-    snap = make_workload("c2", rank, world, "sharded")
+    snap = make_workload("c2", rank, world, "sharded", args.c2_partition)
     eng = Engine(dev_index, args.lib)
     try:
         eng.load(snap)
@@ -784,18 +803,23 @@ def c2_shard_step(torch, Engine, dev_index, args, world, rank, sync_ranks, steps
         eng.close()
 
 
-def shard_summary(world, per_rank, steps):
+def shard_summary(world, per_rank, steps, partition):
     """Whole-node numbers of a sharded configs[2] run from every rank's own numbers."""
     t = [r["step_us"] for r in per_rank]
     pb = [r["predicted_bytes"] for r in per_rank]
     n = sum(r["leases"] for r in per_rank)
-    return {"node_gpus": world, "leases_total": n,
-            "bounds": [int(x) for x in c2_bounds(world)],
-            "step_us_max": max(t), "step_us_min": min(t), "step_max_over_min": round(max(t) / min(t), 4),
-            "predicted_bytes_max_over_mean": round(max(pb) / (sum(pb) / len(pb)), 4),
-            "partition": "contiguous resource-id ranges balanced by hierarchy.tick_cost (28 B per lease + 97 B per "
-                         "resource), not lease count",
-            "ranks": per_rank}
+    out = {"node_gpus": world, "leases_total": n,
+           "step_us_max": max(t), "step_us_min": min(t), "step_max_over_min": round(max(t) / min(t), 4),
+           "predicted_bytes_max_over_mean": round(max(pb) / (sum(pb) / len(pb)), 4),
+           "partition": partition,
+           "partition_note": ("longest-processing-time-first over hierarchy.tick_cost (28 B per lease + 97 B per "
+                              "resource): every rank the same mix of size classes, the largest resources spread "
+                              "first" if partition == "lpt" else
+                              "contiguous resource-id ranges balanced by hierarchy.tick_cost"),
+           "ranks": per_rank}
+    if partition == "contiguous":
+        out["bounds"] = [int(x) for x in c2_bounds(world)]
+    return out
 
 
 def rehearse_c2_shards(torch, Engine, dev_index, args, world, ranks):
@@ -806,7 +830,7 @@ def rehearse_c2_shards(torch, Engine, dev_index, args, world, ranks):
     out = {"metric": "rehearsal: every rank's step of an N-GPU configs[2] node, one after another on one GPU "
                      "(not a bench line)", "steps": args.steps, "warmup": args.warmup,
            "workload": WORKLOADS["c2"] + f"; one snapshot sharded by resource id over {world} GPUs"}
-    out.update(shard_summary(world, per, args.steps) if len(per) == world else {"ranks": per})
+    out.update(shard_summary(world, per, args.steps, args.c2_partition) if len(per) == world else {"ranks": per})
     if len(per) == world:
         out["projected_node_leases_per_s"] = out["leases_total"] / (out["step_us_max"] * 1e-6)
     return out
@@ -823,7 +847,7 @@ def c2_sharded_line(torch, Engine, dev_index, args, world, rank, sync_ranks, dis
     out = {"workload": WORKLOADS["c2"] + f"; one snapshot sharded by resource id over {world} GPUs",
            "value": sum(r["leases"] for r in allr) * args.steps / t, "unit": "leases/s",
            "ms_per_step": t / args.steps * 1e3, "scaling": "strong"}
-    out.update(shard_summary(world, allr, args.steps))
+    out.update(shard_summary(world, allr, args.steps, args.c2_partition))
     return out
 
 
@@ -868,6 +892,9 @@ def main():
                          "copied in place of the RCCL all-gather -- and the root round), on the exchange's own stream "
                          "as at N > 1; prints the rank's step time (not a whole-node measurement)")
     ap.add_argument("--rehearse-rank", type=int, default=0)
+    ap.add_argument("--c2-partition", default="lpt", choices=C2_PARTITIONS,
+                    help="configs[2] over N GPUs: lpt (every rank the same mix of size classes) or contiguous "
+                         "resource-id ranges, both balanced by predicted tick bytes")
     ap.add_argument("--exchange", default="native", choices=["native", "python"],
                     help="native: each step is one library call (dm_hier_step: the leaf tick, then the block "
                          "gathered by the library's own RCCL communicator and the root round on the exchange "
@@ -1006,7 +1033,7 @@ def main():
     def measure(layout):
         """Load this rank's store (and root copy), run the timed steps; returns the run,
         the snapshot and the engines (closed by the caller)."""
-        snap = make_workload(args.workload, s_rank, s_world, layout)
+        snap = make_workload(args.workload, s_rank, s_world, layout, args.c2_partition)
         R = len(snap["seg_off"]) - 1
         eng = Engine(dev_index, args.lib)
         eng.load(snap)

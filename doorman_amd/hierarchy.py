@@ -83,6 +83,29 @@ def partition(seg_sizes, world: int, cost=None) -> np.ndarray:
     return np.asarray(bounds, dtype=np.int64)
 
 
+def assign_lpt(seg_sizes, world: int, cost=None) -> np.ndarray:
+    """Owner rank of every resource: longest-processing-time-first over the predicted
+    tick cost (tick_cost), i.e. each resource, costliest first, to the rank with the
+    least cost so far.  Unlike contiguous ranges every rank then holds the same mix of
+    size classes -- a shard of a Zipf population's tail is all tiles, of its head all
+    large chain, and the classes' kernels run at different rates per byte (the N = 8
+    contiguous shards of configs[2] measured 12-30 us per tick at equal bytes,
+    profiles/r06_c2_shard8_ranks_contiguous.json) -- and the largest resources spread
+    over the ranks first."""
+    import heapq
+    sizes = np.asarray(seg_sizes, dtype=np.int64)
+    c = tick_cost(sizes) if cost is None else np.asarray(cost, dtype=np.float64)
+    owner = np.zeros(len(sizes), dtype=np.int32)
+    if world <= 1:
+        return owner
+    heap = [(0.0, k) for k in range(world)]
+    for i in np.argsort(-c, kind="stable"):
+        load, k = heapq.heappop(heap)
+        owner[i] = k
+        heapq.heappush(heap, (load + float(c[i]), k))
+    return owner
+
+
 def shard(snap: dict, world: int, rank: int, cost=None) -> dict:
     """This rank's contiguous range of the snapshot's resources (partition)."""
     b = partition(np.diff(snap["seg_off"]), world, cost)

@@ -94,8 +94,10 @@ def subset(snap: dict, resources) -> dict:
     resources = np.asarray(resources, dtype=np.int64)
     so = snap["seg_off"]
     sizes = so[resources + 1] - so[resources]
-    rows = np.concatenate([np.arange(so[r], so[r + 1]) for r in resources]) if len(resources) else np.zeros(0, np.int64)
-    out = {"seg_off": np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)}
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    # every row of the listed resources, in order (vectorised: no per-resource arange)
+    rows = np.arange(int(starts[-1]), dtype=np.int64) + np.repeat(so[resources] - starts[:-1], sizes)
+    out = {"seg_off": starts}
     for k in ("wants", "has", "subclients", "expiry_ns"):
         out[k] = np.ascontiguousarray(snap[k][rows])
     for k in CFG_FIELDS:

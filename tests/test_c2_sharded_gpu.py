@@ -1,13 +1,13 @@
 """configs[2] sharded over two ranks: the one 1M-resource Zipf
-snapshot split by bench.c2_bounds (contiguous resource-id ranges balanced by predicted
-tick cost), one process per rank (gloo; both ranks on GPU 0, the rehearsal of a node),
+snapshot split by bench.c2_shard_ids (hierarchy.assign_lpt: each resource, costliest
+first, to the rank with the least predicted tick bytes so far), one process per rank (gloo; both ranks on GPU 0, the rehearsal of a node),
 each rank running bench.py's step -- back-to-back DM_ASYNC | DM_DEFER_JOIN writeback
 ticks on its own shard, no collective on the data path (resources are independent,
 server.go:810-815; algorithm.go:95-293 has no cross-resource term) -- and checking a
 sample of its resources from every size class against the oracle tick by tick
 (tests/test_c2_full_gpu.py's sample and host tick).  The ranks then exchange what they
-hold over gloo: the shards tile the snapshot exactly, each rank's range is the one
-bench.c2_bounds gives, and the predicted bytes are balanced."""
+hold over gloo: the shards tile the snapshot exactly, each rank's resources are the ones
+bench.c2_shard_ids gives, and the predicted bytes are balanced."""
 import os
 import socket
 import sys
@@ -96,14 +96,18 @@ def test_c2_sharded_two_ranks_against_the_oracle():
     allr = res[0]
     assert res[1] == allr  # both ranks saw the same exchange
     sizes = W.zipf_sizes()
-    b = bench.c2_bounds(world)
     full = W.c2(seed=2)
+    seen = np.zeros(len(sizes), np.int32)
     for g, r in enumerate(allr):
-        assert r["resources"] == b[g + 1] - b[g]
-        assert r["leases"] == int(sizes[b[g]:b[g + 1]].sum())
-        assert r["first_wants"] == float(full["wants"][full["seg_off"][b[g]]])  # the rank's range of ONE snapshot
+        ids = bench.c2_shard_ids(world, g)
+        seen[ids] += 1
+        assert r["resources"] == len(ids)
+        assert r["leases"] == int(sizes[ids].sum())
+        assert r["first_wants"] == float(full["wants"][full["seg_off"][ids[0]]])  # the rank's part of ONE snapshot
+    assert np.all(seen == 1)  # the shards tile the snapshot
     assert sum(r["leases"] for r in allr) == 13_970_034
     by = [r["bytes"] for r in allr]
     assert max(by) / (sum(by) / world) <= 1.10
-    # rank 0 holds the large resources (the speculative chain), rank 1 the Zipf tail (tiles)
-    assert allr[0]["kernels"].get("large_spec", 0) >= 3 and allr[1]["kernels"].get("small_tiles", 0) >= 3
+    # LPT: every rank holds every size class (the speculative chain, the sub-wave groups, the tiles)
+    for r in allr:
+        assert all(r["kernels"].get(k, 0) >= 3 for k in ("large_spec", "subs_merged", "small_tiles")), r["kernels"]

@@ -168,3 +168,20 @@ def test_uniform_range_shards_make_the_whole_store():
         bb = bench.c3_bounds(world)
         assert bb[0] == 0 and bb[-1] == bench.C3_R and np.all(np.diff(bb) > 0)
         assert np.diff(bb).max() - np.diff(bb).min() <= 1
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_lpt_assignment_on_configs2(world):
+    """configs[2]'s default multi-GPU split (bench.c2_shard_ids, hierarchy.assign_lpt):
+    every resource on exactly one rank, predicted tick bytes within 1 % of the mean, and
+    every rank holding resources of every size class (a contiguous split gives the head
+    ranks only the large chain and the tail ranks only tiles)."""
+    import bench
+    sizes = W.zipf_sizes(1_000_000, 1_000_000)
+    owner = H.assign_lpt(sizes, world)
+    by = np.bincount(owner, weights=H.tick_cost(sizes), minlength=world)
+    assert by.max() / by.mean() <= 1.01
+    for k in range(world):
+        mine = sizes[owner == k]
+        assert (mine > 4096).any() and ((mine >= 257) & (mine <= 4096)).any() and (mine <= 4).any()
+        np.testing.assert_array_equal(bench.c2_shard_ids(world, k), np.flatnonzero(owner == k))
