@@ -68,9 +68,9 @@ def c2_bounds(world: int, snap=None):
     resource), not by lease count -- a lease-count split leaves the 500k singletons'
     97-B records on the last shard (2.2x the mean bytes at N = 8)."""
     from doorman_amd import workloads as W
-    from doorman_amd.hierarchy import partition
+    from doorman_amd.hierarchy import partition, tick_time
     sizes = np.diff(snap["seg_off"]) if snap is not None else W.zipf_sizes()
-    return partition(sizes, world)
+    return partition(sizes, world, tick_time(sizes))
 
 
 C2_PARTITIONS = ("lpt", "contiguous")

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>  // types only: librccl is loaded when the first communicator is made
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -306,6 +307,24 @@ struct dm_ctx {
     }
     return hipSuccess;
   }
+  // Queue calibration (calib_step): which of the four auxiliary streams -- four hardware
+  // queues -- carries which work class moved configs[2]'s tick from 111 to 157 us over
+  // the 24 assignments (profiles/r05_queues.txt), and a queue's place in the process's
+  // creation order, which a host that made streams of its own first shifts, decides
+  // which assignment is best.  So the context times every assignment on its first
+  // forked writeback ticks (windows of kCalibWin ticks, each between joins of every
+  // class stream, HIP events on the context stream), times the best kCalibFinal again
+  // over longer windows, and keeps the fastest: aux[i] = aux_phys[perm[i]].
+  static constexpr int kCalibSkip = 16, kCalibWin = 6, kCalibFinal = 3, kCalibWin2 = 16;
+  int calib = 0;  // 0 pending, 1 round 1, 2 round 2, 3 waiting for the events, 4 done / off
+  int calib_skip = 0, calib_k = 0, calib_t = 0;
+  int perm[kAux] = {0, 1, 2, 3};
+  hipStream_t aux_phys[kAux] = {};
+  std::vector<std::array<int, kAux>> calib_cand;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> calib_ev;
+  std::vector<int> calib_of_ev;  // candidate timed by each window
+  std::vector<float> calib_ms;
+  int64_t calib_best = -1;  // the chosen permutation (perm[0] + 4 perm[1] + 16 perm[2] + 64 perm[3])
   // plan
   std::vector<Tile> h_tiles;  // small resources (n <= kSmallMax) in tiles (k_tile_small)
   std::vector<TileEntry> h_tile_list;  // the list tiles' resources
@@ -1025,7 +1044,7 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
 // ---------------------------------------------------------------------------
 extern "C" {
 
-const char* dm_version(void) { return "doorman-hip 0.4 (gfx950, abi 4)"; }
+const char* dm_version(void) { return "doorman-hip 0.5 (gfx950, abi 5)"; }
 
 int dm_device_count(int* out) {
   if (!out) return DM_E_INVAL;
@@ -1210,6 +1229,8 @@ struct RcclApi;
 static const RcclApi* rccl_api();
 static void rccl_destroy(const RcclApi* r, ncclComm_t comm);
 
+static void calib_free(dm_ctx* c);
+
 void dm_destroy(dm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
@@ -1225,6 +1246,7 @@ void dm_destroy(dm_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   c->collect_profile();
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  calib_free(c);
   c->free_all();
   give_aux(c);  // kept for the next context on this device (take_aux)
   for (int i = 0; i < dm_ctx::kAux; ++i)  // (a set not returned whole)
@@ -1477,6 +1499,113 @@ static int commit_templates(dm_ctx* c) {
   return DM_OK;
 }
 
+// One forked writeback tick's part in the queue calibration (dm_ctx::calib), called
+// before the tick forks.  Window boundaries join every class stream into the context
+// stream (so the next window's assignment starts after the last one's work: a class's
+// consecutive ticks on two streams are then still ordered) and record an event there.
+static hipError_t calib_apply(dm_ctx* c, const std::array<int, dm_ctx::kAux>& pm) {
+  hipError_t e = c->join_aux();
+  if (e != hipSuccess) return e;
+  for (int i = 0; i < dm_ctx::kAux; ++i) {
+    c->perm[i] = pm[(size_t)i];
+    c->aux[i] = c->aux_phys[pm[(size_t)i]];
+  }
+  c->main_dirty = true;  // the next tick forks: every class stream waits for the context stream
+  return hipSuccess;
+}
+
+static hipError_t calib_mark(dm_ctx* c, bool end) {
+  if (end) {
+    hipEvent_t ev;
+    hipError_t e = c->join_aux();
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+    if (e == hipSuccess) e = hipEventRecord(ev, c->stream);
+    if (e != hipSuccess) return e;
+    c->calib_ev.back().second = ev;
+    c->main_dirty = true;
+    return hipSuccess;
+  }
+  hipEvent_t ev;
+  hipError_t e = hipEventCreate(&ev);
+  if (e == hipSuccess) e = hipEventRecord(ev, c->stream);
+  if (e != hipSuccess) return e;
+  c->calib_ev.push_back({ev, nullptr});
+  c->calib_of_ev.push_back(c->calib_k);
+  return hipSuccess;
+}
+
+static void calib_free(dm_ctx* c) {
+  for (auto& pr : c->calib_ev) {
+    if (pr.first) (void)hipEventDestroy(pr.first);
+    if (pr.second) (void)hipEventDestroy(pr.second);
+  }
+  c->calib_ev.clear();
+  c->calib_of_ev.clear();
+}
+
+static hipError_t calib_step(dm_ctx* c) {
+  if (c->calib == 4) return hipSuccess;
+  if (c->calib == 0) {
+    if (!c->aux_own_queue) {  // shared queues: the assignment does not choose hardware queues
+      c->calib = 4;
+      return hipSuccess;
+    }
+    if (++c->calib_skip < dm_ctx::kCalibSkip) return hipSuccess;
+    for (int i = 0; i < dm_ctx::kAux; ++i) c->aux_phys[i] = c->aux[i];
+    std::array<int, dm_ctx::kAux> pm{0, 1, 2, 3};
+    c->calib_cand.clear();
+    do c->calib_cand.push_back(pm);
+    while (std::next_permutation(pm.begin(), pm.end()));
+    c->calib = 1;
+    c->calib_k = 0;
+    c->calib_t = 1;  // this tick is the window's first
+    hipError_t e = calib_apply(c, c->calib_cand[0]);
+    return e == hipSuccess ? calib_mark(c, false) : e;
+  }
+  if (c->calib == 1 || c->calib == 2) {
+    const int win = c->calib == 1 ? dm_ctx::kCalibWin : dm_ctx::kCalibWin2;
+    if (++c->calib_t <= win) return hipSuccess;
+    hipError_t e = calib_mark(c, true);
+    if (e != hipSuccess) return e;
+    c->calib_t = 1;
+    const int ncand = c->calib == 1 ? (int)c->calib_cand.size() : dm_ctx::kCalibFinal;
+    if (++c->calib_k < ncand) {
+      e = calib_apply(c, c->calib_cand[(size_t)c->calib_k]);
+      return e == hipSuccess ? calib_mark(c, false) : e;
+    }
+    c->calib = 3;  // wait for the windows' events (polled by later ticks)
+    return hipSuccess;
+  }
+  // calib == 3: the last window's end event done?  then pick
+  const hipError_t q = hipEventQuery(c->calib_ev.back().second);
+  if (q == hipErrorNotReady) return hipSuccess;
+  if (q != hipSuccess) return q;
+  std::vector<std::pair<float, size_t>> t;
+  for (size_t w = 0; w < c->calib_ev.size(); ++w) {
+    float ms = 0.0f;
+    hipError_t e = hipEventElapsedTime(&ms, c->calib_ev[w].first, c->calib_ev[w].second);
+    if (e != hipSuccess) return e;
+    t.push_back({ms, w});
+  }
+  std::sort(t.begin(), t.end());
+  if (c->calib_cand.size() > (size_t)dm_ctx::kCalibFinal) {  // round 2: the best of round 1 over longer windows
+    std::vector<std::array<int, dm_ctx::kAux>> fin;
+    for (int i = 0; i < dm_ctx::kCalibFinal; ++i) fin.push_back(c->calib_cand[(size_t)c->calib_of_ev[t[(size_t)i].second]]);
+    calib_free(c);
+    c->calib_cand = fin;
+    c->calib = 2;
+    c->calib_k = 0;
+    c->calib_t = 1;
+    hipError_t e = calib_apply(c, c->calib_cand[0]);
+    return e == hipSuccess ? calib_mark(c, false) : e;
+  }
+  const std::array<int, dm_ctx::kAux> best = c->calib_cand[(size_t)c->calib_of_ev[t[0].second]];
+  calib_free(c);
+  c->calib = 4;
+  c->calib_best = best[0] + 4 * best[1] + 16 * best[2] + 64 * best[3];
+  return calib_apply(c, best);
+}
+
 int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   DM_CHECK_CTX(c);
   int rc = ready(c);
@@ -1584,6 +1713,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   bool parts_only = false;
   for (int b = 0; b < kNumBins; ++b) parts_only |= !c->h_bins[b].empty() && c->bin_parts[b] > 1;
   const bool one_class = (!fork || parts_only) && nch == 0 && c->h_tiles.empty() && !general && nonempty_bins == 1;
+  if (fork && wb && c->tick_signal_wanted == false) DM_HIP(c, calib_step(c), "queue calibration");
   auto cls_stream = [&](int cls) { return fork ? c->aux[c->class_stream[cls]] : st; };
   hipStream_t s_large = cls_stream(kNumBins + 1), s_small = cls_stream(kNumBins);
   if (!fork) {  // everything on the context stream, after any deferred class work
@@ -2922,7 +3052,7 @@ int dm_reset_kernel_times(dm_ctx* c) {
 
 int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   if (!c || !out) return DM_E_INVAL;
-  int64_t v[9 + kNumBins];
+  int64_t v[10 + kNumBins];
   v[0] = (int64_t)c->h_tiles.size();
   for (int b = 0; b < kNumBins; ++b) v[1 + b] = (int64_t)c->h_bins[b].size();
   v[1 + kNumBins] = (int64_t)c->h_large.size();
@@ -2935,7 +3065,10 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   int64_t parts = 1;  // the stream parts of the store's one workgroup bin (dm_ctx::kParts), else 1
   for (int b = 0; b < kNumBins; ++b) parts = std::max<int64_t>(parts, c->bin_parts[b]);
   v[8 + kNumBins] = parts;
-  const int n = 9 + kNumBins;
+  // the class streams' queue assignment the calibration chose (dm_ctx::calib): perm[0] +
+  // 4 perm[1] + 16 perm[2] + 64 perm[3], or -1 before it has finished (or with shared queues)
+  v[9 + kNumBins] = c->calib_best;
+  const int n = 10 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
 }

@@ -17,7 +17,7 @@ from .workloads import CFG_FIELDS
 
 _BIN_NAMES = ("small_tiles", "sub16x4", "sub32x4", "wave64x4", "block128x4", "block128x8", "block256x8",
               "block2k4k", "sub8x2", "sub16x2", "large_resources", "large_chunks", "leases", "bin_shapes",
-              "redo_resident_cap", "spec_fits", "aux_own_queues", "stream_parts")
+              "redo_resident_cap", "spec_fits", "aux_own_queues", "stream_parts", "queue_perm")
 
 
 def _ptr(a):

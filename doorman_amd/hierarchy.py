@@ -55,6 +55,28 @@ def tick_cost(seg_sizes) -> np.ndarray:
     return LEASE_COST_B * sizes + RESOURCE_COST_B
 
 
+# Tick time per byte of each size class of a resource-id shard of configs[2], fitted
+# (non-negative least squares, with a fixed ~10 us per tick) to every rank's rehearsed
+# step of the contiguous N = 2 / 4 / 8 shards on one MI355X (profiles/r06_c2_shard*_ranks
+# _contiguous.json): a shard's classes share the GPU's workgroup slots rather than only
+# its HBM, so a class that is latency-bound per byte (the tiles of 2-4-row resources
+# with the sub-wave groups of the 5-6-row ones beside them) costs several times what
+# the bytes say.  (upper size of the class, us per MB of tick_cost)
+C2_CLASS_US_PER_MB = ((1, 0.087), (4, 0.469), (16, 0.072), (256, 0.195), (4096, 0.150), (1 << 62, 0.250))
+
+
+def tick_time(seg_sizes) -> np.ndarray:
+    """Predicted tick time of each resource of a shard (us): tick_cost weighted by its
+    size class's measured rate (C2_CLASS_US_PER_MB)."""
+    sizes = np.asarray(seg_sizes, dtype=np.int64)
+    w = np.zeros(len(sizes))
+    lo = 0
+    for hi, us in C2_CLASS_US_PER_MB:
+        w[(sizes > lo) & (sizes <= hi)] = us
+        lo = hi
+    return tick_cost(sizes) * w / 1e6
+
+
 def partition(seg_sizes, world: int, cost=None) -> np.ndarray:
     """Contiguous resource ranges balanced by predicted tick cost (tick_cost, or the
     given per-resource cost): boundaries b[0..world] with shard k = resources

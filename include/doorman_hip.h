@@ -38,13 +38,15 @@
 extern "C" {
 #endif
 
-/* 4 (round 5): dm_kernel_class_names, dm_hier_comm_info; dm_plan_info's slot 14 is the
+/* 5 (round 6): dm_plan_info's slot 18 is the class streams' hardware-queue assignment the
+   context's queue calibration chose (-1 before it finished); returns 19.
+   4 (round 5): dm_kernel_class_names, dm_hier_comm_info; dm_plan_info's slot 14 is the
    redo's co-resident workgroup bound (was the per-chunk redo's chunk bound), slot 15
    always 1, slot 16 the aux queues flag, slot 17 the stream parts; a published block's
    record 0 holds two 32-bit flags words (their OR is the request's flags); the DM_*
    environment switches other than the test hooks are gone.  3 (round 4): dm_hier_attach / dm_hier_step / dm_rccl_unique_id /
    dm_hier_comm_init and DM_E_INTERNAL added, dm_set_large_path and DM_LARGE_* removed. */
-#define DM_ABI_VERSION 4
+#define DM_ABI_VERSION 5
 
 /* return codes */
 #define DM_OK 0
@@ -391,7 +393,10 @@ int dm_reset_kernel_times(dm_ctx* ctx);
  * speculate: the redo by teams needs only 64 co-resident workgroups), and 1 when the
  * work classes' auxiliary streams each have a hardware queue of their own, and the
  * stream parts of the store's one workgroup bin (2: its halves run on two auxiliary
- * streams, unjoined from tick to tick; else 1); returns 18 */
+ * streams, unjoined from tick to tick; else 1), and the queue assignment the context chose
+ * for its class streams (perm[0] + 4 perm[1] + 16 perm[2] + 64 perm[3]: class stream i
+ * runs on the i-th auxiliary queue's perm[i]-th creation; timed on the context's first
+ * forked writeback ticks, -1 until then); returns 19 */
 int dm_plan_info(dm_ctx* ctx, int64_t* out, int max);
 /* row-state summary of the device store (synchronous): dense resources (every row a
  * live follower with one subclient count: a tick reads 24 B per lease, not 28),

@@ -38,8 +38,11 @@ def test_partition_balances_predicted_bytes_on_configs2(world):
     by_old = np.add.reduceat(28.0 * sizes + 97.0, leases_only[:-1])
     if world == 8:
         assert by_old.max() / by_old.mean() > 2.0
-    import bench
-    np.testing.assert_array_equal(bench.c2_bounds(world), b)
+    import bench  # the contiguous option weights the bytes by each size class's measured rate
+    tb = bench.c2_bounds(world)
+    np.testing.assert_array_equal(tb, H.partition(sizes, world, H.tick_time(sizes)))
+    pt = np.add.reduceat(H.tick_time(sizes), tb[:-1])
+    assert pt.max() / pt.mean() <= 1.05, pt
 
 
 def test_subset_range_is_subset():
