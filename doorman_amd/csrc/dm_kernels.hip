@@ -1673,7 +1673,11 @@ __global__ __launch_bounds__(256, kLight ? 8 : 1) void k_large_redo_team(DevPara
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next tick's slots (its k_large_spec runs after this)
     S.ring[q] = 0;
     S.ring[2 + q] = 0;
-    __hip_atomic_store(S.seen, S.ring[S.par], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // tell the host only that a redo ran (it clears the word when it reads it): a
+    // system-scope store to host memory keeps an otherwise empty launch alive ~2 us
+    // longer, and the steady tick's empty redo is on the large chain's critical path
+    const uint32_t marked = S.ring[S.par];
+    if (marked) __hip_atomic_store(S.seen, marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!S.ring[S.par]) return;  // nothing marked (k_large_spec: the previous launch)
   for (;;) {

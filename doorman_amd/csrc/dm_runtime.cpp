@@ -1189,6 +1189,8 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
   if (const char* sc = getenv("DM_SPEC_CHAIN")) c->spec_chain = atoi(sc) != 0;
   if (const char* rl = getenv("DM_REDO_LIGHT")) c->redo_light = atoi(rl);
+  if (const char* qc = getenv("DM_QUEUE_CALIB"))  // 0: keep the creation-order queue assignment
+    if (atoi(qc) == 0) c->calib = 4;
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1767,7 +1769,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
                        reinterpret_cast<uint32_t*>(c->d_serr + 1), c->p_team.p, c->nslots};
       c->spec_seq += 1;
       const bool light = c->redo_light == 2 || (c->redo_light == 1 && c->redo_epoch == c->row_epoch &&
-                                                __atomic_load_n(c->h_serr + 1, __ATOMIC_RELAXED) == 0);
+                                                __atomic_exchange_n(c->h_serr + 1, 0, __ATOMIC_RELAXED) == 0);
       c->redo_epoch = c->row_epoch;
       const int redo_phase = light ? 2 : 1;
       const int redo_grid = light ? c->team_grid_light : c->team_grid_full;
