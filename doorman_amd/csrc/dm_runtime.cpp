@@ -315,15 +315,18 @@ struct dm_ctx {
   // forked writeback ticks (windows of kCalibWin ticks, each between joins of every
   // class stream, HIP events on the context stream), times the best kCalibFinal again
   // over longer windows, and keeps the fastest: aux[i] = aux_phys[perm[i]].
-  static constexpr int kCalibSkip = 16, kCalibWin = 6, kCalibFinal = 3, kCalibWin2 = 16;
+  // (the skip: a context's first ticks run slow -- first-touch, clocks -- and would bias
+  // the candidates timed first)
+  static constexpr int kCalibSkip = 64, kCalibWin = 6, kCalibFinal = 3, kCalibWin2 = 16;
   int calib = 0;  // 0 pending, 1 round 1, 2 round 2, 3 waiting for the events, 4 done / off
-  int calib_skip = 0, calib_k = 0, calib_t = 0;
+  int calib_skip = 0, calib_k = 0, calib_t = 0, calib_round = 0;
   int perm[kAux] = {0, 1, 2, 3};
   hipStream_t aux_phys[kAux] = {};
   std::vector<std::array<int, kAux>> calib_cand;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> calib_ev;
   std::vector<int> calib_of_ev;  // candidate timed by each window
   std::vector<float> calib_ms;
+  bool calib_log = false;
   int64_t calib_best = -1;  // the chosen permutation (perm[0] + 4 perm[1] + 16 perm[2] + 64 perm[3])
   // plan
   std::vector<Tile> h_tiles;  // small resources (n <= kSmallMax) in tiles (k_tile_small)
@@ -1189,8 +1192,10 @@ int dm_create(int device, dm_ctx** out) {
   if (const char* df = getenv("DM_DECIDE_FAST")) c->decide_fast = atoi(df) != 0;
   if (const char* sc = getenv("DM_SPEC_CHAIN")) c->spec_chain = atoi(sc) != 0;
   if (const char* rl = getenv("DM_REDO_LIGHT")) c->redo_light = atoi(rl);
-  if (const char* qc = getenv("DM_QUEUE_CALIB"))  // 0: keep the creation-order queue assignment
+  if (const char* qc = getenv("DM_QUEUE_CALIB")) {  // 0: keep the creation-order queue assignment; 2: log
     if (atoi(qc) == 0) c->calib = 4;
+    c->calib_log = atoi(qc) == 2;
+  }
   if (const char* ds = getenv("DM_DENSE_SPLIT")) {
     const int v = (int)strtol(ds, nullptr, 0);
     c->dense_split = v == 1 ? 0xF : (v & 0xF);
@@ -1559,6 +1564,7 @@ static hipError_t calib_step(dm_ctx* c) {
     do c->calib_cand.push_back(pm);
     while (std::next_permutation(pm.begin(), pm.end()));
     c->calib = 1;
+    c->calib_round = 1;
     c->calib_k = 0;
     c->calib_t = 1;  // this tick is the window's first
     hipError_t e = calib_apply(c, c->calib_cand[0]);
@@ -1570,7 +1576,7 @@ static hipError_t calib_step(dm_ctx* c) {
     hipError_t e = calib_mark(c, true);
     if (e != hipSuccess) return e;
     c->calib_t = 1;
-    const int ncand = c->calib == 1 ? (int)c->calib_cand.size() : dm_ctx::kCalibFinal;
+    const int ncand = (int)c->calib_cand.size();
     if (++c->calib_k < ncand) {
       e = calib_apply(c, c->calib_cand[(size_t)c->calib_k]);
       return e == hipSuccess ? calib_mark(c, false) : e;
@@ -1589,13 +1595,26 @@ static hipError_t calib_step(dm_ctx* c) {
     if (e != hipSuccess) return e;
     t.push_back({ms, w});
   }
+  if (c->calib_log) {  // test hook (DM_QUEUE_CALIB=2): every window's assignment and time per tick
+    const int win = c->calib_round == 1 ? dm_ctx::kCalibWin : dm_ctx::kCalibWin2;
+    for (const auto& pr : t) {
+      const auto& pm = c->calib_cand[(size_t)c->calib_of_ev[pr.second]];
+      fprintf(stderr, "[dm queue calibration] round %d perm %d%d%d%d %.2f us/tick\n", win == dm_ctx::kCalibWin ? 1 : 2,
+              pm[0], pm[1], pm[2], pm[3], 1000.0 * pr.first / win);
+    }
+  }
   std::sort(t.begin(), t.end());
-  if (c->calib_cand.size() > (size_t)dm_ctx::kCalibFinal) {  // round 2: the best of round 1 over longer windows
+  if (c->calib == 3 && c->calib_round == 1) {  // round 2: the best of round 1 over longer windows
+    // the best kCalibFinal of round 1, and the creation-order assignment (the measured
+    // default) so that the choice is never worse than not calibrating
     std::vector<std::array<int, dm_ctx::kAux>> fin;
+    const std::array<int, dm_ctx::kAux> ident{0, 1, 2, 3};
     for (int i = 0; i < dm_ctx::kCalibFinal; ++i) fin.push_back(c->calib_cand[(size_t)c->calib_of_ev[t[(size_t)i].second]]);
+    if (std::find(fin.begin(), fin.end(), ident) == fin.end()) fin.push_back(ident);
     calib_free(c);
     c->calib_cand = fin;
     c->calib = 2;
+    c->calib_round = 2;
     c->calib_k = 0;
     c->calib_t = 1;
     hipError_t e = calib_apply(c, c->calib_cand[0]);

@@ -70,3 +70,24 @@ def test_the_process_exits_cleanly_with_pooled_streams():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
     assert "done" in r.stdout
+
+
+def test_c2_tick_does_not_depend_on_streams_created_before_the_context():
+    """a host that embeds the library (a cgo server) owns streams of its
+    own.  configs[2]'s tick, in a process that first created 0, 1, 2 or 3 torch streams and
+    used them, stays within 5 % of the clean process: each context times every assignment
+    of its work classes to its four hardware queues on its first forked ticks and keeps
+    the fastest (dm_plan_info queue_perm; the 24 assignments span 113-244 us per tick of
+    calibration window, profiles/r06_queue_robustness.txt).  One process per case, one
+    after another (tools/queue_probe.py)."""
+    import json
+    us = {}
+    for k in (0, 1, 2, 3):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "queue_probe.py"), str(k), "torch", "600"],
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, (k, r.stderr[-2000:])
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        assert line["calibrated_perm"] is not None and line["calibrated_perm"] >= 0, line
+        us[k] = line["us"]
+    for k in (1, 2, 3):
+        assert abs(us[k] / us[0] - 1.0) <= 0.05, us
