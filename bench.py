@@ -73,22 +73,27 @@ def c2_bounds(world: int, snap=None):
     return partition(sizes, world, tick_time(sizes))
 
 
-C2_PARTITIONS = ("lpt", "contiguous")
+C2_PARTITIONS = ("classes", "lpt", "contiguous")
+_OWNERS = {}
 
 
-def c2_shard_ids(world: int, rank: int, partition: str = "lpt", snap=None) -> np.ndarray:
-    """configs[2]'s resource ids of one rank: lpt (default) -- hierarchy.assign_lpt, every
-    rank the same mix of size classes; contiguous -- c2_bounds' range."""
+def c2_shard_ids(world: int, rank: int, partition: str = "classes", snap=None) -> np.ndarray:
+    """configs[2]'s resource ids of one rank: classes (default) -- hierarchy.assign_by_class,
+    every rank 1/N of every size class and the mean bytes; lpt -- hierarchy.assign_lpt
+    over all resources at once; contiguous -- c2_bounds' range."""
     from doorman_amd import workloads as W
-    from doorman_amd.hierarchy import assign_lpt
+    from doorman_amd.hierarchy import assign_by_class, assign_lpt
     sizes = np.diff(snap["seg_off"]) if snap is not None else W.zipf_sizes()
     if partition == "contiguous":
         b = c2_bounds(world, snap)
         return np.arange(int(b[rank]), int(b[rank + 1]), dtype=np.int64)
-    return np.flatnonzero(assign_lpt(sizes, world) == rank).astype(np.int64)
+    key = (partition, world, len(sizes), int(sizes.sum()))
+    if key not in _OWNERS:
+        _OWNERS[key] = (assign_lpt if partition == "lpt" else assign_by_class)(sizes, world)
+    return np.flatnonzero(_OWNERS[key] == rank).astype(np.int64)
 
 
-def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicated", partition: str = "lpt"):
+def make_workload(name: str, rank: int, world: int = 1, layout: str = "replicated", partition: str = "classes"):
     from doorman_amd import workloads as W
     if name == "c1":
         return W.c1(seed=1 + 1000 * rank, kind=W.FAIR_SHARE)
@@ -812,10 +817,11 @@ def shard_summary(world, per_rank, steps, partition):
            "step_us_max": max(t), "step_us_min": min(t), "step_max_over_min": round(max(t) / min(t), 4),
            "predicted_bytes_max_over_mean": round(max(pb) / (sum(pb) / len(pb)), 4),
            "partition": partition,
-           "partition_note": ("longest-processing-time-first over hierarchy.tick_cost (28 B per lease + 97 B per "
-                              "resource): every rank the same mix of size classes, the largest resources spread "
-                              "first" if partition == "lpt" else
-                              "contiguous resource-id ranges balanced by hierarchy.tick_cost"),
+           "partition_note": {"classes": "hierarchy.assign_by_class: within every size class longest-processing-"
+                                         "time-first over hierarchy.tick_cost (28 B per lease + 97 B per resource), "
+                                         "then the smallest resources move until every rank holds the mean bytes",
+                              "lpt": "hierarchy.assign_lpt: longest-processing-time-first over all resources",
+                              "contiguous": "contiguous resource-id ranges balanced by hierarchy.tick_time"}[partition],
            "ranks": per_rank}
     if partition == "contiguous":
         out["bounds"] = [int(x) for x in c2_bounds(world)]
@@ -892,9 +898,10 @@ def main():
                          "copied in place of the RCCL all-gather -- and the root round), on the exchange's own stream "
                          "as at N > 1; prints the rank's step time (not a whole-node measurement)")
     ap.add_argument("--rehearse-rank", type=int, default=0)
-    ap.add_argument("--c2-partition", default="lpt", choices=C2_PARTITIONS,
-                    help="configs[2] over N GPUs: lpt (every rank the same mix of size classes) or contiguous "
-                         "resource-id ranges, both balanced by predicted tick bytes")
+    ap.add_argument("--c2-partition", default="classes", choices=C2_PARTITIONS,
+                    help="configs[2] over N GPUs: classes (every rank 1/N of every size class, bytes balanced), lpt "
+                         "(longest-processing-time-first over all resources) or contiguous resource-id ranges "
+                         "(weighted by the classes' measured rates)")
     ap.add_argument("--exchange", default="native", choices=["native", "python"],
                     help="native: each step is one library call (dm_hier_step: the leaf tick, then the block "
                          "gathered by the library's own RCCL communicator and the root round on the exchange "

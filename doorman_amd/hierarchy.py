@@ -128,6 +128,53 @@ def assign_lpt(seg_sizes, world: int, cost=None) -> np.ndarray:
     return owner
 
 
+# The size classes of a tick: tiles, the sub-wave launch, the four
+# workgroup bins, the large chain.  (first, last row count)
+SIZE_CLASSES = ((1, 4), (5, 256), (257, 512), (513, 1024), (1025, 2048), (2049, 4096), (4097, 1 << 62))
+
+
+def assign_by_class(seg_sizes, world: int, cost=None) -> np.ndarray:
+    """Owner rank of every resource, balanced class by class: within each size class
+    (SIZE_CLASSES, the largest first) longest-processing-time-first over tick_cost from
+    empty ranks, so every rank runs every class the store has with 1/N of its work (a
+    global LPT leaves the rank that took the largest resource without whole classes,
+    and a shard's tick is set by the classes it runs -- each a latency-bound launch at
+    a shard's size -- as much as by its bytes: profiles/r06_c2_shard8_ranks_lpt.json);
+    then the smallest resources (the tiles' class, 125 B each) move from ranks above
+    the mean predicted bytes to ranks below it, so the bytes balance too (the one
+    resource larger than a rank's share of its class, configs[2]'s 1M-row head, stays
+    on its rank)."""
+    import heapq
+    sizes = np.asarray(seg_sizes, dtype=np.int64)
+    c = tick_cost(sizes) if cost is None else np.asarray(cost, dtype=np.float64)
+    owner = np.zeros(len(sizes), dtype=np.int32)
+    if world <= 1:
+        return owner
+    for lo, hi in SIZE_CLASSES[::-1]:
+        ids = np.flatnonzero((sizes >= lo) & (sizes <= hi))
+        heap = [(0.0, k) for k in range(world)]
+        for i in ids[np.argsort(-c[ids], kind="stable")]:
+            load, k = heapq.heappop(heap)
+            owner[i] = k
+            heapq.heappush(heap, (load + float(c[i]), k))
+    load = np.bincount(owner, weights=c, minlength=world)
+    target = load.mean()
+    small = np.flatnonzero(sizes <= SIZE_CLASSES[0][1])[::-1]  # the smallest first (the Zipf tail's end)
+    for k in np.argsort(-load):
+        if load[k] <= target:
+            break
+        for r in small[owner[small] == k]:
+            if load[k] <= target * 1.002:
+                break
+            d = int(np.argmin(load))
+            if load[d] + c[r] > target:
+                break
+            owner[r] = d
+            load[k] -= c[r]
+            load[d] += c[r]
+    return owner
+
+
 def shard(snap: dict, world: int, rank: int, cost=None) -> dict:
     """This rank's contiguous range of the snapshot's resources (partition)."""
     b = partition(np.diff(snap["seg_off"]), world, cost)

@@ -1,6 +1,6 @@
 """configs[2] sharded over two ranks: the one 1M-resource Zipf
-snapshot split by bench.c2_shard_ids (hierarchy.assign_lpt: each resource, costliest
-first, to the rank with the least predicted tick bytes so far), one process per rank (gloo; both ranks on GPU 0, the rehearsal of a node),
+snapshot split by bench.c2_shard_ids (hierarchy.assign_by_class: every rank 1/N of every
+size class and the mean predicted tick bytes), one process per rank (gloo; both ranks on GPU 0, the rehearsal of a node),
 each rank running bench.py's step -- back-to-back DM_ASYNC | DM_DEFER_JOIN writeback
 ticks on its own shard, no collective on the data path (resources are independent,
 server.go:810-815; algorithm.go:95-293 has no cross-resource term) -- and checking a
@@ -108,6 +108,6 @@ def test_c2_sharded_two_ranks_against_the_oracle():
     assert sum(r["leases"] for r in allr) == 13_970_034
     by = [r["bytes"] for r in allr]
     assert max(by) / (sum(by) / world) <= 1.10
-    # LPT: every rank holds every size class (the speculative chain, the sub-wave groups, the tiles)
+    # by class: every rank holds every size class (the speculative chain, the sub-wave groups, the tiles)
     for r in allr:
         assert all(r["kernels"].get(k, 0) >= 3 for k in ("large_spec", "subs_merged", "small_tiles")), r["kernels"]

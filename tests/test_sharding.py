@@ -175,9 +175,9 @@ def test_uniform_range_shards_make_the_whole_store():
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_lpt_assignment_on_configs2(world):
-    """configs[2]'s default multi-GPU split (bench.c2_shard_ids, hierarchy.assign_lpt):
-    every resource on exactly one rank, predicted tick bytes within 1 % of the mean, and
-    every rank holding resources of every size class (a contiguous split gives the head
+    """configs[2]'s "lpt" split (bench.c2_shard_ids, hierarchy.assign_lpt): every resource on
+    exactly one rank, predicted tick bytes within 1 % of the mean, and every rank holding
+    resources of the large, workgroup and tile classes (a contiguous split gives the head
     ranks only the large chain and the tail ranks only tiles)."""
     import bench
     sizes = W.zipf_sizes(1_000_000, 1_000_000)
@@ -187,4 +187,26 @@ def test_lpt_assignment_on_configs2(world):
     for k in range(world):
         mine = sizes[owner == k]
         assert (mine > 4096).any() and ((mine >= 257) & (mine <= 4096)).any() and (mine <= 4).any()
+        np.testing.assert_array_equal(bench.c2_shard_ids(world, k, "lpt"), np.flatnonzero(owner == k))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_by_class_assignment_on_configs2(world):
+    """configs[2]'s default multi-GPU split (bench.c2_shard_ids "classes",
+    hierarchy.assign_by_class): every resource on one rank, every rank 1/N of every size
+    class (within one resource of the class's largest), predicted tick bytes within 1 %
+    of the mean (<= 1.10; a lease-count split: 2.20 at N = 8)."""
+    import bench
+    sizes = W.zipf_sizes(1_000_000, 1_000_000)
+    owner = H.assign_by_class(sizes, world)
+    cost = H.tick_cost(sizes)
+    by = np.bincount(owner, weights=cost, minlength=world)
+    assert by.max() / by.mean() <= 1.01, by
+    for lo, hi in H.SIZE_CLASSES[1:]:  # (the tiles' class also carries the byte rebalance)
+        m = (sizes >= lo) & (sizes <= hi)
+        if not m.any():
+            continue
+        share = np.bincount(owner[m], weights=cost[m], minlength=world)
+        assert share.max() - share.min() <= cost[m].max() + 1e-6, (lo, hi, share)
+    for k in range(world):
         np.testing.assert_array_equal(bench.c2_shard_ids(world, k), np.flatnonzero(owner == k))
