@@ -809,7 +809,7 @@ static hipError_t check_dense(dm_ctx* c, int i, int b, int j, hipStream_t s) {
 // (a resource-id shard of a Zipf population: the head shards hold the large and
 // workgroup classes, the tail shards the small ones) would then run classes one after
 // another on a shared stream while another stream idles: the N = 8 shard of bins 3-6
-// ran 36.6 us against 24-26 for its neighbours (profiles/r06_c2_shard8_ranks_contiguous.json).
+// ran 36.6 us against 24-26 for its neighbours (profiles/r06_c2_shard8_ranks_contiguous_before_stream_plan.json).
 // So, while some stream holds no unit of this store, the largest unit (by rows and
 // records) of a stream holding several moves to it.
 static void plan_streams(dm_ctx* c) {
