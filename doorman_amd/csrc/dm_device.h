@@ -324,6 +324,51 @@ template <> struct RelMask<16> { using T = uint16_t; };
 // in every workgroup bin (n > G * R / 2, R >= 4)
 constexpr int64_t rel_mask_offset(int64_t lo) { return (lo >> 3) << 2; }
 
+// A dense resource stays dense through store updates (round 6, configs[4]'s rounds):
+// a release marks its row in the released-row mask (rmask) and the work item's hint
+// (bit 24, "has released rows") instead of ending the dense state, and an arrival onto
+// one of its rows -- the resource's subclient count, the expiry Assign gives (now +
+// lease length) at or after the followers' -- clears the row's released bit and sets
+// it in the arrival mask (amask) and the item's bit 25 instead of marking the resource
+// explicit.  The tick then reads neither the subclients nor the expiry column for it:
+// arrival rows are live followers unless the followers themselves have lapsed, when
+// the resource takes the column path (the arrivals' own expiries decide); a writeback
+// tick turns the arrivals into followers and clears the arrival mask.
+// Both masks live in the resource's rmask bytes (rel_mask_offset): lane t's entry of
+// R bits (bit k: row k * G + t), RelMask<R> wide; the arrival entry shares the byte
+// (high nibble) for R <= 4, else follows the G released-row entries.
+struct MaskPos {
+  int32_t roff, rbit;  // released-row mask: byte offset from the resource's first mask byte, bit
+  int32_t aoff, abit;  // arrival mask
+};
+__host__ __device__ inline MaskPos mask_pos(int G, int R, int i) {
+  const int t = i % G, k = i / G, es = R <= 8 ? 1 : 2;
+  MaskPos m;
+  m.roff = t * es + (k >> 3);
+  m.rbit = k & 7;
+  if (R <= 4) {
+    m.aoff = m.roff;
+    m.abit = m.rbit + 4;
+  } else {
+    m.aoff = G * es + t * es + (k >> 3);
+    m.abit = k & 7;
+  }
+  return m;
+}
+// What the update kernels need for it: the resource's work item (bins 3-6) and the
+// bins' shapes (G x R: bin 3 128 x 4, bin 4 128 x 8 or 64 x 16, bin 5 256 x 8, bin 6
+// 256 x 16 or 512 x 8).
+struct DenseUpd {
+  const int32_t* item_of;  // [R]: bin << 24 | the item's index in its bin, -1 outside bins 3-6
+  WorkItem* bins[4];
+  int32_t bin4_wave, bin6_wide;
+  uint8_t* rmask;
+};
+__host__ __device__ inline void bin_shape(int bin, int bin4_wave, int bin6_wide, int* G, int* R) {
+  *G = bin == 3 ? 128 : bin == 4 ? (bin4_wave ? 64 : 128) : bin == 5 ? 256 : (bin6_wide ? 512 : 256);
+  *R = bin == 3 ? 4 : bin == 4 ? (bin4_wave ? 16 : 8) : bin == 5 ? 8 : (bin6_wide ? 8 : 16);
+}
+
 struct ReqItem {
   int32_t seg;
   int32_t fast;  // 1 + its slot of the fast path (FastItem), 0: decided by k_decide only

@@ -80,10 +80,15 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // its hint word carries "has released rows" (bit 8) and the tick that set it wrote
   // which rows they are, one mask entry of R bits per lane (RelMask), read here in
   // place of the column: 1-2 B per lane instead of 4 B per row.
-  const int hw = kDense ? wi.n >> 16 : 0;  // hint word: s0 in bits 0-7, released rows in bit 8
+  const int hw = kDense ? wi.n >> 16 : 0;  // hint word: s0 in bits 0-7, released rows in bit 8, arrivals in bit 9
   const int hint = (kHintLoad) ? hw & 0xFF : 0;
   using MaskT = typename RelMask<R>::T;
   MaskT* const mrow = reinterpret_cast<MaskT*>(p.rmask + rel_mask_offset(lo));
+  // rows upserted since the dense state was set (dm_device.h mask_pos): the high nibble
+  // of the released-row entry for R <= 4, else G entries after the released-row ones
+  constexpr unsigned kRowBits = R >= 32 ? ~0u : (1u << R) - 1u;
+  const bool arrivals = kDense && ((hw >> 9) & 1);
+  unsigned arrm = 0;
   if (MODE != kDenseOnly && !hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -95,7 +100,8 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       sr[k] = *col_at(sb, u);
     }
   } else {
-    if (hw >> 8 & 1) relm = mrow[t];
+    if (hw >> 8 & 1) relm = (unsigned)mrow[t] & kRowBits;
+    if (arrivals) arrm = R <= 4 ? ((unsigned)mrow[t] >> 4) & kRowBits : (unsigned)mrow[G + t];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -106,8 +112,11 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     }
   }
   const Res rs = load_res(p, seg);
+  // arrivals outlive the followers (at or after follow_exp): only a tick past follow_exp
+  // needs their own expiries, from the columns
+  const bool arr_lapse = arrivals && p.now > rs.follow_exp;
   if constexpr (MODE == kDenseOnly) {
-    if (dense_subclients(rs) != hint) {  // stale hint: k_block_rest reads the column
+    if (dense_subclients(rs) != hint || arr_lapse) {  // stale hint: k_block_rest reads the column
       if (t == 0) {
         const int q = atomicAdd(qcount, 1);
         if (q < qcap) queue[q] = qidx;  // at most one entry per item and tick (a guarded tick's count may grow)
@@ -115,8 +124,9 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
       }
       return;
     }
-  } else if (kHintLoad && hint && dense_subclients(rs) != hint) {
+  } else if (kHintLoad && hint && (dense_subclients(rs) != hint || arr_lapse)) {
     relm = 0;  // the column says which rows are released now
+    arrm = 0;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -130,7 +140,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   int64_t e[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) e[k] = rs.follow_exp;
-  if (MODE != kDenseOnly && any_explicit(rs)) {  // a dense resource has no explicit rows
+  if (MODE != kDenseOnly && (any_explicit(rs) || arr_lapse)) {  // a dense resource: only its lapsing arrivals
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -286,7 +296,9 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     } else {
       g = fs_uniform_row(w[k], h[k], C, cl.sum_has, fu);
     }
-    put_live<kGroupNT<G>>(p, lo, u, g, rs, sr[k]);
+    // (a live arrival of a dense resource: an explicit row the writeback turns into a
+    // follower; arrm is one register, sr stays the uniform hint)
+    put_live<kGroupNT<G>>(p, lo, u, g, rs, (arrm >> k & 1) ? (int)((unsigned)hint | kSubExplicit) : sr[k]);
     delta.v += g - h[k];
   }
 
@@ -305,8 +317,15 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
                  : (a.smin == a.smax && a.smin >= 1 && a.smin <= 254) ? a.smin : 0;
   const int hw_next = dn ? (dn | (nlive < n ? 1 << 8 : 0)) : 0;
   delta = group_reduce<G, SumD, OpSumD, false>(delta, OpSumD(), lds.d);
-  if (MODE == kDenseOnly ? nlive == 0 : (hw_next >> 8) != 0)  // a dense tick changes the mask only by a lapse
-    mrow[t] = (MaskT)(valid & ~live);
+  // A dense tick changes the mask only by a lapse; a writeback tick that changes the
+  // state word writes it whole (a later release ORs its row in, so it must be valid
+  // whenever the hint is set) and clears the arrivals it turned into followers.
+  if (kDense && (MODE == kDenseOnly ? nlive == 0 || (p.writeback && hw != hw_next)
+                                    : (hw_next >> 8) != 0 || (p.writeback && hw != hw_next))) {
+    // (R <= 4: a non-writeback tick keeps the arrivals' nibble)
+    mrow[t] = (MaskT)((valid & ~live) | (R <= 4 && !p.writeback ? arrm << 4 : 0u));
+    if (R > 4 && arrivals && p.writeback) mrow[G + t] = 0;
+  }
   if (t == 0) {
     write_resource(p, seg, rs, cl, delta.v, dn);
     if (p.writeback && hw != hw_next) item->n = n | hw_next << 16;
@@ -2413,11 +2432,42 @@ __global__ void k_clear_rows(int64_t n, const int64_t* __restrict__ rows, int64_
 // Narrow arrivals (dm_store_batch): has == nullptr -> 0; sub32 instead of sub;
 // expiry == nullptr -> the resource's now + lease length (the Assign's expiry,
 // store.go:161).
+// one byte of a dense resource's masks (dm_device.h mask_pos), atomically: rows of one
+// resource share the mask words
+__device__ __forceinline__ void mask_bit(uint8_t* base, int32_t off, int32_t bit, bool set) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base + off);
+  unsigned* w = reinterpret_cast<unsigned*>(a & ~uintptr_t(3));
+  const unsigned m = 1u << (bit + 8 * (int)(a & 3));
+  if (set)
+    atomicOr(w, m);
+  else
+    atomicAnd(w, ~m);
+}
+
+// The row's place in its dense resource's masks, or false when the resource is not in
+// a dense state its item describes (dm_device.h DenseUpd).
+__device__ __forceinline__ bool dense_row(const DenseUpd& du, const RowIndex& ix, int seg, int64_t r, uint8_t state,
+                                          MaskPos* mp, WorkItem** item) {
+  if (state < 2 || !du.item_of) return false;
+  const int32_t io = du.item_of[seg];
+  if (io < 0) return false;
+  const int bin = io >> 24;
+  WorkItem* it = du.bins[bin - 3] + (io & 0xFFFFFF);
+  if (((it->n >> 16) & 0xFF) != state - 1) return false;  // the hint is the state's (a new shape clears hints)
+  int G, R;
+  bin_shape(bin, du.bin4_wave, du.bin6_wide, &G, &R);
+  const int64_t lo = ix.seg_off[seg];
+  *mp = mask_pos(G, R, (int)(r - lo));
+  *item = it;
+  return true;
+}
+
 __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const double* __restrict__ has,
                          const double* __restrict__ wants, const int64_t* __restrict__ sub,
                          const int32_t* __restrict__ sub32, const int64_t* __restrict__ expiry,
                          const ResCfg* __restrict__ cfg, int64_t now, RowIndex ix, double* s_has, double* s_wants,
-                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags) {
+                         int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                         DenseUpd du) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (*flags & kUpdReject) return;  // uniform over the grid
   const bool active = i < n;
@@ -2435,14 +2485,27 @@ __global__ void k_upsert(int64_t n, const int64_t* __restrict__ rows, const doub
     s_has[r] = hv;
     s_wants[r] = wants[i];
     s_sub[r] = (int32_t)((uint32_t)sv | kSubExplicit);  // in [0, kSubMax] (k_check_rows); expiry explicit
-    s_exp[r] = expiry ? expiry[i] : now + (int64_t)cfg[seg].lease_len_s * kNs;
-    expl[seg] = 1;  // the tick reads this resource's expiry column again
+    const int64_t ex = expiry ? expiry[i] : now + (int64_t)cfg[seg].lease_len_s * kNs;
+    s_exp[r] = ex;
+    // an arrival with the dense resource's count and the Assign's expiry, not before the
+    // followers': the resource stays dense, the row goes into its arrival mask
+    MaskPos mp;
+    WorkItem* it;
+    const uint8_t st = expl[seg];
+    if (!expiry && dense_row(du, ix, seg, r, st, &mp, &it) && sv == (int64_t)st - 1 && ex >= agg[seg].follow_exp) {
+      mask_bit(du.rmask + rel_mask_offset(ix.seg_off[seg]), mp.roff, mp.rbit, false);
+      mask_bit(du.rmask + rel_mask_offset(ix.seg_off[seg]), mp.aoff, mp.abit, true);
+      atomicOr(&it->n, 1 << 25);
+    } else {
+      expl[seg] = 1;  // the tick reads this resource's expiry column again
+    }
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
 
 __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex ix, double* s_has, double* s_wants,
-                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags) {
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                          DenseUpd du) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (*flags & kUpdReject) return;  // uniform over the grid
   const bool active = i < n;
@@ -2459,7 +2522,17 @@ __global__ void k_release(int64_t n, const int64_t* __restrict__ rows, RowIndex 
     s_wants[r] = 0.0;
     s_sub[r] = (int32_t)kSubReleased;  // the mark every reader decodes first: the expiry column is left alone
     (void)s_exp;
-    if (expl[seg] >= 2) expl[seg] = 0;  // no longer dense: the next tick reads the subclients column
+    MaskPos mp;
+    WorkItem* it;
+    const uint8_t st = expl[seg];
+    if (dense_row(du, ix, seg, r, st, &mp, &it)) {  // stays dense: the row into the released-row mask
+      uint8_t* mb = du.rmask + rel_mask_offset(ix.seg_off[seg]);
+      mask_bit(mb, mp.roff, mp.rbit, true);
+      mask_bit(mb, mp.aoff, mp.abit, false);  // (a row that arrived since the last tick)
+      atomicOr(&it->n, 1 << 24);
+    } else if (st >= 2) {
+      expl[seg] = 0;  // no longer dense: the next tick reads the subclients column
+    }
   }
   wave_seg_add(agg, active, seg, dh, dw, ds, true, true);
 }
@@ -3198,18 +3271,19 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int32_t* sub32, const int64_t* expiry, const ResCfg* cfg, int64_t now,
                          const RowIndex& ix, double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp,
-                         ResAgg* agg, uint8_t* expl, const uint32_t* flags, hipStream_t st) {
+                         ResAgg* agg, uint8_t* expl, const uint32_t* flags, const DenseUpd& du, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   k_upsert<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, has, wants, sub, sub32, expiry, cfg, now, ix, s_has,
-                                                        s_wants, s_sub, s_exp, agg, expl, flags);
+                                                        s_wants, s_sub, s_exp, agg, expl, flags, du);
   return hipGetLastError();
 }
 
 hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
                           int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
-                          hipStream_t st) {
+                          const DenseUpd& du, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, ix, s_has, s_wants, s_sub, s_exp, agg, expl, flags);
+  k_release<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rows, ix, s_has, s_wants, s_sub, s_exp, agg, expl, flags,
+                                                         du);
   return hipGetLastError();
 }
 

@@ -44,9 +44,9 @@ hipError_t launch_general(const DevParams& p, const int32_t* glist, const int32_
 hipError_t launch_upsert(int64_t n, const int64_t* rows, const double* has, const double* wants, const int64_t* sub,
                          const int32_t* sub32, const int64_t* expiry, const ResCfg* cfg, int64_t now,
                          const RowIndex& ix, double* s_has, double* s_wants, int32_t* s_sub, int64_t* s_exp,
-                         ResAgg* agg, uint8_t* expl, const uint32_t* flags, hipStream_t st);
+                         ResAgg* agg, uint8_t* expl, const uint32_t* flags, const DenseUpd& du, hipStream_t st);
 hipError_t launch_release(int64_t n, const int64_t* rows, const RowIndex& ix, double* s_has, double* s_wants,
-                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags,
+                          int32_t* s_sub, int64_t* s_exp, ResAgg* agg, uint8_t* expl, const uint32_t* flags, const DenseUpd& du,
                           hipStream_t st);
 hipError_t launch_check_rows(int64_t n, const int64_t* rows, int64_t N, uint32_t* bitmap, const double* wants,
                              const int64_t* sub, const int32_t* sub32, uint32_t* flags, hipStream_t st);
@@ -280,6 +280,7 @@ struct dm_ctx {
   DBuf<ResAgg> agg;
   DBuf<uint8_t> expl;  // per resource: rows may carry explicit expiries (DevParams::expl)
   DBuf<uint8_t> rmask;  // released-row masks of dense workgroup-bin resources (DevParams::rmask)
+  DBuf<int32_t> item_of;  // [R]: bin << 24 | item index for bins 3-6, else -1 (DenseUpd)
   // config, AoS: what every tick reads (32 B), and the rest (safe capacity, refresh)
   DBuf<ResCfg> cfg;
   DBuf<ResCold> cold;
@@ -306,6 +307,16 @@ struct dm_ctx {
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
+  }
+  // the store-update kernels' view of the dense state (dm_device.h DenseUpd)
+  DenseUpd dense_upd() const {
+    DenseUpd d{};
+    d.item_of = item_of.p;
+    for (int b = 3; b <= 6; ++b) d.bins[b - 3] = bins[b].p;
+    d.bin4_wave = bin4_wave ? 1 : 0;
+    d.bin6_wide = bin6_wide ? 1 : 0;
+    d.rmask = rmask.p;
+    return d;
   }
   // Queue calibration (calib_step): which of the four auxiliary streams -- four hardware
   // queues -- carries which work class moved configs[2]'s tick from 111 to 157 us over
@@ -936,6 +947,15 @@ static int upload_plan(dm_ctx* c) {
   DM_HIP(c, upload(c->tiles, c->h_tiles.data(), c->h_tiles.size(), st), "plan tiles");
   DM_HIP(c, upload(c->tile_list, c->h_tile_list.data(), c->h_tile_list.size(), st), "plan tiles");
   for (int b = 0; b < kNumBins; ++b) DM_HIP(c, upload(c->bins[b], c->h_bins[b].data(), c->h_bins[b].size(), st), "plan bins");
+  {  // every workgroup-bin resource's item (the update kernels keep its dense state, DenseUpd)
+    std::vector<int32_t> io((size_t)std::max<int64_t>(c->R, 1), -1);
+    for (int b = 3; b <= 6; ++b)
+      for (size_t i = 0; i < c->h_bins[b].size(); ++i) io[(size_t)c->h_bins[b][i].seg] = (int32_t)(b << 24 | (int)i);
+    DM_HIP(c, upload(c->item_of, io.data(), io.size(), st), "plan items");
+    // the masks of a new plan start empty (the arrival masks are read only where an upsert
+    // set a bit; the released-row masks are written whole when a tick sets the dense state)
+    DM_HIP(c, hipMemsetAsync(c->rmask.p, 0, c->rmask.n, st), "plan masks");
+  }
   DM_HIP(c, upload(c->chunks, c->h_chunks.data(), c->h_chunks.size(), st), "plan chunks");
   DM_HIP(c, upload(c->large, c->h_large.data(), c->h_large.size(), st), "plan large");
   if (!c->h_dq) {
@@ -1389,7 +1409,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_HIP(c, upload(c->agg, agg.data(), (size_t)R, st), "upload running sums");
   const std::vector<uint8_t> expl((size_t)std::max<int64_t>(R, 1), 1);  // loaded rows carry explicit expiries
   DM_HIP(c, upload(c->expl, expl.data(), expl.size(), st), "upload explicit flags");
-  DM_HIP(c, c->rmask.ensure((size_t)(N / 2 + 64)), "alloc released-row masks");  // written before read
+  DM_HIP(c, c->rmask.ensure((size_t)(N / 2 + 64)), "alloc released-row masks");  // zeroed by upload_plan
   build_plan(c);
   int rc = upload_plan(c);
   if (rc) return rc;
@@ -2359,7 +2379,7 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   if (rc) return rc;
   DM_HIP(c, launch_upsert(n, c->st_rows.p, c->st_has.p, c->st_wants.p, c->st_sub.p, nullptr, c->st_exp.p, c->cfg.p, 0,
                           c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p,
-                          c->upd_flags.p, c->stream),
+                          c->upd_flags.p, c->dense_upd(), c->stream),
          "upsert");
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
@@ -2450,7 +2470,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
   int rc = staged_check(c, n, cols, 1, false, false);
   if (rc) return rc;
   DM_HIP(c, launch_release(n, c->st_rows.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p,
-                           c->agg.p, c->expl.p, c->upd_flags.p, c->stream),
+                           c->agg.p, c->expl.p, c->upd_flags.p, c->dense_upd(), c->stream),
          "release");
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
@@ -2567,7 +2587,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
            "check rows");
     DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
     DM_HIP(c, launch_release(nr, c->st_rel.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
-                             c->expl.p, F + 1, st),
+                             c->expl.p, F + 1, c->dense_upd(), st),
            "release");
     DM_HIP(c, launch_clear_rows(nr, c->st_rel.p, c->N, c->row_bits.p, st), "clear rows");
   } else {
@@ -2583,7 +2603,7 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     DM_HIP(c, launch_carry_reject(F + 1, F + 2, st), "carry");
     DM_HIP(c, launch_upsert(nu, c->st_rows.p, b->upsert_has ? c->st_has.p : nullptr, c->st_wants.p, s64, s32,
                             b->upsert_expiry_ns ? c->st_exp.p : nullptr, c->cfg.p, b->upsert_now_ns, c->row_index(),
-                            c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, F + 2, st),
+                            c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, F + 2, c->dense_upd(), st),
            "upsert");
     DM_HIP(c, launch_clear_rows(nu, c->st_rows.p, c->N, c->row_bits.p, st), "clear rows");
   }

@@ -1149,6 +1149,60 @@ def test_c4_loop_store_apply_matches_oracle(eng, cols, narrow):
         np.testing.assert_array_equal(st[k], host[k])
 
 
+@pytest.mark.parametrize("n,R,fs_only", [(300, 2000, False), (800, 1000, False), (1500, 500, False),
+                                         (3000, 300, False), (800, 5000, True)],
+                         ids=["bin3_128x4", "bin4_128x8", "bin5_256x8", "bin6", "bin4_wave_64x16"])
+def test_dense_state_survives_releases_and_arrivals(eng, n, R, fs_only):
+    """configs[4]'s rounds keep the workgroup bins' resources dense.  A
+    release marks its row in the released-row mask and an arrival (the resource's count,
+    the Assign's expiry) goes into the arrival mask instead of ending the dense state
+    (dm_device.h DenseUpd), for every bin shape (the nibble-packed 128 x 4, 128 x 8,
+    256 x 8, bin 6, and bin 4's one-wave 64 x 16 shape of a FairShare store in stream
+    parts).  Rounds as the bench's (narrow arrivals, row-mask wants refresh), a tenth of
+    the resources on a 4-s lease so their followers lapse while arrivals made at the
+    round's time outlive them (the column path).  Each tick against the oracle; the dense
+    share at tick time (dm_store_stats) after each round's updates; the store read back
+    equal to the host's copy at the end."""
+    rng = np.random.default_rng(505 + n)
+    snap = _c4_store(rng, R, n)
+    if fs_only:
+        snap["kind"] = np.full(R, W.FAIR_SHARE, np.int32)
+    eng.load(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    now = NOW
+    so = snap["seg_off"]
+    for t in range(2):  # writeback ticks: every resource dense (released rows in its mask)
+        eng.apportion(now, writeback=True)
+        ref = O.apportion(host, now)
+        _writeback_host(host, ref)
+    W.add_store_sums(host)
+    shares = []
+    for rnd in range(5):
+        now += 5 * W.NS
+        mask, w, gone, new, nh, nw, ns, ne, upd = _c4_round(rng, host, now)
+        ne = now + snap["lease_length_s"][np.searchsorted(so, new, side="right") - 1] * W.NS
+        eng.apply(mask, w, gone, (new, None, nw, ns.astype(np.int32), None), now_ns=now)
+        _apply_host(host, upd, w, gone, new, nh, nw, ns, ne)
+        st = eng.store_stats()
+        shares.append(st["dense_leases"] / len(host["wants"]))
+        eng.apportion(now, writeback=True)
+        gets, exp = eng.leases()
+        ref = O.apportion(host, now)
+        assert_leases_match(host, gets, exp, ref, f"round {rnd}")
+        _writeback_host(host, ref)
+        W.add_store_sums(host)
+        res = eng.resources(safe=False)
+        np.testing.assert_array_equal(res["count"], host["agg_count"])
+    # the 4-s resources lapse every round; the rest keep their dense state through the updates
+    assert min(shares) >= 0.8, shares
+    st = eng.read_store()
+    for k in ("subclients", "expiry_ns"):
+        np.testing.assert_array_equal(st[k], host[k], err_msg=k)
+    assert float_close(st["has"], host["has"], row_capacity(host)).all()
+    if fs_only:
+        assert eng.plan_info()["bin_shapes"] & 2  # bin 4 ran on one wave per resource
+
+
 def test_c4_full_size_properties_after_bench_rounds(eng):
     """configs[4] at full per-GPU size (125M leases, bench.make_workload("c4")):
     three of the bench's own rounds (bench.streaming_step: dm_store_apply + writeback
