@@ -1175,7 +1175,7 @@ def test_dense_state_survives_releases_and_arrivals(eng, n, R, fs_only):
         eng.apportion(now, writeback=True)
         ref = O.apportion(host, now)
         _writeback_host(host, ref)
-    W.add_store_sums(host)
+        W.add_store_sums(host)
     shares = []
     for rnd in range(5):
         now += 5 * W.NS
