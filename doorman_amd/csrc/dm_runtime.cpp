@@ -289,6 +289,10 @@ struct dm_ctx {
   DBuf<int64_t> out_expiry;
   DBuf<ResAgg> res;
   bool last_writeback = false, have_result = false;
+  // the workgroup bins' items carry dense hints: set by a writeback tick, kept by the
+  // store updates (which keep a dense resource's state or end it: DenseUpd), cleared by
+  // a new store
+  bool hints_set = false;
   int64_t seg_uniform = 0;  // rows per resource when every resource has the same count, else 0
   // A forked tick's work classes run on the auxiliary streams.  Normally they are
   // joined back into the context stream at the end of the tick; with DM_DEFER_JOIN
@@ -1424,6 +1428,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   c->expl_rows = true;
   c->rows_changed();
   c->have_result = false;
+  c->hints_set = false;
   if (c->cfg_loaded && (int64_t)c->h_refresh_s.size() != R) c->cfg_loaded = false;
   return DM_OK;
 }
@@ -1831,7 +1836,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
     chain_live = nch > 0 && !het;
   }
   // the workgroup bins split by the dense hint after a writeback tick (hints set)
-  const bool split_dense = c->have_result && c->last_writeback;
+  const bool split_dense = c->hints_set;
   // the sub-wave bins (8x2, 16x2, 16x4, 32x4, 64x4) in one launch on bin 0's stream
   {
     SubBins sb{};
@@ -1940,6 +1945,7 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   if (pingpong) std::swap(c->has, c->out_gets);  // the written column becomes the store's (stream order)
   c->last_writeback = wb;
   c->have_result = true;
+  if (wb) c->hints_set = true;
   if (wb) c->expl_rows = false;
   c->chain_live_ok = wb && chain_live;
   if (!(flags & DM_ASYNC)) {
