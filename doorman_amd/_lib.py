@@ -123,6 +123,7 @@ _SIGS = {
     "dm_reset_kernel_times": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_plan_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "dm_store_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
+    "dm_store_lost": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "dm_read_leases_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]),
     # round-oriented GetCapacity dispatch (dm_server.cpp)

@@ -520,6 +520,11 @@ struct dm_ctx {
   // Round 4 stored a word from a one-wave k_tick_done after the dense kernel (5 us of
   // the leaf's queue): the N = 8 rehearsal step 60.2-60.7 -> 58.7-58.8 us (round 5,
   // gpurun_out/r5b2shard, three alternations).
+  // The event covers the tick's leases and sums, not every launch of it: once per row
+  // epoch a writeback tick enqueues k_count_undense after the event-carrying kernel on
+  // the same stream (check_dense).  That kernel only reads the work items' hints and
+  // writes a host-mapped count, which no consumer of the event (the exchange, a template
+  // slot's reuse) touches; a consumer that needed it would have to join the stream.
   uint64_t tick_seq = 0;          // the last tick's number
   bool tick_flagged = false;      // ... and whether its last kernels complete tick_ev[*][tick_seq % kTickEv]
   static constexpr int kTickEv = 16;
@@ -574,10 +579,11 @@ struct dm_ctx {
         lost_msg = "a redo workgroup of the speculative chain gave up waiting for its resource";
       }
     }
-    if (!store_lost) return DM_OK;
+    if (!store_lost || reading) return DM_OK;  // (a reader of a lost store: dm_store_lost says so)
     return fail(DM_E_INTERNAL, "internal failure on the device: " + lost_msg +
                                    "; the store's leases and sums may be wrong, reload it (dm_store_load)");
   }
+  bool reading = false;  // a read call in progress (DM_STORE_READABLE): a lost store may be read
   // wait for the context stream, then report a device failure the wait completed
   int synced(const char* what) {
     const hipError_t e = hipStreamSynchronize(stream);
@@ -693,6 +699,16 @@ struct dm_ctx {
   do {                                               \
     if (int _rc = (ctx)->check_device()) return _rc; \
   } while (0)
+// The read calls work on a lost store too (for diagnosis): the failure is
+// still recorded, and dm_store_lost reports it.  Ticks and updates keep refusing it.
+struct ReadScope {
+  dm_ctx* c;
+  explicit ReadScope(dm_ctx* x) : c(x) { c->reading = true; }
+  ~ReadScope() { c->reading = false; }
+};
+#define DM_STORE_READABLE(ctx)  \
+  ReadScope _read_scope(ctx); \
+  (void)(ctx)->check_device()
 
 template <typename T>
 static hipError_t upload(DBuf<T>& b, const T* src, size_t n, hipStream_t st) {
@@ -1099,7 +1115,7 @@ static hipError_t xs_setup(dm_ctx* c) {
 // kept for the life of the process and reused by later contexts on the same device
 // (dm_destroy returns a context's set; take_aux hands out the earliest-created free
 // set).  The hardware queues behind the streams are not interchangeable: measured on
-// C2 (round 5, tools/gpu_r5_perm.sh, profiles/r05_queues.txt), which of the four
+// C2 (round 5, tools/archive/gpu_r5_perm.sh, profiles/r05_queues.txt), which of the four
 // masked queues carries which work class moved the tick from 111 us to 157 us, and the
 // best assignment is a property of the queue's position in the process's creation
 // order (period 4, consistent with queues spread over four hardware pipes): the small
@@ -1754,8 +1770,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   const bool fork = __builtin_popcount(used) > 1;
   int nonempty_bins = 0;
   for (int b = 0; b < kNumBins; ++b) nonempty_bins += c->h_bins[b].empty() ? 0 : 1;
-  // one work class (on the context stream, or in stream parts), no kernel after its
-  // split bin's rest kernel: that kernel completes the tick's event
+  // one work class (on the context stream, or in stream parts): its split bin's last
+  // kernel completes the tick's event (only check_dense's hint count may follow it)
   bool parts_only = false;
   for (int b = 0; b < kNumBins; ++b) parts_only |= !c->h_bins[b].empty() && c->bin_parts[b] > 1;
   const bool one_class = (!fork || parts_only) && nch == 0 && c->h_tiles.empty() && !general && nonempty_bins == 1;
@@ -2158,7 +2174,7 @@ static int check_range(dm_ctx* c, int64_t off, int64_t n, int64_t total) {
 
 int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* expiry_ns) {
   DM_ENTER(c);
-  DM_STORE_OK(c);
+  DM_STORE_READABLE(c);
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
@@ -2177,7 +2193,7 @@ int dm_read_leases(dm_ctx* c, int64_t off, int64_t n, double* gets, int64_t* exp
 
 int dm_read_leases_rows(dm_ctx* c, int64_t n, const int64_t* rows, double* gets, int64_t* expiry_ns) {
   DM_ENTER(c);
-  DM_STORE_OK(c);
+  DM_STORE_READABLE(c);
   if (!c->have_result) return c->fail(DM_E_STATE, "no dm_apportion result");
   if (n < 0 || (n > 0 && !rows)) return c->fail(DM_E_INVAL, "bad rows");
   if (n == 0) return DM_OK;
@@ -2237,7 +2253,7 @@ int dm_read_leases_proto(dm_ctx* c, int64_t off, int64_t n, double* capacity, in
 int dm_read_resources(dm_ctx* c, int64_t r0, int64_t n, int64_t* count, double* sum_has, double* sum_wants,
                       double* safe) {
   DM_ENTER(c);
-  DM_STORE_OK(c);
+  DM_STORE_READABLE(c);
   int rc = check_range(c, r0, n, c->R);
   if (rc) return rc;
   if (safe && !c->have_result) return c->fail(DM_E_STATE, "safe capacity needs a dm_apportion result");
@@ -2286,7 +2302,7 @@ int dm_read_config(dm_ctx* c, int64_t r0, int64_t n, int32_t* kind, double* capa
 
 int dm_read_store(dm_ctx* c, int64_t off, int64_t n, double* has, double* wants, int64_t* sub, int64_t* exp) {
   DM_ENTER(c);
-  DM_STORE_OK(c);
+  DM_STORE_READABLE(c);
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   int rc = check_range(c, off, n, c->N);
   if (rc) return rc;
@@ -2365,6 +2381,20 @@ static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
   return DM_OK;
 }
 
+// A store update can make a store "maybe general" (a NaN wants, subclients other than
+// one) after its plan chose stream parts, which plan_parts excludes for such a store:
+// the plan's parts and split slots are set up again, after the deferred
+// class work that may still use them.
+static int mark_maybe_general(dm_ctx* c) {
+  if (c->maybe_general) return DM_OK;
+  c->maybe_general = true;
+  bool parts = false;
+  for (int b = 0; b < kNumBins; ++b) parts |= c->bin_parts[b] > 1;
+  if (!parts) return DM_OK;
+  DM_HIP(c, c->join_aux(), "join");
+  return init_split_slots(c, c->stream);
+}
+
 int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has, const double* wants,
                     const int64_t* sub, const int64_t* exp) {
   DM_ENTER(c);
@@ -2391,7 +2421,8 @@ int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has
   rc = finish_update(c, n, &f);
   if (rc) return rc;
   // an upsert can make a resource's subclients heterogeneous: stay conservative
-  if ((f & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one) c->maybe_general = true;
+  if ((f & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one)
+    if (int rg = mark_maybe_general(c)) return rg;
   if (f & kUpdNotOne) c->all_sub_one = false;
   c->have_result = false;
   return DM_OK;
@@ -2415,7 +2446,8 @@ int dm_store_update_wants(dm_ctx* c, int64_t n, const int64_t* rows, const doubl
   uint32_t f = 0;
   rc = finish_update(c, n, &f);
   if (rc) return rc;
-  if (f & kUpdNaN) c->maybe_general = true;
+  if (f & kUpdNaN)
+    if (int rg = mark_maybe_general(c)) return rg;
   c->have_result = false;
   return DM_OK;
 }
@@ -2459,7 +2491,8 @@ int dm_store_update_wants_mask(dm_ctx* c, int64_t first_row, int64_t nwords, con
   const uint32_t f = *c->h_flags;
   if (f & kUpdRange) return c->fail(DM_E_RANGE, "mask bit past the store's end");
   if (f & kUpdCount) return c->fail(DM_E_INVAL, "packed values must match the mask's set bits");
-  if (f & kUpdNaN) c->maybe_general = true;
+  if (f & kUpdNaN)
+    if (int rg = mark_maybe_general(c)) return rg;
   c->have_result = false;
   return DM_OK;
 }
@@ -2625,11 +2658,13 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     return c->fail(DM_E_INVAL, p + ": subclients must be in [0, 2^31-2]");
   };
   if (f0 & kUpdReject) return reject(f0, "wants refresh");
-  if (f0 & kUpdNaN) c->maybe_general = true;
+  if (f0 & kUpdNaN)
+    if (int rg = mark_maybe_general(c)) return rg;
   if (f1 & kUpdReject) return reject(f1, "release");
   if (f2 & kUpdReject) return reject(f2, "upsert");
   if (nu > 0) {
-    if ((f2 & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one) c->maybe_general = true;
+    if ((f2 & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one)
+      if (int rg = mark_maybe_general(c)) return rg;
     if (f2 & kUpdNotOne) c->all_sub_one = false;
   }
   return DM_OK;
@@ -3118,6 +3153,15 @@ int dm_plan_info(dm_ctx* c, int64_t* out, int max) {
   const int n = 10 + kNumBins;
   for (int i = 0; i < n && i < max; ++i) out[i] = v[i];
   return n;
+}
+
+int dm_store_lost(dm_ctx* c, int* lost) {
+  DM_ENTER(c);
+  if (!lost) return c->fail(DM_E_INVAL, "null output");
+  (void)c->check_device();  // (records a failure the last sync completed)
+  *lost = c->store_lost ? 1 : 0;
+  if (c->store_lost) c->err = "internal failure on the device: " + c->lost_msg;
+  return DM_OK;
 }
 
 int dm_store_stats(dm_ctx* c, int64_t* out, int max) {

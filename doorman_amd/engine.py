@@ -291,6 +291,13 @@ class Engine:
         n = self._chk(self._L.dm_plan_info(self._ctx, arr, 32))
         return {_BIN_NAMES[i]: int(arr[i]) for i in range(min(n, len(_BIN_NAMES)))}
 
+    def store_lost(self) -> bool:
+        """dm_store_lost: a device-side invariant failed; ticks and updates refuse the store
+        until it is reloaded, the read calls still work on it."""
+        v = ctypes.c_int(0)
+        self._chk(self._L.dm_store_lost(self._ctx, ctypes.byref(v)))
+        return bool(v.value)
+
     def store_stats(self) -> dict:
         """dm_store_stats: dense resources (read at 24 B per lease) and their rows,
         resources that may hold explicit expiries, resources."""

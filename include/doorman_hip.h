@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-/* 5 (round 6): dm_plan_info's slot 18 is the class streams' hardware-queue assignment the
+/* 5 (round 6): dm_store_lost (the read calls work on a lost store); dm_plan_info's slot 18 is the class streams' hardware-queue assignment the
    context's queue calibration chose (-1 before it finished); returns 19.
    4 (round 5): dm_kernel_class_names, dm_hier_comm_info; dm_plan_info's slot 14 is the
    redo's co-resident workgroup bound (was the per-chunk redo's chunk bound), slot 15
@@ -156,6 +156,9 @@ const char* dm_last_error(dm_ctx* ctx);
    The HIP null stream therefore cannot be selected: a caller whose current stream is the
    null stream (torch's default) must create a stream to share (doorman_amd/hierarchy.py). */
 int dm_set_stream(dm_ctx* ctx, void* hip_stream);
+/* The context stream.  After dm_destroy the handle must not be used: the stream stays
+   alive (the library pools a destroyed context's streams for the next context on the
+   device), so work queued on it would run in another context's stream. */
 void* dm_get_stream(dm_ctx* ctx);
 int dm_sync(dm_ctx* ctx);
 /* Order every deferred tick (DM_DEFER_JOIN) before later work on the context stream,
@@ -202,6 +205,11 @@ int dm_store_apply(dm_ctx* ctx, const dm_store_batch* batch);
  * rate; ordinary host memory is staged by the HIP runtime. */
 int dm_host_alloc(dm_ctx* ctx, size_t bytes, void** out);
 int dm_host_free(dm_ctx* ctx, void* ptr);
+/* Whether a device-side invariant failed (a redo workgroup gave up, a dense kernel queued
+ * an item a skipped launch would have decided): *lost = 1, with the reason in
+ * dm_last_error.  A lost store refuses ticks and updates (DM_E_INTERNAL) until
+ * dm_store_load; the read calls below still work on it, so its state can be inspected. */
+int dm_store_lost(dm_ctx* ctx, int* lost);
 /* read back stored rows (has/wants/subclients/expiry_ns) — any pointer may be NULL */
 int dm_read_store(dm_ctx* ctx, int64_t off, int64_t n, double* has, double* wants, int64_t* subclients,
                   int64_t* expiry_ns);

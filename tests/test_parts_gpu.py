@@ -183,3 +183,41 @@ def test_bin4_without_parts_keeps_its_shape():
         eng.load(snap)
         info = eng.plan_info()
         assert info["stream_parts"] == 1 and not info["bin_shapes"] & 2, info
+
+
+def test_parts_store_turning_general_replans():
+    """a store in stream parts (no heterogeneous subclients when it was planned)
+    takes an upsert with subclients 3 on some rows of resources in both halves, which
+    makes it "maybe general" (k_general decides heterogeneous FairShare): the plan drops
+    the parts (they exclude such a store) and back-to-back ticks match the oracle."""
+    import torch
+    from doorman_amd.engine import Engine
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(99)
+    sizes = rng.integers(513, 700, 4600)
+    snap = snapshot_with_sizes(rng, sizes, kinds=(2, 3), expired_frac=0.02, learning_frac=0.0)
+    W.add_store_sums(snap)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    so = np.asarray(snap["seg_off"])
+    with Engine(0) as eng:
+        eng.load(snap)
+        assert eng.plan_info()["stream_parts"] == 2
+        now = NOW
+        for _ in range(3):
+            eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
+            _host_tick(host, now)
+        # three subclients on a few live rows of resources in both halves
+        rows = np.concatenate([np.arange(so[r], so[r] + 5) for r in (3, 100, 2400, 4500)])
+        rows = rows[host["expiry_ns"][rows] != W.RELEASED]
+        exp = np.full(len(rows), now + 600 * W.NS, np.int64)
+        eng.upsert(rows, host["has"][rows], host["wants"][rows], np.full(len(rows), 3, np.int64), exp)
+        host["subclients"][rows] = 3
+        host["expiry_ns"][rows] = exp
+        W.add_store_sums(host)
+        assert eng.plan_info()["stream_parts"] == 1  # re-planned without parts
+        for _ in range(4):
+            now += int(rng.integers(0, 20)) * W.NS
+            eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
+            _host_tick(host, now)
+        eng.sync()
+        _check(eng, host, "after the heterogeneous upsert")
