@@ -2382,17 +2382,15 @@ static int finish_update(dm_ctx* c, int64_t n, uint32_t* flags_out) {
 }
 
 // A store update can make a store "maybe general" (a NaN wants, subclients other than
-// one) after its plan chose stream parts, which plan_parts excludes for such a store:
-// the plan's parts and split slots are set up again, after the deferred
-// class work that may still use them.
+// one) after its plan chose stream parts, which plan_parts leaves out for a store
+// that is general when planned.  The parts stay (ADVICE r5 asked which): a tick that
+// may run k_general joins every class stream before it (dm_apportion: no deferred
+// join), so k_general sees both parts' worklist appends, and the parts' own kernels
+// leave a heterogeneous resource untouched for it
+// (tests/test_parts_gpu.py::test_parts_store_turning_general_keeps_its_parts).
 static int mark_maybe_general(dm_ctx* c) {
-  if (c->maybe_general) return DM_OK;
   c->maybe_general = true;
-  bool parts = false;
-  for (int b = 0; b < kNumBins; ++b) parts |= c->bin_parts[b] > 1;
-  if (!parts) return DM_OK;
-  DM_HIP(c, c->join_aux(), "join");
-  return init_split_slots(c, c->stream);
+  return DM_OK;
 }
 
 int dm_store_upsert(dm_ctx* c, int64_t n, const int64_t* rows, const double* has, const double* wants,

@@ -185,11 +185,12 @@ def test_bin4_without_parts_keeps_its_shape():
         assert info["stream_parts"] == 1 and not info["bin_shapes"] & 2, info
 
 
-def test_parts_store_turning_general_replans():
+def test_parts_store_turning_general_keeps_its_parts():
     """a store in stream parts (no heterogeneous subclients when it was planned)
     takes an upsert with subclients 3 on some rows of resources in both halves, which
-    makes it "maybe general" (k_general decides heterogeneous FairShare): the plan drops
-    the parts (they exclude such a store) and back-to-back ticks match the oracle."""
+    makes it "maybe general": its FairShare resources with mixed counts go to k_general.
+    The parts stay; a tick that may run k_general joins both parts' streams first, so
+    back-to-back ticks (nothing read between them) still match the oracle."""
     import torch
     from doorman_amd.engine import Engine
     torch.cuda.set_device(0)
@@ -214,10 +215,11 @@ def test_parts_store_turning_general_replans():
         host["subclients"][rows] = 3
         host["expiry_ns"][rows] = exp
         W.add_store_sums(host)
-        assert eng.plan_info()["stream_parts"] == 1  # re-planned without parts
+        assert eng.plan_info()["stream_parts"] == 2  # the parts stay
         for _ in range(4):
             now += int(rng.integers(0, 20)) * W.NS
             eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
             _host_tick(host, now)
         eng.sync()
         _check(eng, host, "after the heterogeneous upsert")
+        assert eng.kernel_times() is not None
