@@ -1415,6 +1415,9 @@ __device__ __forceinline__ AggC chunk_c(const ChunkRows& rw, int s0, double eq, 
   return x;
 }
 
+// (at 5 waves per SIMD -- amdgpu_waves_per_eu(5): 96 VGPRs, 2 spilled -- C2 lost 105.2 ->
+// 108.7 us, both orders, round 6: the chain's workgroups are latency-bound per phase,
+// and the spill sits on the map's path)
 __global__ __launch_bounds__(256) void k_large_spec(DevParams p, const Chunk* __restrict__ chunks,
                                                     const LargeSeg* __restrict__ ls, Partials P, SpecArgs S) {
   __shared__ Lds<256> lds;
