@@ -88,7 +88,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
   // of the released-row entry for R <= 4, else G entries after the released-row ones
   constexpr unsigned kRowBits = R >= 32 ? ~0u : (1u << R) - 1u;
   const bool arrivals = kDense && ((hw >> 9) & 1);
-  unsigned arrm = 0;
+  bool by_hint = MODE == kDenseOnly;  // the rows' states come from the hint and the masks, not the column
   if (MODE != kDenseOnly && !hint) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -101,7 +101,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     }
   } else {
     if (hw >> 8 & 1) relm = (unsigned)mrow[t] & kRowBits;
-    if (arrivals) arrm = R <= 4 ? ((unsigned)mrow[t] >> 4) & kRowBits : (unsigned)mrow[G + t];
+    by_hint = true;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -126,7 +126,7 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     }
   } else if (kHintLoad && hint && (dense_subclients(rs) != hint || arr_lapse)) {
     relm = 0;  // the column says which rows are released now
-    arrm = 0;
+    by_hint = false;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = k * G + t;
@@ -296,10 +296,20 @@ __device__ __forceinline__ void group_segment(const DevParams& p, const WorkItem
     } else {
       g = fs_uniform_row(w[k], h[k], C, cl.sum_has, fu);
     }
-    // (a live arrival of a dense resource: an explicit row the writeback turns into a
-    // follower; arrm is one register, sr stays the uniform hint)
-    put_live<kGroupNT<G>>(p, lo, u, g, rs, (arrm >> k & 1) ? (int)((unsigned)hint | kSubExplicit) : sr[k]);
+    put_live<kGroupNT<G>>(p, lo, u, g, rs, sr[k]);
     delta.v += g - h[k];
+  }
+  // (uniform) the live arrivals of a dense resource decided by the hint become followers:
+  // their explicit subclients words are rewritten (the arrival mask is loaded only here,
+  // so a store without arrivals carries no register for it)
+  unsigned arrm = 0;
+  if (arrivals && by_hint) {
+    arrm = R <= 4 ? ((unsigned)mrow[t] >> 4) & kRowBits : (unsigned)mrow[G + t];
+    if (p.writeback) {
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if ((arrm & live) >> k & 1) *col_at(p.out_sub + lo, (unsigned)(k * G + t)) = hint;
+    }
   }
 
   // After a writeback tick every live row follows the resource and every other row
