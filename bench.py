@@ -286,11 +286,13 @@ def streaming_step(eng, snap, rank, n_ticks):
     def apply_only():
         mask, w, gone, new, nw, ns, t = next(it)
         eng.apply(mask, w, gone, (new, None, nw, ns, None), now_ns=t)  # the round's three update kinds, one call
+        step.last_now = t  # (busy_kernel_probe ticks on at the last applied round's time)
         return t
 
     def step():
         eng.apportion(apply_only(), writeback=True, asynchronous=True)
 
+    step.last_now = now
     step.apply_only = apply_only  # the state a tick starts from (bench's dense share at tick time)
     return step
 
@@ -752,6 +754,42 @@ def tick_fracs(snap, dense_frac, t_step) -> dict:
             "tick_algorithmic_bytes": tick_bytes, **fp}
 
 
+def busy_kernel_probe(eng, snap, now, dense_frac, ticks=20, warm_s=0.3):
+    """configs[4]'s tick kernel with the GPU kept busy: after the timed streaming
+    rounds, the same store ticked back to back at the last round's time with no
+    update between (~0.3 s first, as timed_steps' warm-up), HIP events around every
+    launch.  In the streaming step the GPU's compute idles through the PCIe-bound
+    apply (~80 % of the step) and the tick starts from that idle state: the same
+    kernel on the same store runs 15-20 % slower there (tools/c4_variants.py: C3's
+    kernel after 4 ticks 516 us, after 0.3 s 416 us on one box).  Reported beside
+    the step's own roofline, never in its place."""
+    t_w = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t_w < warm_s:
+        eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
+        n += 1
+        if n % 8 == 0:
+            eng.sync()
+    eng.sync()
+    eng.set_profiling(True)
+    eng.reset_kernel_times()
+    for _ in range(ticks):
+        eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)
+    eng.sync()
+    kt = eng.kernel_times()
+    eng.set_profiling(False)
+    name, (launches, total_ms) = max(kt.items(), key=lambda kv: kv[1][1])
+    avg_s = total_ms / launches / 1e3
+    units = kernel_units(snap)
+    leases_k, res_k = units[name]
+    alg = algorithmic_bytes(leases_k, res_k, kernel_lease_bytes(name, leases_k, dense_frac))
+    return {"kernel": name, "ticks": ticks, "warm_ticks": n, "avg_launch_us": round(avg_s * 1e6, 2),
+            "achieved": round(alg / avg_s / 1e9, 1), "frac": round(alg / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "the same kernel and store after the timed rounds, ticked back to back with no PCIe update "
+                    "between (the GPU busy); the step's roofline above is the kernel as the streaming step "
+                    "runs it, starting from the idle GPU of the apply"}
+
+
 def workload_line(name, snap, run, steps, single_kernel_tick):
     """One workload's numbers for the bench line's `extra` (or the line itself): rate,
     step time, the tick's fraction of HBM spec over its algorithmic bytes, per-class
@@ -1073,6 +1111,7 @@ def main():
         run = timed_steps(torch, eng, step, args.steps, args.warmup, sync_ranks, extra_warm=args.workload != "c4",
                           also=[root] if root is not None else [])
         run["dense_frac"] = tick_dense_fraction(eng, snap, step)
+        run["last_now"] = getattr(step, "last_now", now)
         run["parts"] = int(eng.plan_info().get("stream_parts", 1))
         if ht is not None:
             ht.sync()
@@ -1112,6 +1151,8 @@ def main():
     t_max, n_total = run["t_max"], run["n_total"]
     roofline = roofline_of(args.workload, snap, run, args.steps,
                            single_kernel_tick=not hier and args.workload != "c4")
+    if args.workload == "c4" and roofline is not None:
+        roofline["busy_gpu"] = busy_kernel_probe(eng, snap, run["last_now"], run["dense_frac"])
     now = W.NOW_NS
 
     extra = {}
@@ -1143,6 +1184,8 @@ def main():
             rx["dense_frac"] = tick_dense_fraction(ex, snapx, stx)
             rx["parts"] = int(ex.plan_info().get("stream_parts", 1))
             extra[name] = workload_line(name, snapx, rx, kx, single_kernel_tick=name == "c1")
+            if name == "c4" and extra[name]["roofline"] is not None:
+                extra[name]["roofline"]["busy_gpu"] = busy_kernel_probe(ex, snapx, stx.last_now, rx["dense_frac"])
             extra[name]["aux_own_queues"] = bool(ex.plan_info().get("aux_own_queues", 0))
             ex.close()
             del snapx
