@@ -22,6 +22,9 @@ from bench import algorithmic_bytes, make_workload  # noqa: E402
 from doorman_amd import workloads as W  # noqa: E402
 from doorman_amd.engine import Engine  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import c4_variants  # noqa: E402
+
 
 @contextlib.contextmanager
 def env(values):
@@ -49,6 +52,8 @@ def main():
     if args.workload.startswith("u") and "x" in args.workload:  # uRxC: R resources x C clients, FairShare
         nr, nc = (int(v) for v in args.workload[1:].split("x"))
         snap = W.uniform(nr, nc, kind=W.FAIR_SHARE, seed=3)
+    elif args.workload in c4_variants.VARIANTS:  # a configs[4]-shaped store (tools/c4_variants.py)
+        snap = c4_variants.make(**c4_variants.VARIANTS[args.workload])
     else:
         snap = make_workload(args.workload, 0)
     R, N = len(snap["seg_off"]) - 1, len(snap["wants"])

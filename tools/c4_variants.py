@@ -53,37 +53,42 @@ VARIANTS = {
     "c3like_100k": {"free": 0.0, "learning": 0.0, "kind": W.FAIR_SHARE, "R": 100_000},
 }
 
-ticks = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-WARM = int(os.environ.get("WARM", "4"))
-names = sys.argv[2:] or list(VARIANTS)
-for name in names:
-    const = name.endswith("_const")  # every tick at the same now (as tools/c2_marginal.py)
-    base = name[:-6] if const else name
-    if base == "bench_c3":
-        import bench
-        snap = bench.make_workload("c3", 0)
-    else:
-        snap = make(**VARIANTS[base])
-    step = 0 if const else 5 * W.NS
-    with Engine(0) as eng:
-        eng.load(snap)
-        t = W.NOW_NS
-        for i in range(WARM):  # ~0.3 s of back-to-back ticks first (bench.timed_steps' extra warm-up)
-            t += step
-            eng.apportion(t, writeback=True, asynchronous=True, defer_join=True)
-            if i % 8 == 7:
-                eng.sync()
-        eng.sync()
-        eng.set_profiling(True)
-        eng.reset_kernel_times()
-        t0 = time.perf_counter()
-        for _ in range(ticks):
-            t += step
-            eng.apportion(t, writeback=True, asynchronous=True, defer_join=True)
-        eng.sync()
-        dt = (time.perf_counter() - t0) / ticks
-        kt = {k: round(v[1] / max(v[0], 1) * 1e3, 2) for k, v in eng.kernel_times().items()}
-        st = eng.store_stats()
-    print(json.dumps({"variant": name, "tick_ms": round(dt * 1e3, 3), "kernels": kt,
-                      "dense": st["dense_leases"], "rows": int(snap["seg_off"][-1])}), flush=True)
-    del snap
+def main():
+    ticks = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    WARM = int(os.environ.get("WARM", "4"))  # noqa: N806
+    names = sys.argv[2:] or list(VARIANTS)
+    for name in names:
+        const = name.endswith("_const")  # every tick at the same now (as tools/c2_marginal.py)
+        base = name[:-6] if const else name
+        if base == "bench_c3":
+            import bench
+            snap = bench.make_workload("c3", 0)
+        else:
+            snap = make(**VARIANTS[base])
+        step = 0 if const else 5 * W.NS
+        with Engine(0) as eng:
+            eng.load(snap)
+            t = W.NOW_NS
+            for i in range(WARM):  # ~0.3 s of back-to-back ticks first (bench.timed_steps' extra warm-up)
+                t += step
+                eng.apportion(t, writeback=True, asynchronous=True, defer_join=True)
+                if i % 8 == 7:
+                    eng.sync()
+            eng.sync()
+            eng.set_profiling(True)
+            eng.reset_kernel_times()
+            t0 = time.perf_counter()
+            for _ in range(ticks):
+                t += step
+                eng.apportion(t, writeback=True, asynchronous=True, defer_join=True)
+            eng.sync()
+            dt = (time.perf_counter() - t0) / ticks
+            kt = {k: round(v[1] / max(v[0], 1) * 1e3, 2) for k, v in eng.kernel_times().items()}
+            st = eng.store_stats()
+        print(json.dumps({"variant": name, "tick_ms": round(dt * 1e3, 3), "kernels": kt,
+                          "dense": st["dense_leases"], "rows": int(snap["seg_off"][-1])}), flush=True)
+        del snap
+
+
+if __name__ == "__main__":
+    main()
