@@ -240,13 +240,16 @@ def kernel_lease_bytes(name, leases_k, dense_frac):
     return 0.0
 
 
-def streaming_step(eng, snap, rank, n_ticks):
+def streaming_step(eng, snap, rank, n_ticks, asynchronous=True):
     """configs[4]: one 5 s refresh tick of a device-resident store.  Per tick the
     host sends 10% wants updates (row mask + packed values, narrow Assign), releases
     1% of the clients (departures, store.go:142-151), inserts 1% new clients into
-    free slots (upsert onto released rows) -- all three in one dm_store_apply call --
+    free slots (upsert onto released rows) -- all three in one store batch --
     then the tick runs with writeback.  The update batches (what the RPCs would deliver) are generated
-    before the timed region."""
+    before the timed region.  asynchronous (the default): the batch through
+    dm_store_apply_async, so one round's PCIe copies follow the previous round's back to
+    back (the host waits only for the batch two rounds back); step.finish retires the
+    batches in flight (a rejected one raises)."""
     from doorman_amd import workloads as W
     rng = np.random.default_rng(400 + rank)
     N = len(snap["wants"])
@@ -285,7 +288,8 @@ def streaming_step(eng, snap, rank, n_ticks):
 
     def apply_only():
         mask, w, gone, new, nw, ns, t = next(it)
-        eng.apply(mask, w, gone, (new, None, nw, ns, None), now_ns=t)  # the round's three update kinds, one call
+        # the round's three update kinds, one call
+        eng.apply(mask, w, gone, (new, None, nw, ns, None), now_ns=t, asynchronous=asynchronous)
         step.last_now = t  # (busy_kernel_probe ticks on at the last applied round's time)
         return t
 
@@ -293,7 +297,8 @@ def streaming_step(eng, snap, rank, n_ticks):
         eng.apportion(apply_only(), writeback=True, asynchronous=True)
 
     step.last_now = now
-    step.apply_only = apply_only  # the state a tick starts from (bench's dense share at tick time)
+    step.apply_only = apply_only
+    step.finish = eng.apply_wait if asynchronous else (lambda: None)  # the state a tick starts from (bench's dense share at tick time)
     return step
 
 
@@ -944,6 +949,9 @@ def main():
                     help="native: each step is one library call (dm_hier_step: the leaf tick, then the block "
                          "gathered by the library's own RCCL communicator and the root round on the exchange "
                          "stream); python: the same sequence from Python (torch.distributed all-gather)")
+    ap.add_argument("--c4-sync-apply", action="store_true",
+                    help="configs[4]: each round's batch through the synchronous dm_store_apply (A/B against the "
+                         "default dm_store_apply_async)")
     ap.add_argument("--lib", default=None,
                     help="A/B only: another build of the same ABI (tools/ab_libs/*.so) for every engine of the run")
     ap.add_argument("--check-corrupt", action="store_true",
@@ -1087,7 +1095,7 @@ def main():
         step = lambda: eng.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
         root = ht = None
         if args.workload == "c4":
-            step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup + 1)
+            step = streaming_step(eng, snap, rank, 2 * args.steps + args.warmup + 1, not args.c4_sync_apply)
         if hier:
             from doorman_amd.hierarchy import HierarchicalTick, root_snapshot
             root = Engine(dev_index, args.lib)
@@ -1112,6 +1120,8 @@ def main():
                           also=[root] if root is not None else [])
         run["dense_frac"] = tick_dense_fraction(eng, snap, step)
         run["last_now"] = getattr(step, "last_now", now)
+        if hasattr(step, "finish"):
+            step.finish()  # the C4 rounds' asynchronous batches: retired, none rejected
         run["parts"] = int(eng.plan_info().get("stream_parts", 1))
         if ht is not None:
             ht.sync()
@@ -1182,6 +1192,8 @@ def main():
                 stx = lambda: ex.apportion(now, writeback=True, asynchronous=True, defer_join=True)  # noqa: E731
             rx = timed_steps(torch, ex, stx, kx, args.warmup, sync_ranks, extra_warm=name != "c4")
             rx["dense_frac"] = tick_dense_fraction(ex, snapx, stx)
+            if hasattr(stx, "finish"):
+                stx.finish()
             rx["parts"] = int(ex.plan_info().get("stream_parts", 1))
             extra[name] = workload_line(name, snapx, rx, kx, single_kernel_tick=name == "c1")
             if name == "c4" and extra[name]["roofline"] is not None:

@@ -91,6 +91,8 @@ _SIGS = {
     "dm_store_upsert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5),
     "dm_store_release": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "dm_store_apply": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_store_apply_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dm_store_apply_wait": (ctypes.c_int, [ctypes.c_void_p]),
     "dm_hier_root_tick": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                          ctypes.c_void_p, ctypes.c_int]),
     "dm_host_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),

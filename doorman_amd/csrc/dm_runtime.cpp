@@ -444,13 +444,48 @@ struct dm_ctx {
   DBuf<uint64_t> st_mask;  // dm_store_update_wants_mask
   DBuf<int64_t> st_blk;
   DBuf<int32_t> st_wpre;
-  DBuf<double> st_mwants;   // dm_store_apply: the refresh part's values
-  DBuf<int64_t> st_rel;     // dm_store_apply: the departures' rows
-  DBuf<uint32_t> bat_flags; // dm_store_apply: one flags word per part
-  uint32_t* h_bat_flags = nullptr;
-  hipEvent_t ev_bat[3] = {};
   static constexpr int kWChunks = 4;  // dm_store_apply: the refresh values' copy chunks
-  hipEvent_t ev_wchunk[kWChunks] = {};
+  // One round's staging (dm_store_apply): set 0 for the synchronous call, sets 1..
+  // kAsyncSets for dm_store_apply_async, whose batch k uses set 1 + k % kAsyncSets and is
+  // retired (its flags read) before batch k + kAsyncSets reuses the set.
+  struct ApplySet {
+    DBuf<uint64_t> mask;
+    DBuf<double> mwants;  // the refresh part's values
+    DBuf<int64_t> blk;
+    DBuf<int32_t> wpre;
+    DBuf<int64_t> rel;  // the departures' rows
+    DBuf<int64_t> rows, sub, exp;
+    DBuf<double> has, wants;
+    DBuf<uint32_t> flags;  // one flags word per part
+    uint32_t* h_flags = nullptr;
+    hipEvent_t ev_bat[3] = {};
+    hipEvent_t ev_wchunk[kWChunks] = {};
+    hipEvent_t ev_done = nullptr;  // (asynchronous sets) the batch's last kernel and flags copy
+    bool pending = false;      // enqueued, not yet retired
+    bool may_general = false;  // its refresh or arrivals may bring NaN wants / other subclient counts
+    int64_t nu = 0;
+    void release() {
+      mask.release(); mwants.release(); blk.release(); wpre.release(); rel.release();
+      rows.release(); sub.release(); exp.release(); has.release(); wants.release(); flags.release();
+      if (h_flags) (void)hipHostFree(h_flags);
+      h_flags = nullptr;
+    }
+    void destroy_events() {
+      for (auto& ev : ev_bat) if (ev) { (void)hipEventDestroy(ev); ev = nullptr; }
+      for (auto& ev : ev_wchunk) if (ev) { (void)hipEventDestroy(ev); ev = nullptr; }
+      if (ev_done) (void)hipEventDestroy(ev_done);
+      ev_done = nullptr;
+    }
+  };
+  static constexpr int kAsyncSets = 2;
+  ApplySet aset[1 + kAsyncSets];
+  int64_t async_seq = 0;  // asynchronous batches enqueued
+  // a tick enqueued while an asynchronous batch that may make the store general is in flight
+  bool async_may_general() const {
+    for (int i = 1; i <= kAsyncSets; ++i)
+      if (aset[i].pending && aset[i].may_general) return true;
+    return false;
+  }
   DBuf<uint32_t> row_bits;     // device row bitmap for the uniqueness check, all-zero between calls
   DBuf<uint32_t> upd_flags;    // k_check_rows result (device)
   // dm_decide: a round's requests (grouped by resource), per-resource work items, results
@@ -648,10 +683,11 @@ struct dm_ctx {
     ph_set_ready = 0;
     glist.release(); gcount.release();
     st_rows.release(); st_sub.release(); st_exp.release(); st_has.release(); st_wants.release();
-    st_mask.release(); st_blk.release(); st_wpre.release(); st_mwants.release(); st_rel.release();
-    bat_flags.release();
-    if (h_bat_flags) (void)hipHostFree(h_bat_flags);
-    h_bat_flags = nullptr;
+    st_mask.release(); st_blk.release(); st_wpre.release();
+    for (auto& a : aset) {
+      a.release();
+      a.pending = false;
+    }
     row_bits.release(); upd_flags.release(); hier_status.release(); hier_lo.release(); pub_sync.release();
     for (int i = 0; i < kTplSlots; ++i) {
       tpl_cfg[i].release();
@@ -1087,7 +1123,7 @@ static hipError_t download(T* dst, const T* src, int64_t off, int64_t n, hipStre
 // ---------------------------------------------------------------------------
 extern "C" {
 
-const char* dm_version(void) { return "doorman-hip 0.5 (gfx950, abi 5)"; }
+const char* dm_version(void) { return "doorman-hip 0.6 (gfx950, abi 6)"; }
 
 int dm_device_count(int* out) {
   if (!out) return DM_E_INVAL;
@@ -1258,9 +1294,12 @@ int dm_create(int device, dm_ctx** out) {
   c->stream = c->own_stream;
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming);
   if (e == hipSuccess) e = xs_setup(c);
-  for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_bat[i], hipEventDisableTiming);
-  for (int i = 0; i < dm_ctx::kWChunks && e == hipSuccess; ++i)
-    e = hipEventCreateWithFlags(&c->ev_wchunk[i], hipEventDisableTiming);
+  for (auto& a : c->aset) {
+    for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&a.ev_bat[i], hipEventDisableTiming);
+    for (int i = 0; i < dm_ctx::kWChunks && e == hipSuccess; ++i)
+      e = hipEventCreateWithFlags(&a.ev_wchunk[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming);
+  }
   for (int j = 0; j < dm_ctx::kParts; ++j)
     for (int i = 0; i < dm_ctx::kTickEv && e == hipSuccess; ++i) e = hipEventCreate(&c->tick_ev[j][i]);
   if (e != hipSuccess) {
@@ -1306,10 +1345,7 @@ void dm_destroy(dm_ctx* c) {
     if (c->xs_ev[i]) (void)hipEventDestroy(c->xs_ev[i]);
   for (auto ev : c->ev_stage)
     if (ev) (void)hipEventDestroy(ev);
-  for (auto ev : c->ev_bat)
-    if (ev) (void)hipEventDestroy(ev);
-  for (auto ev : c->ev_wchunk)
-    if (ev) (void)hipEventDestroy(ev);
+  for (auto& a : c->aset) a.destroy_events();
   for (auto& row : c->tick_ev)
     for (auto ev : row)
       if (ev) (void)hipEventDestroy(ev);
@@ -1353,8 +1389,19 @@ int dm_sync(dm_ctx* c) {
   return rc;
 }
 
+// Asynchronous store batches still in flight finish before the store or its
+// configuration is replaced (their outcome is dropped with the store they updated).
+static void async_drain(dm_ctx* c) {
+  for (int i = 1; i <= dm_ctx::kAsyncSets; ++i)
+    if (c->aset[i].pending) {
+      (void)hipEventSynchronize(c->aset[i].ev_done);
+      c->aset[i].pending = false;
+    }
+}
+
 int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
   DM_ENTER(c);
+  async_drain(c);
   if (!s || s->n_resources < 0 || s->n_leases < 0 || !s->seg_off) return c->fail(DM_E_INVAL, "bad snapshot");
   const int64_t R = s->n_resources, N = s->n_leases;
   if (R > INT32_MAX - 1) return c->fail(DM_E_INVAL, "too many resources for one context (max 2^31-2)");
@@ -1451,6 +1498,7 @@ int dm_store_load(dm_ctx* c, const dm_snapshot* s) {
 
 int dm_config_load(dm_ctx* c, int64_t R, const dm_resource_cfg* cfg) {
   DM_ENTER(c);
+  async_drain(c);  // (an in-flight batch's arrivals take the lease lengths they were sent under)
   c->rows_changed();
   if (!cfg || R < 0 || !cfg->kind || !cfg->capacity || !cfg->lease_length_s || !cfg->refresh_interval_s ||
       !cfg->learning_end_ns || !cfg->parent_expiry_ns || !cfg->safe_capacity)
@@ -1699,7 +1747,8 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   // The speculative large chain (below) writes its gets before they are verified, so a
   // tick that may take it writes the alternate column whatever the store's size.
   const bool spec_eligible = c->spec_chain && wb && !(flags & DM_AGG_RECOMPUTE) && !c->expl_rows &&
-                             !(c->maybe_general && c->n_nonsmall > 0) && !c->h_chunks.empty();
+                             !((c->maybe_general || c->async_may_general()) && c->n_nonsmall > 0) &&
+                             !c->h_chunks.empty();
   const bool pingpong = wb && !(flags & DM_WB_INPLACE) &&
                         ((flags & DM_WB_ALTERNATE) || c->N * 48 > kStreamBytes || spec_eligible);
   // A writeback tick writes no per-lease expiry: the leases it grants follow their
@@ -1751,7 +1800,9 @@ int dm_apportion(dm_ctx* c, int64_t now_ns, uint32_t flags) {
   const int nch = (int)c->h_chunks.size();
   int32_t* gl = c->glist.p;
   int32_t* gc = c->gcount.p;
-  const bool general = c->maybe_general && c->n_nonsmall > 0;
+  // (an asynchronous store batch still in flight may bring NaN wants or other subclient
+  // counts: the tick is ready for k_general until the batch is retired)
+  const bool general = (c->maybe_general || c->async_may_general()) && c->n_nonsmall > 0;
   if (general) {  // only non-small resources are ever appended to the worklist
     DM_HIP(c, hipMemsetAsync(gc, 0, sizeof(int32_t), st), "worklist reset");
     c->main_dirty = true;
@@ -2521,9 +2572,7 @@ int dm_store_release(dm_ctx* c, int64_t n, const int64_t* rows) {
 // columns have landed (overlapping the later parts' copies), in the order refresh,
 // departures, arrivals.  A part whose validation fails is not applied, nor is any
 // later part (k_carry_reject); earlier parts stay applied.
-int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
-  DM_ENTER(c);
-  DM_STORE_OK(c);
+static int batch_args(dm_ctx* c, const dm_store_batch* b) {
   if (!c->store_loaded) return c->fail(DM_E_STATE, "no store loaded");
   if (!b) return c->fail(DM_E_INVAL, "null batch");
   const int64_t nw = b->wants_nwords, nm = b->wants_n, nr = b->release_n, nu = b->upsert_n;
@@ -2544,112 +2593,123 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     return c->fail(DM_E_STATE, "arrivals without expiries take the resource's lease length: load a configuration");
   if (nu > 0 && !b->upsert_expiry_ns && b->upsert_now_ns <= 0)  // an unset clock would insert lapsed leases
     return c->fail(DM_E_INVAL, "arrivals without expiries need upsert_now_ns (> 0): their expiry is now + lease length");
-  if (nw == 0 && nr == 0 && nu == 0) return DM_OK;
+  return DM_OK;
+}
+
+// The batch's copies (copy stream), its three parts' kernels (context stream) and the
+// flags' copy back into S.h_flags; nothing waits for them here.
+static int apply_enqueue(dm_ctx* c, const dm_store_batch* b, dm_ctx::ApplySet& S) {
+  const int64_t nw = b->wants_nwords, nm = b->wants_n, nr = b->release_n, nu = b->upsert_n;
+  const bool sub32 = b->upsert_subclients32 != nullptr;
   if (nu > 0) c->expl_rows = true;  // arrivals take explicit expiries
   if (nu > 0 || nr > 0) c->chain_live_ok = false;  // subclients words written, rows released
   c->rows_changed();  // (wants refreshes too: a NaN wants ends a resource's dense state)
+  S.nu = nu;
   hipStream_t st = c->stream, cp = c->cpy;
-  if (!c->bat_flags.p) {
-    DM_HIP(c, c->bat_flags.ensure(3), "batch flags");
-    DM_HIP(c, hipHostMalloc((void**)&c->h_bat_flags, 3 * sizeof(uint32_t), hipHostMallocDefault), "batch flags");
+  if (!S.flags.p) {
+    DM_HIP(c, S.flags.ensure(3), "batch flags");
+    DM_HIP(c, hipHostMalloc((void**)&S.h_flags, 3 * sizeof(uint32_t), hipHostMallocDefault), "batch flags");
   }
   if (!c->row_bits.p || c->row_bits.n < (size_t)(c->N / 32 + 1)) {
     DM_HIP(c, c->row_bits.ensure((size_t)(c->N / 32 + 1)), "row bitmap");
     DM_HIP(c, hipMemsetAsync(c->row_bits.p, 0, c->row_bits.n * sizeof(uint32_t), st), "row bitmap");
   }
-  DM_HIP(c, hipMemsetAsync(c->bat_flags.p, 0, 3 * sizeof(uint32_t), st), "batch flags");
-  uint32_t* F = c->bat_flags.p;
+  DM_HIP(c, hipMemsetAsync(S.flags.p, 0, 3 * sizeof(uint32_t), st), "batch flags");
+  uint32_t* F = S.flags.p;
   // the refresh's packed values cross in up to kWChunks chunks of >= 2^21 values
   const int nchunk = nw > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(dm_ctx::kWChunks, nm >> 21)) : 0;
   // copies, back to back
   if (nw > 0) {
-    DM_HIP(c, c->st_mask.ensure((size_t)nw), "stage mask");
-    DM_HIP(c, c->st_mwants.ensure((size_t)std::max<int64_t>(nm, 1)), "stage wants");
-    DM_HIP(c, c->st_blk.ensure((size_t)((nw + 255) / 256)), "stage block sums");
-    DM_HIP(c, c->st_wpre.ensure((size_t)nw), "stage word offsets");
-    DM_HIP(c, hipMemcpyAsync(c->st_mask.p, b->wants_mask, (size_t)nw * 8, hipMemcpyHostToDevice, cp), "stage mask");
-    DM_HIP(c, hipEventRecord(c->ev_bat[0], cp), "stage");
+    DM_HIP(c, S.mask.ensure((size_t)nw), "stage mask");
+    DM_HIP(c, S.mwants.ensure((size_t)std::max<int64_t>(nm, 1)), "stage wants");
+    DM_HIP(c, S.blk.ensure((size_t)((nw + 255) / 256)), "stage block sums");
+    DM_HIP(c, S.wpre.ensure((size_t)nw), "stage word offsets");
+    DM_HIP(c, hipMemcpyAsync(S.mask.p, b->wants_mask, (size_t)nw * 8, hipMemcpyHostToDevice, cp), "stage mask");
+    DM_HIP(c, hipEventRecord(S.ev_bat[0], cp), "stage");
     // the packed values in chunks, each applied as soon as it has landed (the apply
     // of one chunk overlaps the next one's copy): C4 3.2 -> ~3.0 ms per step
     for (int k = 0; k < nchunk; ++k) {
       const int64_t v0 = nm * k / nchunk, v1 = nm * (k + 1) / nchunk;
       if (v1 > v0)
-        DM_HIP(c, hipMemcpyAsync(c->st_mwants.p + v0, b->wants + v0, (size_t)(v1 - v0) * 8, hipMemcpyHostToDevice, cp),
+        DM_HIP(c, hipMemcpyAsync(S.mwants.p + v0, b->wants + v0, (size_t)(v1 - v0) * 8, hipMemcpyHostToDevice, cp),
                "stage wants");
-      DM_HIP(c, hipEventRecord(c->ev_wchunk[k], cp), "stage");
+      DM_HIP(c, hipEventRecord(S.ev_wchunk[k], cp), "stage");
     }
   }
   if (nr > 0) {
-    DM_HIP(c, c->st_rel.ensure((size_t)nr), "stage release rows");
-    DM_HIP(c, hipMemcpyAsync(c->st_rel.p, b->release_rows, (size_t)nr * 8, hipMemcpyHostToDevice, cp), "stage rows");
-    DM_HIP(c, hipEventRecord(c->ev_bat[1], cp), "stage");
+    DM_HIP(c, S.rel.ensure((size_t)nr), "stage release rows");
+    DM_HIP(c, hipMemcpyAsync(S.rel.p, b->release_rows, (size_t)nr * 8, hipMemcpyHostToDevice, cp), "stage rows");
+    DM_HIP(c, hipEventRecord(S.ev_bat[1], cp), "stage");
   }
   if (nu > 0) {
-    DM_HIP(c, c->st_rows.ensure((size_t)nu), "stage rows");
-    DM_HIP(c, c->st_has.ensure((size_t)nu), "stage has");
-    DM_HIP(c, c->st_wants.ensure((size_t)nu), "stage wants");
-    DM_HIP(c, c->st_sub.ensure((size_t)nu), "stage sub");
-    DM_HIP(c, c->st_exp.ensure((size_t)nu), "stage expiry");
-    const StageCol cols[] = {{c->st_rows.p, b->upsert_rows, 8},
-                             {c->st_wants.p, b->upsert_wants, 8},
-                             {c->st_sub.p, sub32 ? (const void*)b->upsert_subclients32 : b->upsert_subclients, sub32 ? 4u : 8u},
-                             {c->st_has.p, b->upsert_has, 8},
-                             {c->st_exp.p, b->upsert_expiry_ns, 8}};
+    DM_HIP(c, S.rows.ensure((size_t)nu), "stage rows");
+    DM_HIP(c, S.has.ensure((size_t)nu), "stage has");
+    DM_HIP(c, S.wants.ensure((size_t)nu), "stage wants");
+    DM_HIP(c, S.sub.ensure((size_t)nu), "stage sub");
+    DM_HIP(c, S.exp.ensure((size_t)nu), "stage expiry");
+    const StageCol cols[] = {{S.rows.p, b->upsert_rows, 8},
+                             {S.wants.p, b->upsert_wants, 8},
+                             {S.sub.p, sub32 ? (const void*)b->upsert_subclients32 : b->upsert_subclients, sub32 ? 4u : 8u},
+                             {S.has.p, b->upsert_has, 8},
+                             {S.exp.p, b->upsert_expiry_ns, 8}};
     for (const auto& col : cols)
       if (col.src)
         DM_HIP(c, hipMemcpyAsync(col.dst, col.src, (size_t)nu * col.elem, hipMemcpyHostToDevice, cp), "stage upsert");
-    DM_HIP(c, hipEventRecord(c->ev_bat[2], cp), "stage");
+    DM_HIP(c, hipEventRecord(S.ev_bat[2], cp), "stage");
   }
   // part 1: wants refresh (validated by its count/scan passes over the mask, then
   // applied chunk by chunk as the values land)
   if (nw > 0) {
-    DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[0], 0), "stage");
-    DM_HIP(c, launch_update_wants_mask(nw, c->st_mask.p, b->wants_first_row, c->N, nm, c->st_mwants.p, c->st_blk.p,
-                                       c->st_wpre.p, c->row_index(), c->sub.p, c->wants.p, c->agg.p, F + 0, st, 0, 0, 0),
+    DM_HIP(c, hipStreamWaitEvent(st, S.ev_bat[0], 0), "stage");
+    DM_HIP(c, launch_update_wants_mask(nw, S.mask.p, b->wants_first_row, c->N, nm, S.mwants.p, S.blk.p, S.wpre.p,
+                                       c->row_index(), c->sub.p, c->wants.p, c->agg.p, F + 0, st, 0, 0, 0),
            "masked update");
     for (int k = 0; k < nchunk; ++k) {
       const int64_t v0 = nm * k / nchunk, v1 = nm * (k + 1) / nchunk;
-      DM_HIP(c, hipStreamWaitEvent(st, c->ev_wchunk[k], 0), "stage");
+      DM_HIP(c, hipStreamWaitEvent(st, S.ev_wchunk[k], 0), "stage");
       if (v1 > v0)
-        DM_HIP(c, launch_update_wants_mask(nw, c->st_mask.p, b->wants_first_row, c->N, nm, c->st_mwants.p,
-                                           c->st_blk.p, c->st_wpre.p, c->row_index(), c->sub.p, c->wants.p, c->agg.p,
-                                           F + 0, st, 1, v0, v1),
+        DM_HIP(c, launch_update_wants_mask(nw, S.mask.p, b->wants_first_row, c->N, nm, S.mwants.p, S.blk.p, S.wpre.p,
+                                           c->row_index(), c->sub.p, c->wants.p, c->agg.p, F + 0, st, 1, v0, v1),
                "masked update");
     }
   }
   // part 2: departures
   if (nr > 0) {
-    DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[1], 0), "stage");
-    DM_HIP(c, launch_check_rows(nr, c->st_rel.p, c->N, c->row_bits.p, nullptr, nullptr, nullptr, F + 1, st),
-           "check rows");
+    DM_HIP(c, hipStreamWaitEvent(st, S.ev_bat[1], 0), "stage");
+    DM_HIP(c, launch_check_rows(nr, S.rel.p, c->N, c->row_bits.p, nullptr, nullptr, nullptr, F + 1, st), "check rows");
     DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
-    DM_HIP(c, launch_release(nr, c->st_rel.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
+    DM_HIP(c, launch_release(nr, S.rel.p, c->row_index(), c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p,
                              c->expl.p, F + 1, c->dense_upd(), st),
            "release");
-    DM_HIP(c, launch_clear_rows(nr, c->st_rel.p, c->N, c->row_bits.p, st), "clear rows");
+    DM_HIP(c, launch_clear_rows(nr, S.rel.p, c->N, c->row_bits.p, st), "clear rows");
   } else {
     DM_HIP(c, launch_carry_reject(F + 0, F + 1, st), "carry");
   }
   // part 3: arrivals / full refreshes
   if (nu > 0) {
-    DM_HIP(c, hipStreamWaitEvent(st, c->ev_bat[2], 0), "stage");
-    const int64_t* s64 = sub32 ? nullptr : c->st_sub.p;
-    const int32_t* s32 = sub32 ? (const int32_t*)c->st_sub.p : nullptr;
-    DM_HIP(c, launch_check_rows(nu, c->st_rows.p, c->N, c->row_bits.p, c->st_wants.p, s64, s32, F + 2, st),
-           "check rows");
+    DM_HIP(c, hipStreamWaitEvent(st, S.ev_bat[2], 0), "stage");
+    const int64_t* s64 = sub32 ? nullptr : S.sub.p;
+    const int32_t* s32 = sub32 ? (const int32_t*)S.sub.p : nullptr;
+    DM_HIP(c, launch_check_rows(nu, S.rows.p, c->N, c->row_bits.p, S.wants.p, s64, s32, F + 2, st), "check rows");
     DM_HIP(c, launch_carry_reject(F + 1, F + 2, st), "carry");
-    DM_HIP(c, launch_upsert(nu, c->st_rows.p, b->upsert_has ? c->st_has.p : nullptr, c->st_wants.p, s64, s32,
-                            b->upsert_expiry_ns ? c->st_exp.p : nullptr, c->cfg.p, b->upsert_now_ns, c->row_index(),
+    DM_HIP(c, launch_upsert(nu, S.rows.p, b->upsert_has ? S.has.p : nullptr, S.wants.p, s64, s32,
+                            b->upsert_expiry_ns ? S.exp.p : nullptr, c->cfg.p, b->upsert_now_ns, c->row_index(),
                             c->has.p, c->wants.p, c->sub.p, c->expiry.p, c->agg.p, c->expl.p, F + 2, c->dense_upd(), st),
            "upsert");
-    DM_HIP(c, launch_clear_rows(nu, c->st_rows.p, c->N, c->row_bits.p, st), "clear rows");
+    DM_HIP(c, launch_clear_rows(nu, S.rows.p, c->N, c->row_bits.p, st), "clear rows");
   }
-  DM_HIP(c, hipMemcpyAsync(c->h_bat_flags, F, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "batch flags");
-  if (int rs = c->synced("batch")) return rs;
+  DM_HIP(c, hipMemcpyAsync(S.h_flags, F, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "batch flags");
   c->have_result = false;
-  const uint32_t f0 = c->h_bat_flags[0], f1 = c->h_bat_flags[1], f2 = c->h_bat_flags[2];
+  return DM_OK;
+}
+
+// A landed batch's flags: the first rejected part fails the call (its message names the
+// part; `late` marks an asynchronous batch reported by a later call), NaN wants or
+// other subclient counts make the store maybe-general.
+static int apply_check(dm_ctx* c, const dm_ctx::ApplySet& S, bool late) {
+  const uint32_t f0 = S.h_flags[0], f1 = S.h_flags[1], f2 = S.h_flags[2];
   auto reject = [&](uint32_t f, const char* part) -> int {
-    const std::string p(part);
+    const std::string p = std::string(late ? "an earlier asynchronous batch's " : "") + part;
     if (f & kUpdRange) return c->fail(DM_E_RANGE, p + ": row out of range");
     if (f & kUpdCount) return c->fail(DM_E_INVAL, p + ": packed values must match the mask's set bits");
     if (f & kUpdDup) return c->fail(DM_E_INVAL, p + ": rows must be unique within one part");
@@ -2660,12 +2720,66 @@ int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
     if (int rg = mark_maybe_general(c)) return rg;
   if (f1 & kUpdReject) return reject(f1, "release");
   if (f2 & kUpdReject) return reject(f2, "upsert");
-  if (nu > 0) {
+  if (S.nu > 0) {
     if ((f2 & (kUpdNaN | kUpdNotOne)) || !c->all_sub_one)
       if (int rg = mark_maybe_general(c)) return rg;
     if (f2 & kUpdNotOne) c->all_sub_one = false;
   }
   return DM_OK;
+}
+
+int dm_store_apply(dm_ctx* c, const dm_store_batch* b) {
+  DM_ENTER(c);
+  DM_STORE_OK(c);
+  if (int rc = batch_args(c, b)) return rc;
+  if (b->wants_nwords == 0 && b->release_n == 0 && b->upsert_n == 0) return DM_OK;
+  dm_ctx::ApplySet& S = c->aset[0];
+  if (int rc = apply_enqueue(c, b, S)) return rc;
+  if (int rs = c->synced("batch")) return rs;
+  return apply_check(c, S, false);
+}
+
+// Retire asynchronous set S: wait for its batch, then its flags.
+static int async_retire(dm_ctx* c, dm_ctx::ApplySet& S) {
+  if (!S.pending) return DM_OK;
+  const hipError_t e = hipEventSynchronize(S.ev_done);
+  S.pending = false;
+  if (e != hipSuccess) return c->fail(DM_E_HIP, std::string("asynchronous batch: ") + hipGetErrorString(e));
+  return apply_check(c, S, true);
+}
+
+int dm_store_apply_async(dm_ctx* c, const dm_store_batch* b) {
+  DM_ENTER(c);
+  DM_STORE_OK(c);
+  if (int rc = batch_args(c, b)) return rc;
+  if (b->wants_nwords == 0 && b->release_n == 0 && b->upsert_n == 0) return DM_OK;
+  dm_ctx::ApplySet& S = c->aset[1 + (int)(c->async_seq % dm_ctx::kAsyncSets)];
+  // the set's previous batch (kAsyncSets batches back) first: its flags, and its
+  // staging free for these copies (this wait is what keeps the host kAsyncSets
+  // batches ahead of the device at most)
+  if (int rc = async_retire(c, S)) return rc;
+  S.may_general = b->wants_nwords > 0 || b->upsert_n > 0;
+  if (int rc = apply_enqueue(c, b, S)) return rc;
+  DM_HIP(c, hipEventRecord(S.ev_done, c->stream), "batch done");
+  S.pending = true;
+  c->async_seq += 1;
+  return DM_OK;
+}
+
+int dm_store_apply_wait(dm_ctx* c) {
+  DM_ENTER(c);
+  int first = DM_OK;
+  std::string msg;
+  for (int64_t k = c->async_seq - dm_ctx::kAsyncSets; k < c->async_seq; ++k) {  // oldest first
+    if (k < 0) continue;
+    const int rc = async_retire(c, c->aset[1 + (int)(k % dm_ctx::kAsyncSets)]);
+    if (rc && first == DM_OK) {
+      first = rc;
+      msg = c->err;
+    }
+  }
+  if (first != DM_OK) c->err = msg;
+  return first;
 }
 
 int dm_host_alloc(dm_ctx* c, size_t bytes, void** out) {

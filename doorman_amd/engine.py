@@ -159,11 +159,14 @@ class Engine:
                                                      _ptr(wants)))
 
     def apply(self, wants_mask=None, wants=None, release_rows=None, upsert=None, wants_first_row: int = 0,
-              now_ns: int | None = None):
+              now_ns: int | None = None, asynchronous: bool = False):
         """dm_store_apply: one round's refresh (row mask + packed wants), departures and
         arrivals (upsert = (rows, has, wants, subclients, expiry_ns)) in one call.
         Narrow arrivals: has None (= 0), subclients as int32 (sent as 4 B), expiry_ns None
-        (= now_ns + the resource's lease length: now_ns is then required)."""
+        (= now_ns + the resource's lease length: now_ns is then required).
+        asynchronous: dm_store_apply_async -- enqueued, not waited for; the arrays are kept
+        alive here until the batch is retired (apply_wait, or two batches later), and a
+        rejected batch raises from the call that retires it."""
         if upsert is not None and upsert[4] is None and now_ns is None:
             raise ValueError("arrivals without expiries need now_ns (their expiry is now_ns + lease length)")
         keep = []
@@ -193,7 +196,21 @@ class Engine:
                 b.upsert_subclients = _ptr(col(sub, np.int64))
             b.upsert_expiry_ns = None if exp is None else _ptr(col(exp, np.int64))
             b.upsert_now_ns = int(now_ns or 0)
-        self._chk(self._L.dm_store_apply(self._ctx, ctypes.byref(b)))
+        if not asynchronous:
+            self._chk(self._L.dm_store_apply(self._ctx, ctypes.byref(b)))
+            return
+        self._chk(self._L.dm_store_apply_async(self._ctx, ctypes.byref(b)))
+        # the library reads these columns until it retires the batch (at most two
+        # batches in flight): keep the last three batches' arrays alive
+        self._async_keep = (getattr(self, "_async_keep", []) + [keep])[-3:]
+
+    def apply_wait(self):
+        """dm_store_apply_wait: retire every in-flight asynchronous batch (raises for the
+        first rejected one)."""
+        try:
+            self._chk(self._L.dm_store_apply_wait(self._ctx))
+        finally:
+            self._async_keep = []
 
     def release(self, rows):
         """Release (store.go:142-151)."""

@@ -38,7 +38,9 @@
 extern "C" {
 #endif
 
-/* 5 (round 6): dm_store_lost (the read calls work on a lost store); dm_plan_info's slot 18 is the class streams' hardware-queue assignment the
+/* 6 (round 6): dm_store_apply_async / dm_store_apply_wait (a round's store batch enqueued
+   without waiting; its outcome reported by a later call).
+   5 (round 6): dm_store_lost (the read calls work on a lost store); dm_plan_info's slot 18 is the class streams' hardware-queue assignment the
    context's queue calibration chose (-1 before it finished); returns 19.
    4 (round 5): dm_kernel_class_names, dm_hier_comm_info; dm_plan_info's slot 14 is the
    redo's co-resident workgroup bound (was the per-chunk redo's chunk bound), slot 15
@@ -46,7 +48,7 @@ extern "C" {
    record 0 holds two 32-bit flags words (their OR is the request's flags); the DM_*
    environment switches other than the test hooks are gone.  3 (round 4): dm_hier_attach / dm_hier_step / dm_rccl_unique_id /
    dm_hier_comm_init and DM_E_INTERNAL added, dm_set_large_path and DM_LARGE_* removed. */
-#define DM_ABI_VERSION 5
+#define DM_ABI_VERSION 6
 
 /* return codes */
 #define DM_OK 0
@@ -198,6 +200,24 @@ int dm_store_release(dm_ctx* ctx, int64_t n, const int64_t* rows);
    in order; the first rejected part returns its error, earlier parts stay applied
    and later ones are not applied.  Synchronous on return, like the single calls. */
 int dm_store_apply(dm_ctx* ctx, const dm_store_batch* batch);
+/* dm_store_apply without waiting: the batch's copies and kernels are enqueued (ordered
+   after the context's earlier work, before its later ticks) and the call returns.  The
+   batch's host columns must stay unchanged until the batch is retired: by
+   dm_store_apply_wait, or by the dm_store_apply_async call two batches later, which
+   first waits for it (so the host runs at most two batches ahead of the device).  A
+   retired batch that was rejected fails that retiring call (DM_E_RANGE / DM_E_INVAL,
+   the message naming "an earlier asynchronous batch" and its part), and the retiring
+   dm_store_apply_async then enqueues nothing; as with dm_store_apply, the rejected part
+   and the batch's later parts are not applied, its earlier parts are, and so is every
+   batch enqueued after it.  While a batch with a refresh or arrivals is in flight, ticks
+   are prepared for heterogeneous subclients (k_general) as for a maybe-general store.
+   dm_store_load and dm_config_load wait for in-flight batches first (their outcome is
+   dropped).  The C4 streaming round: its PCIe copies back to back from round to round
+   (DESIGN.md §5). */
+int dm_store_apply_async(dm_ctx* ctx, const dm_store_batch* batch);
+/* Retire every in-flight dm_store_apply_async batch, oldest first; returns the first
+   failure (DM_OK if none). */
+int dm_store_apply_wait(dm_ctx* ctx);
 /* The three update calls validate on the device (rows in [0, N), unique within the
  * call, subclients in [0, 2^31 - 1)); a rejected call (DM_E_RANGE / DM_E_INVAL) leaves the
  * store untouched.  They return after the update is applied, so the caller may reuse

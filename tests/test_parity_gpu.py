@@ -846,6 +846,94 @@ def test_store_apply_stops_at_the_first_rejected_part(eng):
         assert st[k].tobytes() == before[k].tobytes(), k
 
 
+def test_c4_rounds_async_back_to_back(eng):
+    """bench.py's C4 step with nothing read in between: five rounds of
+    dm_store_apply_async + an asynchronous writeback tick enqueued back to back (two
+    batches in flight, each batch's copies overlapping the tick before it), then the
+    store and the last tick's leases those of the same rounds through the synchronous
+    dm_store_apply on another context: wants, subclients, expiries and the running
+    Count bit for bit; has, gets and the running sums within 1e-12 of capacity (the
+    sums' updates are atomic adds, so their rounding order differs between contexts)."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(405)
+    snap = _c4_store(rng, 2000, 300)
+    host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in snap.items()}
+    so = snap["seg_off"]
+    rounds, now = [], NOW
+    for _ in range(5):
+        now += 5 * W.NS
+        mask, w, gone, new, nh, nw, ns, ne, upd = _c4_round(rng, host, now)
+        ne = now + snap["lease_length_s"][np.searchsorted(so, new, side="right") - 1] * W.NS
+        _apply_host(host, upd, w, gone, new, nh, nw, ns, ne)
+        rounds.append((mask, w, gone, (new, None, nw, ns.astype(np.int32), None), now))
+    other = Engine(0)
+    try:
+        eng.load(snap)
+        other.load(snap)
+        for mask, w, gone, ups, t in rounds:
+            eng.apply(mask, w, gone, ups, now_ns=t, asynchronous=True)
+            eng.apportion(t, writeback=True, asynchronous=True)
+            other.apply(mask, w, gone, ups, now_ns=t)
+            other.apportion(t, writeback=True)
+        eng.apply_wait()
+        s1, s2 = eng.read_store(), other.read_store()
+        for k in ("wants", "subclients", "expiry_ns"):
+            assert s1[k].tobytes() == s2[k].tobytes(), k
+        cap_row = np.repeat(np.maximum(snap["capacity"], 1.0), np.diff(so))
+        assert float_close(s1["has"], s2["has"], cap_row, 1e-12).all()
+        r1, r2 = eng.resources(safe=False), other.resources(safe=False)
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        for k in ("sum_has", "sum_wants"):
+            assert float_close(r1[k], r2[k], np.maximum(snap["capacity"], 1.0), 1e-12).all(), k
+        g1, e1 = eng.leases()
+        g2, e2 = other.leases()
+        assert e1.tobytes() == e2.tobytes()
+        assert float_close(g1, g2, cap_row, 1e-12).all()
+    finally:
+        other.close()
+
+
+def test_store_apply_async_reports_a_rejected_batch_later(eng):
+    """dm_store_apply_async: a batch with a rejected part (duplicate departure rows) is
+    enqueued without an error; the call that retires it (apply_wait) raises, naming the
+    earlier asynchronous batch and its part.  The store then holds what dm_store_apply
+    leaves for the same batch (its refresh, no departure, no arrival) plus a valid batch
+    enqueued after it (rows bit for bit, sums within 1e-12); a clean batch retires
+    without an error."""
+    from doorman_amd._lib import DM_E_INVAL, DmError
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(42)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=False), expired_frac=0.0)
+    N = len(snap["wants"])
+    upd, w, gone, ups = _round_parts(rng, snap)
+    upd2 = np.setdiff1d(np.arange(0, N, 7), np.concatenate([gone, ups[0]]))
+    w2 = rng.uniform(0.5, 1.5, len(upd2))
+    other = Engine(0)
+    try:
+        eng.load(snap)
+        other.load(snap)
+        eng.apply(W.rows_to_mask(upd, N), w, np.concatenate([gone, gone[:1]]), ups, asynchronous=True)
+        eng.apply(W.rows_to_mask(upd2, N), w2, asynchronous=True)  # a valid batch after it
+        with pytest.raises(DmError) as e:
+            eng.apply_wait()
+        assert e.value.code == DM_E_INVAL and "earlier asynchronous batch" in str(e.value)
+        assert "release" in str(e.value)
+        with pytest.raises(DmError):
+            other.apply(W.rows_to_mask(upd, N), w, np.concatenate([gone, gone[:1]]), ups)
+        other.apply(W.rows_to_mask(upd2, N), w2)
+        s1, s2 = eng.read_store(), other.read_store()
+        for k in ("has", "wants", "subclients", "expiry_ns"):
+            assert s1[k].tobytes() == s2[k].tobytes(), k
+        r1, r2 = eng.resources(safe=False), other.resources(safe=False)
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        for k in ("sum_has", "sum_wants"):  # (atomic adds: the rounding order may differ)
+            assert float_close(r1[k], r2[k], np.maximum(snap["capacity"], 1.0), 1e-12).all(), k
+        eng.apply(W.rows_to_mask(upd2, N), w2, asynchronous=True)
+        eng.apply_wait()  # nothing rejected
+    finally:
+        other.close()
+
+
 @pytest.mark.parametrize("cols", ["inplace", "alternate"])
 def test_follower_expiry_encoding(eng, cols):
     """A writeback tick leaves every lease a follower of its resource's expiry (only
@@ -1107,8 +1195,9 @@ def _writeback_host(host, ref):
     host["expiry_ns"] = ref["expiry_ns"].copy()
 
 
-@pytest.mark.parametrize("cols,narrow", [("inplace", False), ("alternate", False), ("inplace", True)])
-def test_c4_loop_store_apply_matches_oracle(eng, cols, narrow):
+@pytest.mark.parametrize("cols,narrow,asynchronous", [("inplace", False, False), ("alternate", False, False),
+                                                      ("inplace", True, False), ("alternate", True, True)])
+def test_c4_loop_store_apply_matches_oracle(eng, cols, narrow, asynchronous):
     """configs[4]'s own loop under the oracle.  Every 5-s round the bench's
     update call -- dm_store_apply with the wants refresh as a row mask, departures and
     arrivals -- then a writeback tick; 5% learning resources, leases that lapse
@@ -1117,7 +1206,10 @@ def test_c4_loop_store_apply_matches_oracle(eng, cols, narrow):
     every round (store.go:142-181, resource.go:108-111) from exact sums while the
     device uses its running sums.  narrow: the arrivals as bench.py sends them -- row,
     wants, int32 subclients, has and expiry implied (0 and now + the resource's lease
-    length, the Assign of a new client)."""
+    length, the Assign of a new client).  asynchronous: each round's batch through
+    dm_store_apply_async and the tick enqueued behind it, as bench.py's C4 step (the
+    store's sums read back every other round; test_c4_rounds_async_back_to_back below
+    keeps several rounds in flight)."""
     rng = np.random.default_rng(404)
     snap = _c4_store(rng, 2000, 300)
     eng.load(snap)
@@ -1130,20 +1222,23 @@ def test_c4_loop_store_apply_matches_oracle(eng, cols, narrow):
         if narrow:
             so = snap["seg_off"]
             ne = now + snap["lease_length_s"][np.searchsorted(so, new, side="right") - 1] * W.NS
-            eng.apply(mask, w, gone, (new, None, nw, ns.astype(np.int32), None), now_ns=now)
+            eng.apply(mask, w, gone, (new, None, nw, ns.astype(np.int32), None), now_ns=now, asynchronous=asynchronous)
         else:
-            eng.apply(mask, w, gone, (new, nh, nw, ns, ne))
+            eng.apply(mask, w, gone, (new, nh, nw, ns, ne), asynchronous=asynchronous)
         _apply_host(host, upd, w, gone, new, nh, nw, ns, ne)
-        res = eng.resources(safe=False)
-        np.testing.assert_array_equal(res["count"], host["agg_count"])  # the running Count, exact
-        assert float_close(res["sum_wants"], host["agg_sum_wants"], np.maximum(snap["capacity"], 1.0)).all()
-        eng.apportion(now, writeback=True, wb_columns=cols)
+        if not asynchronous or rnd % 2 == 0:
+            res = eng.resources(safe=False)
+            np.testing.assert_array_equal(res["count"], host["agg_count"])  # the running Count, exact
+            assert float_close(res["sum_wants"], host["agg_sum_wants"], np.maximum(snap["capacity"], 1.0)).all()
+        eng.apportion(now, writeback=True, wb_columns=cols, asynchronous=asynchronous)
         gets, exp = eng.leases()
         ref = O.apportion(host, now)
         assert_leases_match(host, gets, exp, ref, f"C4 loop round {rnd}")
         released_by_clean += int(((host["expiry_ns"] != W.RELEASED) & (ref["expiry_ns"] == W.RELEASED)).sum())
         _writeback_host(host, ref)
     assert released_by_clean > 0  # Clean released leases during the loop
+    if asynchronous:
+        eng.apply_wait()
     st = eng.read_store()
     for k in ("subclients", "expiry_ns"):
         np.testing.assert_array_equal(st[k], host[k])
@@ -1205,8 +1300,8 @@ def test_dense_state_survives_releases_and_arrivals(eng, n, R, fs_only):
 
 def test_c4_full_size_properties_after_bench_rounds(eng):
     """configs[4] at full per-GPU size (125M leases, bench.make_workload("c4")):
-    three of the bench's own rounds (bench.streaming_step: dm_store_apply + writeback
-    tick), then size-independent properties over every resource: the running Count
+    three of the bench's own rounds (bench.streaming_step: dm_store_apply_async +
+    writeback tick, enqueued back to back), then size-independent properties over every resource: the running Count
     equals the live rows (bit-exact; every client has one subclient) and the running
     SumHas equals the sum of the live leases' gets within 1e-9 * capacity."""
     import bench
@@ -1216,6 +1311,7 @@ def test_c4_full_size_properties_after_bench_rounds(eng):
     for _ in range(3):
         step()
     eng.sync()
+    step.finish()  # the rounds' asynchronous batches retired: none rejected
     gets, exp = eng.leases()
     res = eng.resources(safe=False)
     so = snap["seg_off"]
