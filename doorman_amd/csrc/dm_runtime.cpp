@@ -2616,8 +2616,12 @@ static int apply_enqueue(dm_ctx* c, const dm_store_batch* b, dm_ctx::ApplySet& S
   }
   DM_HIP(c, hipMemsetAsync(S.flags.p, 0, 3 * sizeof(uint32_t), st), "batch flags");
   uint32_t* F = S.flags.p;
-  // the refresh's packed values cross in up to kWChunks chunks of >= 2^21 values
-  const int nchunk = nw > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(dm_ctx::kWChunks, nm >> 21)) : 0;
+  // the refresh's packed values cross in up to kWChunks chunks of >= 2^21 values, so
+  // that the synchronous call's apply overlaps its own copies; an asynchronous batch's
+  // apply overlaps the next batch's copies anyway, and one copy costs less than four
+  // (C4 2.95 -> 2.91 ms per step, alternated: tools/archive/gpu_r6_c4chunk.sh)
+  const bool sync_set = &S == &c->aset[0];
+  const int nchunk = nw == 0 ? 0 : !sync_set ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(dm_ctx::kWChunks, nm >> 21));
   // copies, back to back
   if (nw > 0) {
     DM_HIP(c, S.mask.ensure((size_t)nw), "stage mask");
