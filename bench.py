@@ -949,6 +949,9 @@ def main():
                     help="native: each step is one library call (dm_hier_step: the leaf tick, then the block "
                          "gathered by the library's own RCCL communicator and the root round on the exchange "
                          "stream); python: the same sequence from Python (torch.distributed all-gather)")
+    ap.add_argument("--no-busy-probe", action="store_true",
+                    help="configs[4]: skip roofline.busy_gpu (tools/gpu_profile.sh: the profile then holds the "
+                         "streaming step's ticks only)")
     ap.add_argument("--c4-sync-apply", action="store_true",
                     help="configs[4]: each round's batch through the synchronous dm_store_apply (A/B against the "
                          "default dm_store_apply_async)")
@@ -1161,7 +1164,7 @@ def main():
     t_max, n_total = run["t_max"], run["n_total"]
     roofline = roofline_of(args.workload, snap, run, args.steps,
                            single_kernel_tick=not hier and args.workload != "c4")
-    if args.workload == "c4" and roofline is not None:
+    if args.workload == "c4" and roofline is not None and not args.no_busy_probe:
         roofline["busy_gpu"] = busy_kernel_probe(eng, snap, run["last_now"], run["dense_frac"])
     now = W.NOW_NS
 

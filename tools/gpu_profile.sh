@@ -13,7 +13,7 @@ rm -rf $OUT; mkdir -p $OUT
 run() {  # $1 = tag, rest = rocprofv3 args before --
   local tag=$1; shift
   timeout -k 10 600 rocprofv3 "$@" --output-format csv -d $OUT/$tag -o run -- \
-    python3 bench.py --steps $STEPS --warmup 3 --workload $W --no-cpu-baseline --no-extra > $OUT/$tag.log 2>&1
+    python3 bench.py --steps $STEPS --warmup 3 --workload $W --no-cpu-baseline --no-extra --no-busy-probe > $OUT/$tag.log 2>&1
   local s=$?
   if [ $s -ne 0 ]; then echo "STOP: $tag status $s"; tail -5 $OUT/$tag.log; exit $s; fi
 }
