@@ -893,6 +893,49 @@ def test_c4_rounds_async_back_to_back(eng):
         other.close()
 
 
+def test_store_apply_async_between_synchronous_calls_and_a_reload(eng):
+    """Asynchronous batches interleaved with the synchronous update calls (which stage
+    through their own buffers, stream-ordered after the batches) leave the store those
+    calls leave in the same order on another context; a store load while a batch is in
+    flight waits for it and then holds exactly the new snapshot."""
+    from doorman_amd.engine import Engine
+    rng = np.random.default_rng(44)
+    snap = snapshot_with_sizes(rng, binned_sizes(rng, large=False), expired_frac=0.0)
+    N = len(snap["wants"])
+    upd, w, gone, ups = _round_parts(rng, snap)
+    used = np.concatenate([upd, gone, ups[0]])
+    extra = np.setdiff1d(np.arange(1, N, 5), used)[:2000]
+    w_extra = rng.uniform(0.5, 1.5, len(extra))
+    upd2 = np.setdiff1d(np.arange(2, N, 9), np.concatenate([used, extra]))
+    w2 = rng.uniform(0.5, 1.5, len(upd2))
+    other = Engine(0)
+    try:
+        eng.load(snap)
+        other.load(snap)
+        eng.apply(W.rows_to_mask(upd, N), w, gone, ups, asynchronous=True)
+        eng.update_wants(extra, w_extra)
+        eng.apply(W.rows_to_mask(upd2, N), w2, asynchronous=True)
+        other.apply(W.rows_to_mask(upd, N), w, gone, ups)
+        other.update_wants(extra, w_extra)
+        other.apply(W.rows_to_mask(upd2, N), w2)
+        s1, s2 = eng.read_store(), other.read_store()
+        for k in ("has", "wants", "subclients", "expiry_ns"):
+            assert s1[k].tobytes() == s2[k].tobytes(), k
+        r1, r2 = eng.resources(safe=False), other.resources(safe=False)
+        np.testing.assert_array_equal(r1["count"], r2["count"])
+        for k in ("sum_has", "sum_wants"):
+            assert float_close(r1[k], r2[k], np.maximum(snap["capacity"], 1.0), 1e-12).all(), k
+        eng.apply_wait()
+        eng.apply(W.rows_to_mask(upd, N), w, gone, ups, asynchronous=True)
+        eng.load(snap)  # waits for the batch, then replaces the store
+        st = eng.read_store()
+        for k in ("wants", "has"):
+            assert st[k].tobytes() == np.asarray(snap[k], np.float64).tobytes(), k
+        eng.apply_wait()  # nothing left in flight
+    finally:
+        other.close()
+
+
 def test_store_apply_async_reports_a_rejected_batch_later(eng):
     """dm_store_apply_async: a batch with a rejected part (duplicate departure rows) is
     enqueued without an error; the call that retires it (apply_wait) raises, naming the
