@@ -763,11 +763,11 @@ def busy_kernel_probe(eng, snap, now, dense_frac, ticks=20, warm_s=0.3):
     """configs[4]'s tick kernel with the GPU kept busy: after the timed streaming
     rounds, the same store ticked back to back at the last round's time with no
     update between (~0.3 s first, as timed_steps' warm-up), HIP events around every
-    launch.  In the streaming step the GPU's compute idles through the PCIe-bound
-    apply (~80 % of the step) and the tick starts from that idle state: the same
-    kernel on the same store runs 15-20 % slower there (tools/c4_variants.py: C3's
-    kernel after 4 ticks 516 us, after 0.3 s 416 us on one box).  Reported beside
-    the step's own roofline, never in its place."""
+    launch.  The same kernel on the same store runs 15-20 % faster after sustained
+    back-to-back ticks than inside the streaming step (tools/c4_variants.py: C3's
+    kernel after 4 ticks 516 us, after 0.3 s 416 us on one box; not the compute clock:
+    profiles/r06_c4_variants.md).  Reported beside the step's own roofline, never in
+    its place."""
     t_w = time.perf_counter()
     n = 0
     while time.perf_counter() - t_w < warm_s:
@@ -791,8 +791,8 @@ def busy_kernel_probe(eng, snap, now, dense_frac, ticks=20, warm_s=0.3):
     return {"kernel": name, "ticks": ticks, "warm_ticks": n, "avg_launch_us": round(avg_s * 1e6, 2),
             "achieved": round(alg / avg_s / 1e9, 1), "frac": round(alg / avg_s / 1e9 / HBM_PEAK_GBS, 4),
             "note": "the same kernel and store after the timed rounds, ticked back to back with no PCIe update "
-                    "between (the GPU busy); the step's roofline above is the kernel as the streaming step "
-                    "runs it, starting from the idle GPU of the apply"}
+                    "between; the step's roofline above is the kernel as the streaming step runs it, between "
+                    "the rounds' store updates"}
 
 
 def workload_line(name, snap, run, steps, single_kernel_tick):

@@ -5,7 +5,10 @@ batches (bench.streaming_step), the tick's kernel time (HIP events) under varian
   sync       the same, with a sync after each tick (no overlap with the next apply)
   none       no updates at all, synced ticks
   none_async no updates, back-to-back asynchronous ticks
-usage: python tools/c4_probe.py [rounds]"""
+  heater     the bench's step while a side stream keeps the GPU busy (one spinning
+             kernel, torch.cuda._sleep): the clock state without the idle gaps, the store
+             updates unchanged
+usage: python tools/c4_probe.py [rounds] [variant ...]"""
 import json
 import os
 import sys
@@ -22,9 +25,10 @@ from doorman_amd import workloads as W  # noqa: E402
 from doorman_amd.engine import Engine  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+variants = sys.argv[2:] or ["fresh", "none_async", "reloaded"]
 snap = bench.make_workload("c4", 0)
 out = {}
-for variant in ("fresh", "none_async", "reloaded"):
+for variant in variants:
     eng = Engine(0)
     eng.load(snap)
     step = bench.streaming_step(eng, snap, 0, 2 * rounds + 8)
@@ -32,6 +36,7 @@ for variant in ("fresh", "none_async", "reloaded"):
         for _ in range(3):
             step()
         eng.sync()
+        step.finish()
     if variant == "reloaded":  # the state after the rounds, loaded again into a fresh store
         st, rs = eng.read_store(), eng.resources(safe=False)
         s2 = dict(snap)
@@ -44,11 +49,17 @@ for variant in ("fresh", "none_async", "reloaded"):
         for _ in range(3):
             eng.apportion(W.NOW_NS + 3 * 5 * W.NS, writeback=True)
     t = W.NOW_NS + 3 * 5 * W.NS
+    heat = None
+    if variant == "heater":  # one spinning kernel on a side stream through the rounds
+        hs = torch.cuda.Stream()
+        heat = True
+        with torch.cuda.stream(hs):
+            torch.cuda._sleep(int(2.4e9 * 0.005 * rounds))
     eng.set_profiling(True)
     eng.reset_kernel_times()
     t0 = time.perf_counter()
     for _ in range(rounds):
-        if variant == "bench":
+        if variant in ("bench", "heater"):
             step()
         elif variant == "none":
             t += 5 * W.NS
@@ -60,8 +71,11 @@ for variant in ("fresh", "none_async", "reloaded"):
             t = step.apply_only()
             eng.apportion(t, writeback=True)
     eng.sync()
+    step.finish()
+    if heat is not None:
+        torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / rounds
     kt = {k: round(v[1] / max(v[0], 1) * 1e3, 2) for k, v in eng.kernel_times().items()}
-    out[variant] = {"round_ms": round(dt * 1e3, 3), "kernels": kt, "dense": eng.store_stats()["dense_leases"]}
+    out[variant + ("" if variant not in out else "_2")] = {"round_ms": round(dt * 1e3, 3), "kernels": kt, "dense": eng.store_stats()["dense_leases"]}
     eng.close()
 print(json.dumps(out), flush=True)
