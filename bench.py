@@ -765,9 +765,9 @@ def busy_kernel_probe(eng, snap, now, dense_frac, ticks=20, warm_s=0.3):
     update between (~0.3 s first, as timed_steps' warm-up), HIP events around every
     launch.  The same kernel on the same store runs 15-20 % faster after sustained
     back-to-back ticks than inside the streaming step (tools/c4_variants.py: C3's
-    kernel after 4 ticks 516 us, after 0.3 s 416 us on one box; not the compute clock:
-    profiles/r06_c4_variants.md).  Reported beside the step's own roofline, never in
-    its place."""
+    kernel after 4 ticks 516 us, after 0.3 s 416 us on one box; a ramp only sustained
+    memory load reaches: profiles/r06_c4_variants.md).  Reported beside the step's own
+    roofline, never in its place."""
     t_w = time.perf_counter()
     n = 0
     while time.perf_counter() - t_w < warm_s:

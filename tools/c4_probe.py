@@ -8,6 +8,8 @@ batches (bench.streaming_step), the tick's kernel time (HIP events) under varian
   heater     the bench's step while a side stream keeps the GPU busy (one spinning
              kernel, torch.cuda._sleep): the clock state without the idle gaps, the store
              updates unchanged
+  memheater  the same with 1-GiB device-to-device copies on the side stream instead
+             (HBM traffic through the rounds)
 usage: python tools/c4_probe.py [rounds] [variant ...]"""
 import json
 import os
@@ -55,11 +57,19 @@ for variant in variants:
         heat = True
         with torch.cuda.stream(hs):
             torch.cuda._sleep(int(2.4e9 * 0.005 * rounds))
+    if variant == "memheater":  # HBM traffic on a side stream: 1 GiB device copies through the rounds
+        hs = torch.cuda.Stream()
+        a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        heat = (a, b)
+        with torch.cuda.stream(hs):
+            for _ in range(rounds * 6):  # ~0.4 ms each at ~5 TB/s of read + write
+                b.copy_(a)
     eng.set_profiling(True)
     eng.reset_kernel_times()
     t0 = time.perf_counter()
     for _ in range(rounds):
-        if variant in ("bench", "heater"):
+        if variant in ("bench", "heater", "memheater"):
             step()
         elif variant == "none":
             t += 5 * W.NS

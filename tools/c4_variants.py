@@ -3,7 +3,8 @@ of C4's differences from configs[3] (mixed FS/PS kinds, 5 % learning, 2 % free s
 125M rows) costs the dense kernel its rate.  Writeback ticks back to back (as
 c4_probe's "fresh"), HIP-event kernel times.
 usage: python tools/c4_variants.py [ticks] [variant ...]   (variant: a VARIANTS key or
-bench_c3, optionally with _const: every tick at the same now; WARM=n warm-up ticks, default 4)"""
+bench_c3, optionally with _const: every tick at the same now; WARM=n warm-up ticks, default 4;
+GAP_MS=x: the GPU idle x ms after each warm-up tick)"""
 import json
 import os
 import sys
@@ -34,6 +35,7 @@ def make(free=0.02, learning=0.05, kind="mixed", R=125_000, wscale=1.0):
     return W.add_store_sums(snap)
 
 
+GAP_MS = 0.0
 VARIANTS = {
     "c4": {},
     "no_free": {"free": 0.0},
@@ -56,6 +58,8 @@ VARIANTS = {
 def main():
     ticks = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     WARM = int(os.environ.get("WARM", "4"))  # noqa: N806
+    global GAP_MS
+    GAP_MS = float(os.environ.get("GAP_MS", "0"))
     names = sys.argv[2:] or list(VARIANTS)
     for name in names:
         const = name.endswith("_const")  # every tick at the same now (as tools/c2_marginal.py)
@@ -72,7 +76,10 @@ def main():
             for i in range(WARM):  # ~0.3 s of back-to-back ticks first (bench.timed_steps' extra warm-up)
                 t += step
                 eng.apportion(t, writeback=True, asynchronous=True, defer_join=True)
-                if i % 8 == 7:
+                if GAP_MS:  # (the GPU idle between warm-up ticks: tick count without sustained load)
+                    eng.sync()
+                    time.sleep(GAP_MS / 1e3)
+                elif i % 8 == 7:
                     eng.sync()
             eng.sync()
             eng.set_profiling(True)
