@@ -330,9 +330,12 @@ struct dm_ctx {
   // forked writeback ticks (windows of kCalibWin ticks, each between joins of every
   // class stream, HIP events on the context stream), times the best kCalibFinal again
   // over longer windows, and keeps the fastest: aux[i] = aux_phys[perm[i]].
-  // (the skip: a context's first ticks run slow -- first-touch, clocks -- and would bias
-  // the candidates timed first)
-  static constexpr int kCalibSkip = 64, kCalibWin = 6, kCalibFinal = 3, kCalibWin2 = 16;
+  // (the skip: a context's first ticks run slow -- first-touch, and the GPU reaches its
+  // sustained-load operating point only after ~0.1-0.3 s of back-to-back work,
+  // profiles/r06_c4_variants.md -- which biases the candidates timed first; round 2
+  // therefore also interleaves its candidates, kCalibRep2 short windows each, and sums
+  // them, so that a drift of the clocks falls on every candidate alike)
+  static constexpr int kCalibSkip = 1024, kCalibWin = 6, kCalibFinal = 3, kCalibWin2 = 4, kCalibRep2 = 4;
   int calib = 0;  // 0 pending, 1 round 1, 2 round 2, 3 waiting for the events, 4 done / off
   int calib_skip = 0, calib_k = 0, calib_t = 0, calib_round = 0;
   int perm[kAux] = {0, 1, 2, 3};
@@ -1701,7 +1704,9 @@ static hipError_t calib_step(dm_ctx* c) {
     for (int i = 0; i < dm_ctx::kCalibFinal; ++i) fin.push_back(c->calib_cand[(size_t)c->calib_of_ev[t[(size_t)i].second]]);
     if (std::find(fin.begin(), fin.end(), ident) == fin.end()) fin.push_back(ident);
     calib_free(c);
-    c->calib_cand = fin;
+    c->calib_cand.clear();
+    for (int r = 0; r < dm_ctx::kCalibRep2; ++r)  // interleaved: fin[0], fin[1], ..., fin[0], ...
+      c->calib_cand.insert(c->calib_cand.end(), fin.begin(), fin.end());
     c->calib = 2;
     c->calib_round = 2;
     c->calib_k = 0;
@@ -1709,7 +1714,17 @@ static hipError_t calib_step(dm_ctx* c) {
     hipError_t e = calib_apply(c, c->calib_cand[0]);
     return e == hipSuccess ? calib_mark(c, false) : e;
   }
-  const std::array<int, dm_ctx::kAux> best = c->calib_cand[(size_t)c->calib_of_ev[t[0].second]];
+  // round 2: each candidate's windows summed
+  std::vector<std::pair<std::array<int, dm_ctx::kAux>, float>> sum;
+  for (const auto& pr : t) {
+    const auto& pm = c->calib_cand[(size_t)c->calib_of_ev[pr.second]];
+    auto it = std::find_if(sum.begin(), sum.end(), [&](const auto& x) { return x.first == pm; });
+    if (it == sum.end()) sum.push_back({pm, pr.first});
+    else it->second += pr.first;
+  }
+  const auto best = std::min_element(sum.begin(), sum.end(), [](const auto& a, const auto& b) {
+                      return a.second < b.second;
+                    })->first;
   calib_free(c);
   c->calib = 4;
   c->calib_best = best[0] + 4 * best[1] + 16 * best[2] + 64 * best[3];
